@@ -1,0 +1,163 @@
+// Python bindings of the native runtime (module ddlb_amd._C).
+//
+// Tensors cross the boundary as raw device pointers + the caller's HIP stream handle
+// (torch.cuda.current_stream().cuda_stream): no dependency on torch's C++ ABI, and every call is a
+// single C++ entry. Python-side wrappers (ddlb_amd/ops, ddlb_amd/parallel) validate shapes, dtypes,
+// devices and alignment BEFORE anything is launched. Symmetric buffers are exported to torch via
+// DLPack (kDLROCM) so they can be used as ordinary tensors.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <ATen/dlpack.h>
+
+#include <memory>
+
+#include "comm/comm.h"
+#include "gemm/gemm.h"
+#include "runtime/kernels.h"
+#include "runtime/plan.h"
+
+namespace py = pybind11;
+using namespace ddlb;
+
+namespace {
+
+void check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+struct DLCtx {
+  std::shared_ptr<SymmetricBuffer> owner;
+  int64_t shape[1];
+};
+
+void dl_deleter(DLManagedTensor* t) {
+  delete static_cast<DLCtx*>(t->manager_ctx);
+  delete t;
+}
+
+void capsule_destructor(PyObject* cap) {
+  if (PyCapsule_IsValid(cap, "dltensor")) {  // never consumed
+    auto* t = static_cast<DLManagedTensor*>(PyCapsule_GetPointer(cap, "dltensor"));
+    if (t && t->deleter) t->deleter(t);
+  }
+}
+
+py::object buffer_dlpack(std::shared_ptr<SymmetricBuffer> buf, int device) {
+  auto* ctx = new DLCtx{buf, {(int64_t)buf->bytes()}};
+  auto* t = new DLManagedTensor();
+  t->dl_tensor.data = (void*)buf->local();
+  t->dl_tensor.device = DLDevice{kDLROCM, device};
+  t->dl_tensor.ndim = 1;
+  t->dl_tensor.dtype = DLDataType{kDLUInt, 8, 1};
+  t->dl_tensor.shape = ctx->shape;
+  t->dl_tensor.strides = nullptr;
+  t->dl_tensor.byte_offset = 0;
+  t->manager_ctx = ctx;
+  t->deleter = dl_deleter;
+  return py::reinterpret_steal<py::object>(PyCapsule_New(t, "dltensor", capsule_destructor));
+}
+
+GemmArgs make_args(uintptr_t a, uintptr_t b, uintptr_t c, int64_t lda, int64_t ldb, int64_t ldc,
+                   int M, int N, int K, int64_t a_grp, int64_t a_gstride, int64_t c_grp,
+                   int64_t c_gstride) {
+  GemmArgs g;
+  g.a = (const void*)a; g.b = (const void*)b; g.c = (void*)c;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  g.M = M; g.N = N; g.K = K;
+  g.a_grp = a_grp; g.a_gstride = a_gstride; g.c_grp = c_grp; g.c_gstride = c_gstride;
+  return g;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "ddlb_amd native runtime: CDNA4 MFMA GEMM, RCCL/IPC data plane, plan executor";
+  m.attr("OP_WORDS") = kOpWords;
+  m.attr("MAX_REDUCE_SRC") = kMaxReduceSrc;
+  m.attr("MAX_COPY_SEG") = kMaxCopySeg;
+  m.attr("MAX_SIGNAL") = kMaxSignal;
+
+  m.def("gemm",
+        [](uintptr_t a, uintptr_t b, uintptr_t c, int64_t lda, int64_t ldb, int64_t ldc, int M,
+           int N, int K, int din, int dout, int tile, int mode, int64_t a_grp, int64_t a_gstride,
+           int64_t c_grp, int64_t c_gstride, uintptr_t stream) {
+          GemmArgs g = make_args(a, b, c, lda, ldb, ldc, M, N, K, a_grp, a_gstride, c_grp,
+                                 c_gstride);
+          check(gemm_launch(g, din, dout, tile, mode, (hipStream_t)stream), "gemm_launch");
+        },
+        py::arg("a"), py::arg("b"), py::arg("c"), py::arg("lda"), py::arg("ldb"), py::arg("ldc"),
+        py::arg("M"), py::arg("N"), py::arg("K"), py::arg("din"), py::arg("dout"),
+        py::arg("tile") = 0, py::arg("mode") = 0, py::arg("a_grp") = 0, py::arg("a_gstride") = 0,
+        py::arg("c_grp") = 0, py::arg("c_gstride") = 0, py::arg("stream") = 0);
+  m.def("gemm_fast_path_ok",
+        [](uintptr_t a, uintptr_t b, uintptr_t c, int64_t lda, int64_t ldb, int64_t ldc, int M,
+           int N, int K, int din, int dout) {
+          GemmArgs g = make_args(a, b, c, lda, ldb, ldc, M, N, K, M, M, M, M);
+          return gemm_fast_path_ok(g, din, dout);
+        });
+  m.def("choose_tile", &choose_tile);
+  m.def("tile_rows", &tile_rows);
+  m.def("tile_cols", &tile_cols);
+
+  m.def("reduce_sum",
+        [](uintptr_t dst, std::vector<uintptr_t> srcs, int64_t count, int dtype, uintptr_t s) {
+          ReduceArgs a;
+          a.dst = (void*)dst;
+          a.count = count;
+          a.nsrc = (int)srcs.size();
+          if (a.nsrc < 1 || a.nsrc > kMaxReduceSrc) throw std::runtime_error("1..16 sources");
+          for (int i = 0; i < a.nsrc; ++i) a.src[i] = (const void*)srcs[(size_t)i];
+          check(reduce_sum_launch(a, dtype, (hipStream_t)s), "reduce_sum");
+        });
+  m.def("copy",
+        [](uintptr_t dst, uintptr_t src, int64_t bytes, int max_blocks, uintptr_t s) {
+          CopyArgs a;
+          a.nseg = 1;
+          a.dst[0] = (void*)dst;
+          a.src[0] = (const void*)src;
+          a.bytes[0] = bytes;
+          check(copy_launch(a, max_blocks, (hipStream_t)s), "copy");
+        });
+  m.def("device_synchronize", []() { check(hipDeviceSynchronize(), "hipDeviceSynchronize"); });
+  m.def("get_last_error", []() { return std::string(hipGetErrorString(hipGetLastError())); });
+
+  py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
+      .def_static("unique_id", []() { return py::bytes(RcclComm::unique_id()); })
+      .def(py::init([](py::bytes uid, int nranks, int rank, int device) {
+             return std::make_shared<RcclComm>(std::string(uid), nranks, rank, device);
+           }),
+           py::call_guard<py::gil_scoped_release>())
+      .def("destroy", &RcclComm::destroy)
+      .def("async_error", &RcclComm::async_error)
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("nranks", &RcclComm::nranks);
+
+  py::class_<SymmetricBuffer, std::shared_ptr<SymmetricBuffer>>(m, "SymmetricBuffer")
+      .def(py::init<size_t, int>())
+      .def("ipc_handle", [](const SymmetricBuffer& b) { return py::bytes(b.ipc_handle()); })
+      .def("open_peers",
+           [](SymmetricBuffer& b, std::vector<py::bytes> hs, int my_rank) {
+             std::vector<std::string> v;
+             for (auto& h : hs) v.emplace_back(std::string(h));
+             b.open_peers(v, my_rank);
+           })
+      .def("close_peers", &SymmetricBuffer::close_peers)
+      .def("local", &SymmetricBuffer::local)
+      .def("peer", &SymmetricBuffer::peer)
+      .def("npeers", &SymmetricBuffer::npeers)
+      .def_property_readonly("bytes", &SymmetricBuffer::bytes);
+  m.def("buffer_dlpack", &buffer_dlpack);
+
+  py::class_<PlanExecutor, std::shared_ptr<PlanExecutor>>(m, "PlanExecutor")
+      .def(py::init<int, int, int, const std::vector<int>&>())
+      .def("load", &PlanExecutor::load)
+      .def("set_comm", [](PlanExecutor& p, std::shared_ptr<RcclComm> c) { p.set_comm(c.get()); },
+           py::keep_alive<1, 2>())
+      .def("run", &PlanExecutor::run)
+      .def("epoch", &PlanExecutor::epoch)
+      .def("nops", &PlanExecutor::nops)
+      .def("stream", &PlanExecutor::stream)
+      .def("timeout_word", &PlanExecutor::timeout_word)
+      .def("read_timeout", &PlanExecutor::read_timeout);
+}

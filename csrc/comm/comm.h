@@ -1,0 +1,69 @@
+// Native data plane: our own RCCL communicator + HIP IPC symmetric memory.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace ddlb {
+
+#define DDLB_HIP(x)                                                                       \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    if (e_ != hipSuccess)                                                                 \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(e_) + " at " + \
+                               __FILE__ + ":" + std::to_string(__LINE__) + ": " #x);      \
+  } while (0)
+#define DDLB_NCCL(x)                                                                       \
+  do {                                                                                     \
+    ncclResult_t r_ = (x);                                                                 \
+    if (r_ != ncclSuccess)                                                                 \
+      throw std::runtime_error(std::string("RCCL error ") + ncclGetErrorString(r_) + " at " + \
+                               __FILE__ + ":" + std::to_string(__LINE__) + ": " #x);       \
+  } while (0)
+
+// RCCL communicator created from a unique id that Python exchanges over the torch store, so the
+// collectives are enqueued on *our* HIP streams (not torch's internal NCCL stream).
+class RcclComm {
+ public:
+  static std::string unique_id();  // 128 raw bytes
+  RcclComm(const std::string& uid, int nranks, int rank, int device);
+  ~RcclComm();
+  void destroy();
+  ncclComm_t get() const { return comm_; }
+  int rank() const { return rank_; }
+  int nranks() const { return nranks_; }
+  std::string async_error() const;
+
+ private:
+  ncclComm_t comm_ = nullptr;
+  int rank_ = 0, nranks_ = 1;
+};
+
+ncclDataType_t nccl_dtype(int dt);  // DT_* -> ncclDataType_t
+
+// One symmetric allocation: a hipMalloc'd buffer on this device + the IPC-mapped pointers of the
+// same-named buffer on every peer (index = rank; own rank -> local pointer).
+class SymmetricBuffer {
+ public:
+  SymmetricBuffer(size_t bytes, int device);
+  ~SymmetricBuffer();
+  std::string ipc_handle() const;                       // 64 raw bytes
+  void open_peers(const std::vector<std::string>& handles, int my_rank);
+  void close_peers();
+  uintptr_t local() const { return (uintptr_t)ptr_; }
+  uintptr_t peer(int r) const { return (uintptr_t)peers_.at(r); }
+  size_t bytes() const { return bytes_; }
+  int npeers() const { return (int)peers_.size(); }
+
+ private:
+  void* ptr_ = nullptr;
+  size_t bytes_ = 0;
+  int device_ = 0;
+  std::vector<void*> peers_;
+  std::vector<bool> opened_;
+};
+
+}  // namespace ddlb

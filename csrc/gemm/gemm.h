@@ -1,0 +1,48 @@
+// Public interface of the CDNA4 MFMA GEMM (csrc/gemm/gemm_mfma.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ddlb {
+
+// dtype codes shared with Python (ddlb_amd/ops/_dtypes.py)
+enum DType : int { DT_F32 = 0, DT_F16 = 1, DT_BF16 = 2, DT_FP8 = 3, DT_F64 = 4, DT_U8 = 5 };
+inline int dtype_size(int dt) {
+  switch (dt) {
+    case DT_F32: return 4;
+    case DT_F16: case DT_BF16: return 2;
+    case DT_FP8: case DT_U8: return 1;
+    case DT_F64: return 8;
+    default: return 0;
+  }
+}
+
+enum Tile : int { TILE_AUTO = 0, TILE_256x256 = 1, TILE_256x128 = 2, TILE_128x256 = 3,
+                  TILE_128x128 = 4 };
+enum GemmMode : int { GEMM_MODE_AUTO = 0, GEMM_MODE_GENERIC = 1, GEMM_MODE_MX = 2 };
+
+// C[M,N] = A[M,K] * Bt[N,K]^T. Leading dimensions in ELEMENTS.
+// Logical row i of A (and of C) lives at physical row (i / grp) * gstride + (i % grp).
+struct GemmArgs {
+  const void* a = nullptr;
+  const void* b = nullptr;
+  void* c = nullptr;
+  int64_t lda = 0, ldb = 0, ldc = 0;
+  int64_t a_grp = 0, a_gstride = 0;  // 0 -> identity
+  int64_t c_grp = 0, c_gstride = 0;
+  int M = 0, N = 0, K = 0;
+  // Arrival-ordered consumption (p2p pipeline): optional
+  const unsigned* flags = nullptr;  // flags[shard] >= epoch once shard's A rows have landed
+  unsigned epoch = 0;
+  int64_t flag_rows = 1;            // physical A rows per shard
+  unsigned* timeout_word = nullptr; // set to 1 if a spin gave up
+  int tile_order = 0, nshards = 1, first_shard = 0;
+};
+
+hipError_t gemm_launch(const GemmArgs& p, int din, int dout, int tile, int mode, hipStream_t s);
+bool gemm_fast_path_ok(const GemmArgs& p, int din, int dout);
+int choose_tile(int64_t M, int64_t N, int din);
+int tile_rows(int tile);
+int tile_cols(int tile);
+
+}  // namespace ddlb

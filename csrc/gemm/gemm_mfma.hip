@@ -1,0 +1,558 @@
+// CDNA4 (gfx950) MFMA GEMM:  C[M,N] = A[M,K] * Bt[N,K]^T  ("TN": both operands K-contiguous).
+//
+// Replaces the cuBLAS GEMM the reference reaches through torch.matmul
+// (ddlb/primitives/TPColumnwise/pytorch.py:97, TPRowwise/pytorch.py:82, compute_only.py:40).
+//
+// Design (see /opt/skills/guides/cdna_hip_programming.md §5):
+//  * Operands staged global->LDS with LDS-DMA (`global_load_lds_dwordx4`, 16 B/lane, 1 KiB per
+//    wave-instruction), double-buffered, one barrier per K-tile (the "minimum 2-phase" schedule).
+//  * Every K-tile row is 128 bytes (BK = 64 for 16-bit types, 128 for fp8, 32 for fp32), so one
+//    LDS layout serves every dtype. 16-byte chunks are XOR-swizzled with (row>>1)&7; because the
+//    LDS-DMA destination is lane-linear, the swizzle is applied to the per-lane SOURCE address and
+//    undone on the ds_read_b128 (rule 21). Conflict-free for the 16x16 fragment reads.
+//  * MFMA 16x16x32 (bf16/f16), 2x 16x16x32 fp8 per 16 B, 4x 16x16x4 f32 per 16 B, or the
+//    block-scaled 16x16x128 f8f6f4 (MX-fp8, unit scales) that runs at 2x the bf16 rate.
+//    Any k-permutation that is identical for A and B leaves the dot product unchanged, which is
+//    what lets one 16-byte ds_read feed every instruction shape.
+//  * Operands are swapped in the MFMA (D = Bt_frag x A_frag) so each lane ends with 4 consecutive
+//    COLUMNS of one C row: the epilogue is one 8-byte (bf16) / 16-byte (f32) store per fragment.
+//  * Grouped-row addressing for A and C: logical row i lives at physical row
+//        base + (i / grp) * gstride + (i % grp)
+//    so pipeline stages read strided row blocks of A and write straight to their final rows of C
+//    (no permutation copy).
+//  * Bijective XCD-aware block remap (8 XCDs, private L2s): blocks that share an A panel land on
+//    the same XCD.
+//  * Optional arrival flags: a tile whose A rows belong to shard s spins (bounded) until
+//    flags[s] >= epoch before loading A, so one persistent-size GEMM launch can consume shards as
+//    the copy engines deliver them (p2p pipeline).
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <hip/hip_fp16.h>
+#include <stdint.h>
+
+#include "gemm.h"
+
+namespace ddlb {
+namespace {
+
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+
+#define LDS_AS __attribute__((address_space(3)))
+#define GLB_AS __attribute__((address_space(1)))
+
+__device__ __forceinline__ void glds16(const void* g, void* lds) {
+  __builtin_amdgcn_global_load_lds((const GLB_AS void*)g, (LDS_AS void*)lds, 16, 0, 0);
+}
+
+// Rows and group sizes fit in 32 bits: 32-bit unsigned division is ~10x cheaper than 64-bit.
+__device__ __forceinline__ int64_t map_row(int64_t i, int64_t grp, int64_t gstride) {
+  const unsigned ui = (unsigned)i, ug = (unsigned)grp;
+  const unsigned q = ui / ug;
+  return (int64_t)q * gstride + (int64_t)(ui - q * ug);
+}
+
+// Bijective XCD remap (guide §5, "XCD swizzle must be bijective").
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, idx = bid >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+// Block -> tile. Default: bijective XCD remap over the whole grid. With ``tile_order`` the grid
+// is dispatched shard-major (shard (first_shard + j) % nshards at dispatch position j, so the
+// tiles of the shard that arrives first run first) and XCD-remapped within each shard.
+__device__ __forceinline__ int tile_index(const GemmArgs& p, int nwg) {
+  if (!p.tile_order) return xcd_remap((int)blockIdx.x, nwg);
+  const int per = nwg / p.nshards;
+  const int j = (int)blockIdx.x / per, local = (int)blockIdx.x % per;
+  const int shard = (p.first_shard + j) % p.nshards;
+  return shard * per + xcd_remap(local, per);
+}
+
+// ---------------------------------------------------------------- MFMA "consume 16 bytes" ops
+struct MmaBF16 {
+  static constexpr int kElem = 2;
+  static __device__ __forceinline__ void step(f32x4& acc, const i32x4& b, const i32x4& a) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, b),
+                                                  __builtin_bit_cast(bf16x8, a), acc, 0, 0, 0);
+  }
+};
+struct MmaF16 {
+  static constexpr int kElem = 2;
+  static __device__ __forceinline__ void step(f32x4& acc, const i32x4& b, const i32x4& a) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, b),
+                                                 __builtin_bit_cast(f16x8, a), acc, 0, 0, 0);
+  }
+};
+struct MmaFP8 {  // OCP e4m3 x e4m3, f32 accumulate; 2 instructions per 16 B
+  static constexpr int kElem = 1;
+  static __device__ __forceinline__ void step(f32x4& acc, const i32x4& b, const i32x4& a) {
+    const long b0 = ((long)(unsigned)b.y << 32) | (unsigned)b.x;
+    const long b1 = ((long)(unsigned)b.w << 32) | (unsigned)b.z;
+    const long a0 = ((long)(unsigned)a.y << 32) | (unsigned)a.x;
+    const long a1 = ((long)(unsigned)a.w << 32) | (unsigned)a.z;
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(b0, a0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(b1, a1, acc, 0, 0, 0);
+  }
+};
+struct MmaF32 {  // exact f32 MFMA; 4 instructions per 16 B
+  static constexpr int kElem = 4;
+  static __device__ __forceinline__ void step(f32x4& acc, const i32x4& b, const i32x4& a) {
+    const f32x4 bf = __builtin_bit_cast(f32x4, b), af = __builtin_bit_cast(f32x4, a);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(bf.x, af.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(bf.y, af.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(bf.z, af.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(bf.w, af.w, acc, 0, 0, 0);
+  }
+};
+
+// ---------------------------------------------------------------- output conversion
+template <int OUT> struct Store4;
+template <> struct Store4<DT_BF16> {
+  static __device__ __forceinline__ void st(void* p, const f32x4 v) {
+    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+    bf16x4 o = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+    *(uint2*)p = __builtin_bit_cast(uint2, o);
+  }
+  static __device__ __forceinline__ void st1(void* p, float v) { *(__bf16*)p = (__bf16)v; }
+};
+template <> struct Store4<DT_F16> {
+  static __device__ __forceinline__ void st(void* p, const f32x4 v) {
+    typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
+    f16x4 o = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+    *(uint2*)p = __builtin_bit_cast(uint2, o);
+  }
+  static __device__ __forceinline__ void st1(void* p, float v) { *(_Float16*)p = (_Float16)v; }
+};
+template <> struct Store4<DT_F32> {
+  static __device__ __forceinline__ void st(void* p, const f32x4 v) { *(f32x4*)p = v; }
+  static __device__ __forceinline__ void st1(void* p, float v) { *(float*)p = v; }
+};
+
+template <int OUT> constexpr int out_size() { return OUT == DT_F32 ? 4 : 2; }
+
+// ---------------------------------------------------------------- bounded arrival spin
+__device__ __forceinline__ void wait_flag(const GemmArgs& p, int64_t row) {
+  if (p.flags == nullptr) return;
+  const int shard = (int)(row / p.flag_rows);
+  unsigned* f = const_cast<unsigned*>(p.flags) + shard;
+  if (threadIdx.x == 0) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) <
+           p.epoch) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1u << 26)) {  // ~seconds: give up, report, let the grid drain
+        if (p.timeout_word) atomicOr(p.timeout_word, 1u);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------- the tiled kernel
+template <class Mma, int OUT, int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(WM* WN * 64) void gemm_tn_kernel(const GemmArgs p) {
+  constexpr int NT = WM * WN * 64, NW = WM * WN;
+  constexpr int ROWB = 128;  // bytes per row per K-tile
+  constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, STAGE = A_BYTES + B_BYTES;
+  constexpr int TM = BM / WM, TN = BN / WN, MR = TM / 16, NR = TN / 16;
+  constexpr int LA = BM / 8 / NW, LB = BN / 8 / NW;  // LDS-DMA instructions per wave per tile
+  static_assert(LA * NW * 8 == BM && LB * NW * 8 == BN, "tile rows must split over waves");
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
+  const int nwg = tiles_m * tiles_n;
+  const int wg = tile_index(p, nwg);
+  const int tm = wg / tiles_n, tn = wg % tiles_n;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+
+  // Per-lane source pointers for the LDS-DMA rows this wave stages.
+  const int esz = Mma::kElem;
+  const char* aptr[LA];
+  const char* bptr[LB];
+#pragma unroll
+  for (int i = 0; i < LA; ++i) {
+    const int row = (wave * LA + i) * 8 + (lane >> 3);
+    int64_t gr = m0 + row;
+    gr = gr < p.M ? gr : p.M - 1;
+    const int64_t phys = map_row(gr, p.a_grp, p.a_gstride);
+    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+    aptr[i] = (const char*)p.a + phys * p.lda * esz + chunk * 16;
+  }
+#pragma unroll
+  for (int i = 0; i < LB; ++i) {
+    const int row = (wave * LB + i) * 8 + (lane >> 3);
+    int64_t gr = n0 + row;
+    gr = gr < p.N ? gr : p.N - 1;
+    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+    bptr[i] = (const char*)p.b + gr * p.ldb * esz + chunk * 16;
+  }
+
+  wait_flag(p, map_row(m0, p.a_grp, p.a_gstride));
+
+  auto stage = [&](int buf, int kt) {
+    char* base = smem + buf * STAGE;
+    const int64_t koff = (int64_t)kt * ROWB;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) glds16(aptr[i] + koff, base + (wave * LA + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < LB; ++i) glds16(bptr[i] + koff, base + A_BYTES + (wave * LB + i) * 1024);
+  };
+
+  const int wm = wave / WN, wn = wave % WN;
+  const int swz = (lane & 15) >> 1;
+  const int frow = lane & 15, fq = lane >> 4;
+  f32x4 acc[MR][NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf) {
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int c4 = 0; c4 < 8; c4 += 4) {
+      const int choff = ((c4 + fq) ^ swz) * 16;
+      i32x4 af[MR], bfr[NR];
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+        af[i] = *(const i32x4*)(As + (wm * TM + i * 16 + frow) * ROWB + choff);
+#pragma unroll
+      for (int j = 0; j < NR; ++j)
+        bfr[j] = *(const i32x4*)(Bs + (wn * TN + j * 16 + frow) * ROWB + choff);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j) Mma::step(acc[i][j], bfr[j], af[i]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  };
+
+  const int nk = p.K * esz / ROWB;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  int cur = 0;
+  for (int kt = 0; kt < nk - 1; ++kt) {
+    stage(cur ^ 1, kt + 1);
+    compute(cur);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    cur ^= 1;
+  }
+  compute(cur);
+
+  // Epilogue: lane holds C[row = .. + frow][col = .. + 4*fq + r], r = 0..3.
+  constexpr int OSZ = out_size<OUT>();
+#pragma unroll
+  for (int i = 0; i < MR; ++i) {
+    const int64_t row = m0 + wm * TM + i * 16 + frow;
+    if (row >= p.M) continue;
+    char* crow = (char*)p.c + map_row(row, p.c_grp, p.c_gstride) * p.ldc * OSZ;
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      const int64_t col = n0 + wn * TN + j * 16 + fq * 4;
+      if (col + 3 < p.N) {
+        Store4<OUT>::st(crow + col * OSZ, acc[i][j]);
+      } else {
+        const float v[4] = {acc[i][j].x, acc[i][j].y, acc[i][j].z, acc[i][j].w};
+        for (int r = 0; r < 4; ++r)
+          if (col + r < p.N) Store4<OUT>::st1(crow + (col + r) * OSZ, v[r]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- MX-fp8 (block-scaled) kernel
+// One v_mfma_scale_f32_16x16x128_f8f6f4 per 128-byte K-row (unit E8M0 scales = 127): 2x the bf16
+// MFMA rate (MI355X_MICROARCH.md "Matrix cores"). Same staging as above.
+template <int OUT, int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(WM* WN * 64) void gemm_tn_mxfp8_kernel(const GemmArgs p) {
+  constexpr int NW = WM * WN, ROWB = 128;
+  constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, STAGE = A_BYTES + B_BYTES;
+  constexpr int TM = BM / WM, TN = BN / WN, MR = TM / 16, NR = TN / 16;
+  constexpr int LA = BM / 8 / NW, LB = BN / 8 / NW;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
+  const int nwg = tiles_m * tiles_n;
+  const int wg = tile_index(p, nwg);
+  const int tm = wg / tiles_n, tn = wg % tiles_n;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const char* aptr[LA];
+  const char* bptr[LB];
+#pragma unroll
+  for (int i = 0; i < LA; ++i) {
+    const int row = (wave * LA + i) * 8 + (lane >> 3);
+    int64_t gr = m0 + row;
+    gr = gr < p.M ? gr : p.M - 1;
+    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+    aptr[i] = (const char*)p.a + map_row(gr, p.a_grp, p.a_gstride) * p.lda + chunk * 16;
+  }
+#pragma unroll
+  for (int i = 0; i < LB; ++i) {
+    const int row = (wave * LB + i) * 8 + (lane >> 3);
+    int64_t gr = n0 + row;
+    gr = gr < p.N ? gr : p.N - 1;
+    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+    bptr[i] = (const char*)p.b + gr * p.ldb + chunk * 16;
+  }
+  wait_flag(p, map_row(m0, p.a_grp, p.a_gstride));
+  auto stage = [&](int buf, int kt) {
+    char* base = smem + buf * STAGE;
+    const int64_t koff = (int64_t)kt * ROWB;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) glds16(aptr[i] + koff, base + (wave * LA + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < LB; ++i) glds16(bptr[i] + koff, base + A_BYTES + (wave * LB + i) * 1024);
+  };
+  const int wm = wave / WN, wn = wave % WN;
+  const int swz = (lane & 15) >> 1, frow = lane & 15, fq = lane >> 4;
+  f32x4 acc[MR][NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](int buf) {
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + A_BYTES;
+    const int c0 = ((fq) ^ swz) * 16, c1 = ((4 + fq) ^ swz) * 16;
+    i32x8 af[MR], bfr[NR];
+#pragma unroll
+    for (int i = 0; i < MR; ++i) {
+      const char* r = As + (wm * TM + i * 16 + frow) * ROWB;
+      const i32x4 lo = *(const i32x4*)(r + c0), hi = *(const i32x4*)(r + c1);
+      af[i] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    }
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      const char* r = Bs + (wn * TN + j * 16 + frow) * ROWB;
+      const i32x4 lo = *(const i32x4*)(r + c0), hi = *(const i32x4*)(r + c1);
+      bfr[j] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int j = 0; j < NR; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfr[j], af[i], acc[i][j], 0,
+                                                                       0, 0, 127, 0, 127);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  const int nk = p.K / ROWB;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  int cur = 0;
+  for (int kt = 0; kt < nk - 1; ++kt) {
+    stage(cur ^ 1, kt + 1);
+    compute(cur);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    cur ^= 1;
+  }
+  compute(cur);
+  constexpr int OSZ = out_size<OUT>();
+#pragma unroll
+  for (int i = 0; i < MR; ++i) {
+    const int64_t row = m0 + wm * TM + i * 16 + frow;
+    if (row >= p.M) continue;
+    char* crow = (char*)p.c + map_row(row, p.c_grp, p.c_gstride) * p.ldc * OSZ;
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      const int64_t col = n0 + wn * TN + j * 16 + fq * 4;
+      if (col + 3 < p.N) {
+        Store4<OUT>::st(crow + col * OSZ, acc[i][j]);
+      } else {
+        const float v[4] = {acc[i][j].x, acc[i][j].y, acc[i][j].z, acc[i][j].w};
+        for (int r = 0; r < 4; ++r)
+          if (col + r < p.N) Store4<OUT>::st1(crow + (col + r) * OSZ, v[r]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- generic fallback kernel
+// Any shape / alignment / dtype (incl. f64): 64x64 tile, 4x4 per thread, f32 (f64) FMA.
+template <typename T> __device__ __forceinline__ double ld_as_double(const void* p, int64_t i);
+template <int DT> __device__ __forceinline__ double load_elem(const char* base, int64_t idx) {
+  if constexpr (DT == DT_BF16) return (double)(float)((const __bf16*)base)[idx];
+  else if constexpr (DT == DT_F16) return (double)(float)((const _Float16*)base)[idx];
+  else if constexpr (DT == DT_F32) return (double)((const float*)base)[idx];
+  else if constexpr (DT == DT_F64) return ((const double*)base)[idx];
+  else {  // OCP e4m3fn
+    const uint8_t v = ((const uint8_t*)base)[idx];
+    const int s = v >> 7, e = (v >> 3) & 0xF, m = v & 7;
+    double r;
+    if (e == 0xF && m == 7) r = __builtin_nan("");
+    else if (e == 0) r = ldexp((double)m / 8.0, -6);
+    else r = ldexp(1.0 + (double)m / 8.0, e - 7);
+    return s ? -r : r;
+  }
+}
+template <int DT> __device__ __forceinline__ void store_elem(char* base, int64_t idx, double v) {
+  if constexpr (DT == DT_BF16) ((__bf16*)base)[idx] = (__bf16)(float)v;
+  else if constexpr (DT == DT_F16) ((_Float16*)base)[idx] = (_Float16)(float)v;
+  else if constexpr (DT == DT_F32) ((float*)base)[idx] = (float)v;
+  else ((double*)base)[idx] = v;
+}
+
+template <int DIN, int DOUT, typename Acc>
+__global__ __launch_bounds__(256) void gemm_generic_kernel(const GemmArgs p) {
+  const int tn = blockIdx.x, tm = blockIdx.y;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  Acc acc[4][4] = {};
+  const char* A = (const char*)p.a;
+  const char* B = (const char*)p.b;
+  for (int k = 0; k < p.K; ++k) {
+    Acc av[4], bv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t r = (int64_t)tm * 64 + ty * 4 + i;
+      av[i] = r < p.M ? (Acc)load_elem<DIN>(A, map_row(r, p.a_grp, p.a_gstride) * p.lda + k) : 0;
+      const int64_t c = (int64_t)tn * 64 + tx * 4 + i;
+      bv[i] = c < p.N ? (Acc)load_elem<DIN>(B, c * p.ldb + k) : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] += av[i] * bv[j];
+  }
+  char* C = (char*)p.c;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t r = (int64_t)tm * 64 + ty * 4 + i;
+    if (r >= p.M) continue;
+    const int64_t rp = map_row(r, p.c_grp, p.c_gstride) * p.ldc;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t c = (int64_t)tn * 64 + tx * 4 + j;
+      if (c < p.N) store_elem<DOUT>(C, rp + c, (double)acc[i][j]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- dispatch
+template <class Mma, int OUT, int BM, int BN, int WM, int WN>
+hipError_t launch_tiled(const GemmArgs& p, hipStream_t s) {
+  const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm_tn_kernel<Mma, OUT, BM, BN, WM, WN>), dim3(tiles), dim3(WM * WN * 64),
+                     0, s, p);
+  return hipGetLastError();
+}
+template <int OUT, int BM, int BN, int WM, int WN>
+hipError_t launch_mx(const GemmArgs& p, hipStream_t s) {
+  const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm_tn_mxfp8_kernel<OUT, BM, BN, WM, WN>), dim3(tiles),
+                     dim3(WM * WN * 64), 0, s, p);
+  return hipGetLastError();
+}
+
+template <class Mma, int OUT>
+hipError_t launch_cfg(const GemmArgs& p, int tile, hipStream_t s) {
+  switch (tile) {
+    case TILE_256x256: return launch_tiled<Mma, OUT, 256, 256, 2, 4>(p, s);
+    case TILE_256x128: return launch_tiled<Mma, OUT, 256, 128, 4, 2>(p, s);
+    case TILE_128x256: return launch_tiled<Mma, OUT, 128, 256, 2, 4>(p, s);
+    case TILE_128x128: return launch_tiled<Mma, OUT, 128, 128, 2, 2>(p, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+template <int OUT>
+hipError_t launch_mx_cfg(const GemmArgs& p, int tile, hipStream_t s) {
+  switch (tile) {
+    case TILE_256x256: return launch_mx<OUT, 256, 256, 2, 4>(p, s);
+    case TILE_256x128: return launch_mx<OUT, 256, 128, 4, 2>(p, s);
+    case TILE_128x256: return launch_mx<OUT, 128, 256, 2, 4>(p, s);
+    case TILE_128x128: return launch_mx<OUT, 128, 128, 2, 2>(p, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int DIN, int DOUT>
+hipError_t launch_generic_t(const GemmArgs& p, hipStream_t s) {
+  dim3 grid((p.N + 63) / 64, (p.M + 63) / 64);
+  if constexpr (DIN == DT_F64)
+    hipLaunchKernelGGL((gemm_generic_kernel<DIN, DOUT, double>), grid, dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm_generic_kernel<DIN, DOUT, float>), grid, dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+int tile_rows(int tile) { return (tile == TILE_128x128 || tile == TILE_128x256) ? 128 : 256; }
+int tile_cols(int tile) { return (tile == TILE_256x128 || tile == TILE_128x128) ? 128 : 256; }
+
+bool gemm_fast_path_ok(const GemmArgs& p, int din, int dout) {
+  const int esz = dtype_size(din);
+  if (din == DT_F64 || (din == DT_FP8 && dout == DT_FP8)) return false;
+  if (p.M <= 0 || p.N <= 0 || p.K <= 0) return false;
+  if ((int64_t)p.K * esz % 128 != 0) return false;
+  if (p.lda * esz % 16 || p.ldb * esz % 16) return false;
+  if (((uintptr_t)p.a | (uintptr_t)p.b) & 15) return false;
+  if ((p.ldc * dtype_size(dout)) % 8 || ((uintptr_t)p.c & 7)) return false;
+  if (p.a_grp <= 0 || p.c_grp <= 0) return false;
+  return true;
+}
+
+int choose_tile(int64_t M, int64_t N, int din) {
+  // Fill the 256 CUs: prefer the big tile while it yields >= ~1.5 waves of blocks.
+  auto tiles = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
+  if (tiles(256, 256) >= 384) return TILE_256x256;
+  if (tiles(256, 128) >= 384) return TILE_256x128;
+  if (tiles(128, 256) >= 384) return TILE_128x256;
+  return TILE_128x128;
+}
+
+hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mode,
+                       hipStream_t s) {
+  GemmArgs p = p_in;
+  if (p.a_grp <= 0) { p.a_grp = p.M > 0 ? p.M : 1; p.a_gstride = p.a_grp; }
+  if (p.c_grp <= 0) { p.c_grp = p.M > 0 ? p.M : 1; p.c_gstride = p.c_grp; }
+  if (p.M == 0 || p.N == 0) return hipSuccess;
+  const bool fast = mode != GEMM_MODE_GENERIC && gemm_fast_path_ok(p, din, dout);
+  if (p.tile_order && !fast) p.tile_order = 0;
+  if (fast) {
+    if (tile == TILE_AUTO) tile = choose_tile(p.M, p.N, din);
+    if (p.tile_order && (p.nshards <= 0 || p.M % p.nshards != 0 ||
+                         (p.M / p.nshards) % tile_rows(tile) != 0))
+      p.tile_order = 0;
+    if (din == DT_FP8 && mode == GEMM_MODE_MX) {
+      if (dout == DT_BF16) return launch_mx_cfg<DT_BF16>(p, tile, s);
+      if (dout == DT_F16) return launch_mx_cfg<DT_F16>(p, tile, s);
+      if (dout == DT_F32) return launch_mx_cfg<DT_F32>(p, tile, s);
+    }
+    if (din == DT_BF16) {
+      if (dout == DT_BF16) return launch_cfg<MmaBF16, DT_BF16>(p, tile, s);
+      if (dout == DT_F32) return launch_cfg<MmaBF16, DT_F32>(p, tile, s);
+    } else if (din == DT_F16) {
+      if (dout == DT_F16) return launch_cfg<MmaF16, DT_F16>(p, tile, s);
+      if (dout == DT_F32) return launch_cfg<MmaF16, DT_F32>(p, tile, s);
+    } else if (din == DT_FP8) {
+      if (dout == DT_BF16) return launch_cfg<MmaFP8, DT_BF16>(p, tile, s);
+      if (dout == DT_F16) return launch_cfg<MmaFP8, DT_F16>(p, tile, s);
+      if (dout == DT_F32) return launch_cfg<MmaFP8, DT_F32>(p, tile, s);
+    } else if (din == DT_F32) {
+      if (dout == DT_F32) return launch_cfg<MmaF32, DT_F32>(p, tile, s);
+    }
+  }
+  if (p.flags != nullptr) return hipErrorNotSupported;  // arrival flags need the tiled kernel
+  // generic path
+#define GEN(DI, DO) if (din == DI && dout == DO) return launch_generic_t<DI, DO>(p, s)
+  GEN(DT_BF16, DT_BF16); GEN(DT_BF16, DT_F32); GEN(DT_F16, DT_F16); GEN(DT_F16, DT_F32);
+  GEN(DT_F32, DT_F32); GEN(DT_F64, DT_F64); GEN(DT_FP8, DT_BF16); GEN(DT_FP8, DT_F16);
+  GEN(DT_FP8, DT_F32);
+#undef GEN
+  return hipErrorInvalidValue;
+}
+
+}  // namespace ddlb

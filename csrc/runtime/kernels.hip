@@ -1,0 +1,199 @@
+// Small data-movement / synchronisation kernels used by the plan executor.
+//
+//  * reduce_sum: dst = sum_j src_j (up to 16 sources, any of them peer memory over xGMI), f32
+//    accumulation, one rounding — the fused "sum d partial tiles -> output" of the p2p
+//    reduce-scatter (SURVEY.md §2.4 "Reductions inside RS").
+//  * copy: CU-driven 16-byte vector copy (the `kernel` protocol; stands in for NVLS multimem,
+//    which MI355X does not have). Reads/writes may be peer pointers.
+//  * signal / wait: cross-process flags in symmetric memory. Release stores at system scope,
+//    bounded relaxed polling, acquire at system scope after the match (cdna guide §6 G16).
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <hip/hip_fp16.h>
+#include <stdint.h>
+
+#include "kernels.h"
+
+namespace ddlb {
+namespace {
+
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+
+template <int DT> struct V8;  // 16-byte vector of the element type, widened to f32
+template <> struct V8<0> {    // f32: 4 elements per 16 B
+  static constexpr int N = 4;
+  static __device__ __forceinline__ void load(const void* p, float* o) {
+    const f32x4 v = *(const f32x4*)p;
+    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+  }
+  static __device__ __forceinline__ void store(void* p, const float* o) {
+    *(f32x4*)p = f32x4{o[0], o[1], o[2], o[3]};
+  }
+};
+template <> struct V8<1> {  // f16
+  static constexpr int N = 8;
+  static __device__ __forceinline__ void load(const void* p, float* o) {
+    const f16x8 v = *(const f16x8*)p;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (float)v[i];
+  }
+  static __device__ __forceinline__ void store(void* p, const float* o) {
+    f16x8 v;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (_Float16)o[i];
+    *(f16x8*)p = v;
+  }
+};
+template <> struct V8<2> {  // bf16
+  static constexpr int N = 8;
+  static __device__ __forceinline__ void load(const void* p, float* o) {
+    const bf16x8 v = *(const bf16x8*)p;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (float)v[i];
+  }
+  static __device__ __forceinline__ void store(void* p, const float* o) {
+    bf16x8 v;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (__bf16)o[i];
+    *(bf16x8*)p = v;
+  }
+};
+
+template <int DT>
+__device__ __forceinline__ float load1(const void* p, int64_t i) {
+  if constexpr (DT == 0) return ((const float*)p)[i];
+  else if constexpr (DT == 1) return (float)((const _Float16*)p)[i];
+  else return (float)((const __bf16*)p)[i];
+}
+template <int DT>
+__device__ __forceinline__ void store1(void* p, int64_t i, float v) {
+  if constexpr (DT == 0) ((float*)p)[i] = v;
+  else if constexpr (DT == 1) ((_Float16*)p)[i] = (_Float16)v;
+  else ((__bf16*)p)[i] = (__bf16)v;
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void reduce_sum_kernel(ReduceArgs a) {
+  using V = V8<DT>;
+  const int64_t nvec = a.count / V::N;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    float acc[V::N], t[V::N];
+    V::load((const char*)a.src[0] + v * 16, acc);
+    for (int s = 1; s < a.nsrc; ++s) {
+      V::load((const char*)a.src[s] + v * 16, t);
+#pragma unroll
+      for (int i = 0; i < V::N; ++i) acc[i] += t[i];
+    }
+    V::store((char*)a.dst + v * 16, acc);
+  }
+  const int64_t tail0 = nvec * V::N;
+  for (int64_t i = tail0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.count;
+       i += stride) {
+    float acc = 0.f;
+    for (int s = 0; s < a.nsrc; ++s) acc += load1<DT>(a.src[s], i);
+    store1<DT>(a.dst, i, acc);
+  }
+}
+
+__global__ __launch_bounds__(256) void copy_kernel(CopyArgs a) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int seg = 0; seg < a.nseg; ++seg) {
+    const char* src = (const char*)a.src[seg];
+    char* dst = (char*)a.dst[seg];
+    const int64_t bytes = a.bytes[seg];
+    const int64_t nvec = bytes / 16;
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // 4 x 16 B in flight per lane
+    int64_t v = t0;
+    for (; v + 3 * stride < nvec; v += 4 * stride) {
+      const uint4 x0 = *(const uint4*)(src + v * 16);
+      const uint4 x1 = *(const uint4*)(src + (v + stride) * 16);
+      const uint4 x2 = *(const uint4*)(src + (v + 2 * stride) * 16);
+      const uint4 x3 = *(const uint4*)(src + (v + 3 * stride) * 16);
+      *(uint4*)(dst + v * 16) = x0;
+      *(uint4*)(dst + (v + stride) * 16) = x1;
+      *(uint4*)(dst + (v + 2 * stride) * 16) = x2;
+      *(uint4*)(dst + (v + 3 * stride) * 16) = x3;
+    }
+    for (; v < nvec; v += stride) *(uint4*)(dst + v * 16) = *(const uint4*)(src + v * 16);
+    for (int64_t b = nvec * 16 + t0; b < bytes; b += stride) dst[b] = src[b];
+  }
+}
+
+__global__ void signal_kernel(SignalArgs a) {
+  const int i = threadIdx.x;
+  if (i < a.n) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+    __hip_atomic_store(a.ptr[i], a.value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+__global__ void wait_kernel(WaitArgs a) {
+  if (threadIdx.x != 0) return;
+  for (int i = 0; i < a.n; ++i) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(a.ptr[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.value) {
+      __builtin_amdgcn_s_sleep(4);
+      if (++spins > (1u << 27)) {  // bounded: report and drain instead of hanging the GPU
+        if (a.timeout_word) atomicOr(a.timeout_word, 2u);
+        break;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
+
+int grid_for(int64_t work_items) {
+  int64_t g = (work_items + 255) / 256;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace
+
+hipError_t reduce_sum_launch(const ReduceArgs& a, int dtype, hipStream_t s) {
+  if (a.nsrc < 1 || a.nsrc > kMaxReduceSrc || a.count <= 0) return hipErrorInvalidValue;
+  for (int i = 0; i < a.nsrc; ++i)
+    if ((uintptr_t)a.src[i] & 15) return hipErrorInvalidValue;
+  if ((uintptr_t)a.dst & 15) return hipErrorInvalidValue;
+  const int per = dtype == 0 ? 4 : 8;
+  const int g = grid_for(a.count / per + 1);
+  switch (dtype) {
+    case 0: hipLaunchKernelGGL(reduce_sum_kernel<0>, dim3(g), dim3(256), 0, s, a); break;
+    case 1: hipLaunchKernelGGL(reduce_sum_kernel<1>, dim3(g), dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL(reduce_sum_kernel<2>, dim3(g), dim3(256), 0, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t copy_launch(const CopyArgs& a, int max_blocks, hipStream_t s) {
+  if (a.nseg < 1 || a.nseg > kMaxCopySeg) return hipErrorInvalidValue;
+  int64_t total = 0;
+  for (int i = 0; i < a.nseg; ++i) {
+    if (((uintptr_t)a.src[i] | (uintptr_t)a.dst[i]) & 15) return hipErrorInvalidValue;
+    total += a.bytes[i];
+  }
+  int g = grid_for(total / 64 + 1);
+  if (max_blocks > 0 && g > max_blocks) g = max_blocks;
+  hipLaunchKernelGGL(copy_kernel, dim3(g), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t signal_launch(const SignalArgs& a, hipStream_t s) {
+  if (a.n < 1 || a.n > kMaxSignal) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(signal_kernel, dim3(1), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t wait_launch(const WaitArgs& a, hipStream_t s) {
+  if (a.n < 1 || a.n > kMaxSignal) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(wait_kernel, dim3(1), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace ddlb

@@ -1,0 +1,217 @@
+// Plan executor implementation (see plan.h).
+#include "plan.h"
+
+#include <stdexcept>
+
+#include "../gemm/gemm.h"
+#include "kernels.h"
+
+namespace ddlb {
+
+PlanExecutor::PlanExecutor(int device, int nstreams, int nevents,
+                           const std::vector<int>& priorities)
+    : device_(device) {
+  DDLB_HIP(hipSetDevice(device));
+  if (nstreams < 1) nstreams = 1;
+  streams_.assign((size_t)nstreams, nullptr);
+  fork_join_.assign((size_t)nstreams * 2, nullptr);
+  used_.assign((size_t)nstreams, false);
+  int lo = 0, hi = 0;
+  DDLB_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  for (int i = 1; i < nstreams; ++i) {
+    int prio = (size_t)i < priorities.size() ? priorities[(size_t)i] : 0;
+    // priority: 0 = normal, 1 = high (comm streams)
+    const int p = prio > 0 ? hi : lo;
+    DDLB_HIP(hipStreamCreateWithPriority(&streams_[(size_t)i], hipStreamNonBlocking, p));
+  }
+  for (auto& e : fork_join_) DDLB_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  events_.assign((size_t)(nevents > 0 ? nevents : 0), nullptr);
+  for (auto& e : events_) DDLB_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  DDLB_HIP(hipMalloc(&d_timeout_, 256));
+  DDLB_HIP(hipMemset(d_timeout_, 0, 256));
+}
+
+PlanExecutor::~PlanExecutor() {
+  hipSetDevice(device_);
+  for (size_t i = 1; i < streams_.size(); ++i)
+    if (streams_[i]) {
+      hipStreamSynchronize(streams_[i]);
+      hipStreamDestroy(streams_[i]);
+    }
+  for (auto e : fork_join_) if (e) hipEventDestroy(e);
+  for (auto e : events_) if (e) hipEventDestroy(e);
+  if (d_timeout_) hipFree(d_timeout_);
+}
+
+void PlanExecutor::load(const std::vector<int64_t>& ops) {
+  if (ops.size() % kOpWords != 0) throw std::runtime_error("plan: bad op array length");
+  std::fill(used_.begin(), used_.end(), false);
+  for (size_t i = 0; i < ops.size(); i += kOpWords) {
+    const int64_t s = ops[i + 1];
+    if (s < 0 || (size_t)s >= streams_.size()) throw std::runtime_error("plan: bad stream index");
+    used_[(size_t)s] = true;
+    const int64_t kind = ops[i];
+    if (kind == OP_RECORD || kind == OP_WAIT) {
+      const int64_t e = ops[i + 2];
+      if (e < 0 || (size_t)e >= events_.size()) throw std::runtime_error("plan: bad event index");
+    }
+    if (kind == OP_GEMM) {
+      if (ops[i + 12] < 0 || ops[i + 13] < 0 || ops[i + 14] <= 0)
+        throw std::runtime_error("plan: bad GEMM shape");
+      if (!ops[i + 2] || !ops[i + 3] || !ops[i + 4]) throw std::runtime_error("plan: null GEMM ptr");
+    }
+  }
+  ops_ = ops;
+}
+
+unsigned PlanExecutor::read_timeout() {
+  unsigned v = 0;
+  DDLB_HIP(hipMemcpy(&v, d_timeout_, sizeof(v), hipMemcpyDeviceToHost));
+  return v;
+}
+
+unsigned PlanExecutor::run(uintptr_t main_stream) {
+  hipStream_t main = (hipStream_t)main_stream;
+  ++epoch_;
+  // fork: every used side stream waits for everything already queued on the caller's stream
+  DDLB_HIP(hipEventRecord(fork_join_[0], main));
+  for (size_t i = 1; i < streams_.size(); ++i)
+    if (used_[i]) DDLB_HIP(hipStreamWaitEvent(streams_[i], fork_join_[0], 0));
+  for (size_t i = 0; i < ops_.size(); i += kOpWords) exec(&ops_[i], main);
+  // join
+  for (size_t i = 1; i < streams_.size(); ++i)
+    if (used_[i]) {
+      DDLB_HIP(hipEventRecord(fork_join_[streams_.size() + i], streams_[i]));
+      DDLB_HIP(hipStreamWaitEvent(main, fork_join_[streams_.size() + i], 0));
+    }
+  return epoch_;
+}
+
+void PlanExecutor::exec(const int64_t* o, hipStream_t main) {
+  hipStream_t s = S(o[1], main);
+  switch (o[0]) {
+    case OP_NOP: return;
+    case OP_GEMM: {
+      GemmArgs g;
+      g.a = (const void*)o[2];
+      g.b = (const void*)o[3];
+      g.c = (void*)o[4];
+      g.lda = o[5]; g.ldb = o[6]; g.ldc = o[7];
+      g.a_grp = o[8]; g.a_gstride = o[9];
+      g.c_grp = o[10]; g.c_gstride = o[11];
+      g.M = (int)o[12]; g.N = (int)o[13]; g.K = (int)o[14];
+      g.flags = (const unsigned*)o[19];
+      g.epoch = epoch_;
+      g.flag_rows = o[20] > 0 ? o[20] : 1;
+      g.nshards = o[21] > 0 ? (int)o[21] : 1;
+      g.first_shard = (int)o[22];
+      g.tile_order = (int)o[23];
+      g.timeout_word = d_timeout_;
+      DDLB_HIP(gemm_launch(g, (int)o[15], (int)o[16], (int)o[17], (int)o[18], s));
+      return;
+    }
+    case OP_RECORD: DDLB_HIP(hipEventRecord(events_[(size_t)o[2]], s)); return;
+    case OP_WAIT: DDLB_HIP(hipStreamWaitEvent(s, events_[(size_t)o[2]], 0)); return;
+    case OP_ALLGATHER:
+      if (!comm_) throw std::runtime_error("plan: allgather without an RCCL communicator");
+      DDLB_NCCL(ncclAllGather((const void*)o[2], (void*)o[3], (size_t)o[4], nccl_dtype((int)o[5]),
+                              comm_->get(), s));
+      return;
+    case OP_REDUCE_SCATTER:
+      if (!comm_) throw std::runtime_error("plan: reduce-scatter without an RCCL communicator");
+      DDLB_NCCL(ncclReduceScatter((const void*)o[2], (void*)o[3], (size_t)o[4],
+                                  nccl_dtype((int)o[5]), ncclSum, comm_->get(), s));
+      return;
+    case OP_SEND:
+      if (!comm_) throw std::runtime_error("plan: send without an RCCL communicator");
+      DDLB_NCCL(ncclSend((const void*)o[2], (size_t)o[3], nccl_dtype((int)o[4]), (int)o[5],
+                         comm_->get(), s));
+      return;
+    case OP_RECV:
+      if (!comm_) throw std::runtime_error("plan: recv without an RCCL communicator");
+      DDLB_NCCL(ncclRecv((void*)o[2], (size_t)o[3], nccl_dtype((int)o[4]), (int)o[5],
+                         comm_->get(), s));
+      return;
+    case OP_GROUP_START: DDLB_NCCL(ncclGroupStart()); return;
+    case OP_GROUP_END: DDLB_NCCL(ncclGroupEnd()); return;
+    case OP_COPY:
+      if (o[5] == 0) {
+        DDLB_HIP(hipMemcpyAsync((void*)o[2], (const void*)o[3], (size_t)o[4],
+                                hipMemcpyDeviceToDevice, s));
+      } else {
+        CopyArgs c;
+        c.nseg = 1;
+        c.dst[0] = (void*)o[2];
+        c.src[0] = (const void*)o[3];
+        c.bytes[0] = o[4];
+        DDLB_HIP(copy_launch(c, (int)o[6], s));
+      }
+      return;
+    case OP_COPY_MULTI: {
+      CopyArgs c;
+      c.nseg = (int)o[2];
+      if (c.nseg < 1 || c.nseg > kMaxCopySeg || 4 + 3 * c.nseg > kOpWords)
+        throw std::runtime_error("plan: bad multi-copy");
+      for (int i = 0; i < c.nseg; ++i) {
+        c.dst[i] = (void*)o[4 + 3 * i];
+        c.src[i] = (const void*)o[5 + 3 * i];
+        c.bytes[i] = o[6 + 3 * i];
+      }
+      DDLB_HIP(copy_launch(c, (int)o[3], s));
+      return;
+    }
+    case OP_SIGNAL: {
+      const int n = (int)o[2];
+      if (n < 1 || n > kMaxSignal || 4 + n > kOpWords) throw std::runtime_error("plan: bad signal");
+      if (o[3] == 1) {
+        for (int i = 0; i < n; ++i)
+          DDLB_HIP(hipStreamWriteValue32(s, (void*)o[4 + i], epoch_, 0));
+      } else {
+        SignalArgs a;
+        a.n = n;
+        a.value = epoch_;
+        for (int i = 0; i < n; ++i) a.ptr[i] = (unsigned*)o[4 + i];
+        DDLB_HIP(signal_launch(a, s));
+      }
+      return;
+    }
+    case OP_WAIT_SIGNAL: {
+      const int n = (int)o[2];
+      if (n < 1 || n > kMaxSignal || 4 + n > kOpWords) throw std::runtime_error("plan: bad wait");
+      if (o[3] == 1) {
+        for (int i = 0; i < n; ++i)
+          DDLB_HIP(hipStreamWaitValue32(s, (void*)o[4 + i], epoch_, hipStreamWaitValueGte,
+                                        0xffffffffu));
+      } else {
+        WaitArgs a;
+        a.n = n;
+        a.value = epoch_;
+        a.timeout_word = d_timeout_;
+        for (int i = 0; i < n; ++i) a.ptr[i] = (unsigned*)o[4 + i];
+        DDLB_HIP(wait_launch(a, s));
+      }
+      return;
+    }
+    case OP_REDUCE: {
+      ReduceArgs a;
+      a.dst = (void*)o[2];
+      a.count = o[3];
+      a.nsrc = (int)o[5];
+      if (a.nsrc < 1 || a.nsrc > kMaxReduceSrc || 6 + a.nsrc > kOpWords)
+        throw std::runtime_error("plan: bad reduce");
+      for (int i = 0; i < a.nsrc; ++i) a.src[i] = (const void*)o[6 + i];
+      const int dt = (int)o[4];
+      const int kdt = dt == DT_F32 ? 0 : dt == DT_F16 ? 1 : dt == DT_BF16 ? 2 : -1;
+      if (kdt < 0) throw std::runtime_error("plan: reduce dtype must be f32/f16/bf16");
+      DDLB_HIP(reduce_sum_launch(a, kdt, s));
+      return;
+    }
+    case OP_MEMSET:
+      DDLB_HIP(hipMemsetAsync((void*)o[2], (int)o[4], (size_t)o[3], s));
+      return;
+    default:
+      throw std::runtime_error("plan: unknown op kind " + std::to_string(o[0]));
+  }
+}
+
+}  // namespace ddlb

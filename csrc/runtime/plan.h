@@ -1,0 +1,76 @@
+// Plan executor: a tiny host IR for distributed-GEMM schedules, executed natively.
+//
+// The reference lowers its pipelines through nvFuser's MultiDeviceExecutor / host IR
+// (ddlb/primitives/TPColumnwise/fuser.py:247-257). Here Python (ddlb_amd/parallel/plan.py) builds a
+// flat list of ops once at construction; every run() is ONE call into this executor, which
+// enqueues GEMM kernels, RCCL collectives, copy-engine transfers, cross-process signals and
+// event edges on a fixed set of HIP streams. Stream 0 is the caller's stream: the executor forks
+// every other stream from it at the start and joins them back at the end, so the plan is
+// ordered with surrounding torch work and a device synchronize covers all of it.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../comm/comm.h"
+
+namespace ddlb {
+
+// Op layout: kOpWords int64 per op. word 0 = kind, word 1 = stream index.
+constexpr int kOpWords = 32;
+enum OpKind : int64_t {
+  OP_NOP = 0,
+  OP_GEMM = 1,        // 2 a, 3 b, 4 c, 5 lda, 6 ldb, 7 ldc, 8 a_grp, 9 a_gstride, 10 c_grp,
+                      // 11 c_gstride, 12 M, 13 N, 14 K, 15 din, 16 dout, 17 tile, 18 mode,
+                      // 19 flags ptr (0 = none), 20 flag_rows, 21 nshards, 22 first_shard,
+                      // 23 tile_order
+  OP_RECORD = 2,      // 2 event
+  OP_WAIT = 3,        // 2 event
+  OP_ALLGATHER = 4,   // 2 send, 3 recv, 4 count per rank, 5 dtype
+  OP_REDUCE_SCATTER = 5,  // 2 send, 3 recv, 4 recv count, 5 dtype
+  OP_SEND = 6,        // 2 buf, 3 count, 4 dtype, 5 peer
+  OP_RECV = 7,        // 2 buf, 3 count, 4 dtype, 5 peer
+  OP_GROUP_START = 8,
+  OP_GROUP_END = 9,
+  OP_COPY = 10,       // 2 dst, 3 src, 4 bytes, 5 method (0 copy engine, 1 CU kernel),
+                      // 6 max CU blocks (kernel method)
+  OP_SIGNAL = 11,     // 2 n, 3 method (0 kernel, 1 stream write), 4.. flag ptrs; value = epoch
+  OP_WAIT_SIGNAL = 12,  // 2 n, 3 method (0 kernel, 1 stream wait), 4.. flag ptrs; >= epoch
+  OP_REDUCE = 13,     // 2 dst, 3 count, 4 dtype, 5 nsrc, 6.. src ptrs
+  OP_MEMSET = 14,     // 2 dst, 3 bytes, 4 byte value
+  OP_COPY_MULTI = 15, // 2 nseg, 3 max blocks, then (dst, src, bytes) triples from word 4
+};
+
+class PlanExecutor {
+ public:
+  PlanExecutor(int device, int nstreams, int nevents, const std::vector<int>& priorities);
+  ~PlanExecutor();
+  void load(const std::vector<int64_t>& ops);
+  void set_comm(RcclComm* comm) { comm_ = comm; }
+  // Enqueue the whole plan behind `main_stream`; returns the epoch used (1, 2, ...).
+  unsigned run(uintptr_t main_stream);
+  unsigned epoch() const { return epoch_; }
+  int nops() const { return (int)(ops_.size() / kOpWords); }
+  uintptr_t timeout_word() const { return (uintptr_t)d_timeout_; }
+  unsigned read_timeout();  // synchronous; 0 = healthy
+  uintptr_t stream(int i) const { return (uintptr_t)streams_.at(i); }
+
+ private:
+  void exec(const int64_t* op, hipStream_t main);
+  hipStream_t S(int64_t idx, hipStream_t main) const {
+    return idx == 0 ? main : streams_.at((size_t)idx);
+  }
+  int device_;
+  std::vector<hipStream_t> streams_;  // [0] unused (= caller stream)
+  std::vector<hipEvent_t> events_;
+  std::vector<hipEvent_t> fork_join_;  // one per stream
+  std::vector<int64_t> ops_;
+  std::vector<bool> used_;             // stream i touched by the plan
+  RcclComm* comm_ = nullptr;
+  unsigned epoch_ = 0;
+  unsigned* d_timeout_ = nullptr;
+};
+
+}  // namespace ddlb

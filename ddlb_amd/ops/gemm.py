@@ -1,0 +1,117 @@
+"""Python front-end of the CDNA4 MFMA GEMM (``csrc/gemm/gemm_mfma.hip``).
+
+``gemm(a, w)`` computes ``a @ w.T`` for ``a: [M, K]`` and ``w: [N, K]`` (the weight kept
+K-contiguous, like ``te.Linear``'s ``[out, in]``), with optional grouped-row addressing of A and C:
+logical row ``i`` lives at physical row ``base + (i // grp) * gstride + i % grp``.
+
+Every shape / dtype / device / alignment / bounds check happens here, on the host, before the
+kernel launches (a bad launch can fault every GPU of the node).
+
+dtypes: bf16 -> bf16|f32, f16 -> f16|f32, f32 -> f32 (exact f32 MFMA), float8_e4m3fn -> bf16|f16|f32
+(``mx=True``: block-scaled MX-fp8 MFMA at 2x the bf16 rate, unit scales), f64 (generic kernel).
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+from ddlb_amd.ops import load
+
+DT_F32, DT_F16, DT_BF16, DT_FP8, DT_F64, DT_U8 = 0, 1, 2, 3, 4, 5
+TILES = {"auto": 0, "256x256": 1, "256x128": 2, "128x256": 3, "128x128": 4}
+MODES = {"auto": 0, "generic": 1, "mx": 2}
+
+SUPPORTED_IN = ("float32", "float16", "bfloat16", "float8_e4m3fn", "float64")
+
+
+def dtype_code(dt) -> int:
+    import torch
+
+    table = {torch.float32: DT_F32, torch.float16: DT_F16, torch.bfloat16: DT_BF16,
+             torch.float8_e4m3fn: DT_FP8, torch.float64: DT_F64, torch.uint8: DT_U8}
+    if dt not in table:
+        raise TypeError(f"dtype {dt} is not supported by the native GEMM")
+    return table[dt]
+
+
+def check_supported(dtype_name: str) -> None:
+    if dtype_name not in SUPPORTED_IN:
+        raise TypeError(f"native GEMM supports {SUPPORTED_IN}, not {dtype_name}")
+
+
+def default_out_dtype(in_dtype):
+    import torch
+
+    return torch.bfloat16 if in_dtype == torch.float8_e4m3fn else in_dtype
+
+
+def _check_operands(a, w, out, M, a_rows_phys):
+    import torch
+
+    if a.device.type != "cuda" or w.device.type != "cuda" or out.device.type != "cuda":
+        raise ValueError("native GEMM operands must be ROCm device tensors")
+    if not (a.device == w.device == out.device):
+        raise ValueError("operands on different devices")
+    if a.dim() != 2 or w.dim() != 2 or out.dim() != 2:
+        raise ValueError("native GEMM expects 2-D operands")
+    if a.stride(1) != 1 or w.stride(1) != 1 or out.stride(1) != 1:
+        raise ValueError("operands must be row-major with unit inner stride")
+    if a.dtype != w.dtype:
+        raise TypeError(f"A dtype {a.dtype} != W dtype {w.dtype}")
+    if a.shape[1] != w.shape[1]:
+        raise ValueError(f"K mismatch: A {tuple(a.shape)} vs W {tuple(w.shape)}")
+    if out.shape[1] < w.shape[0]:
+        raise ValueError(f"output has {out.shape[1]} columns < N={w.shape[0]}")
+    if a_rows_phys > a.shape[0]:
+        raise ValueError(f"A row mapping reaches row {a_rows_phys - 1} >= {a.shape[0]}")
+    if a.dtype == torch.float8_e4m3fn and out.dtype not in (torch.bfloat16, torch.float16,
+                                                             torch.float32):
+        raise TypeError("fp8 GEMM output must be bf16, f16 or f32")
+
+
+def _phys_rows(M: int, grp: int, gstride: int, base_rows: int = 0) -> int:
+    """One past the largest physical row the mapping touches."""
+    if M == 0:
+        return 0
+    if grp <= 0:
+        return M
+    last = M - 1
+    return (last // grp) * gstride + (last % grp) + 1
+
+
+def gemm(a, w, out=None, *, out_dtype=None, tile: str = "auto", mode: str = "auto",
+         M: Optional[int] = None, a_grp: int = 0, a_gstride: int = 0, c_grp: int = 0,
+         c_gstride: int = 0, stream=None):
+    """``out[:M] = a[:M] @ w.T`` on the current HIP stream (grouped-row addressing optional)."""
+    import torch
+
+    C = load()
+    if out is None:
+        rows = M if M is not None else a.shape[0]
+        out = torch.empty((rows, w.shape[0]), dtype=out_dtype or default_out_dtype(a.dtype),
+                          device=a.device)
+    M = a.shape[0] if M is None else int(M)
+    N, K = w.shape
+    a_need = _phys_rows(M, a_grp, a_gstride)
+    c_need = _phys_rows(M, c_grp, c_gstride)
+    _check_operands(a, w, out, M, a_need)
+    if c_need > out.shape[0]:
+        raise ValueError(f"C row mapping reaches row {c_need - 1} >= {out.shape[0]}")
+    if a_grp and (a_grp < 0 or a_gstride < a_grp):
+        raise ValueError("a_gstride must be >= a_grp")
+    if c_grp and (c_grp < 0 or c_gstride < c_grp):
+        raise ValueError("c_gstride must be >= c_grp")
+    if M >= 2 ** 31 or N >= 2 ** 31 or K >= 2 ** 31:
+        raise ValueError("dimensions must fit in 32 bits")
+    s = stream if stream is not None else torch.cuda.current_stream(a.device).cuda_stream
+    C.gemm(a.data_ptr(), w.data_ptr(), out.data_ptr(), a.stride(0), w.stride(0), out.stride(0),
+           M, N, K, dtype_code(a.dtype), dtype_code(out.dtype), TILES[tile], MODES[mode],
+           a_grp, a_gstride, c_grp, c_gstride, s)
+    return out
+
+
+def fast_path_ok(a, w, out) -> bool:
+    C = load()
+    return bool(C.gemm_fast_path_ok(a.data_ptr(), w.data_ptr(), out.data_ptr(), a.stride(0),
+                                    w.stride(0), out.stride(0), a.shape[0], w.shape[0],
+                                    a.shape[1], dtype_code(a.dtype), dtype_code(out.dtype)))

@@ -1,0 +1,153 @@
+"""Primitive base class: dtype map, seeding, option parsing, input generation, validation.
+
+Parity: the shared parts of ``ddlb/primitives/TPColumnwise/tp_columnwise.py:13-162`` and
+``ddlb/primitives/TPRowwise/tp_rowwise.py:13-185``.
+
+MI355X-first differences:
+
+* Inputs are generated **on the device** from a seeded ``torch.Generator`` (identical on every
+  rank, no H2D of a 1 GB matrix, no CPU RNG at m=65536) — the reference draws A on the CPU
+  (``tp_columnwise.py:105-110``).
+* Validation computes an fp32 reference **on the device** (the reference does a CPU matmul in the
+  benchmark dtype, ``tp_columnwise.py:148``, which is minutes at m=65536). The tolerance rule is
+  unchanged: ``rtol=0, atol=(1e-3 if 16-bit/8-bit else 1e-4) * k``.
+* ``float8_e4m3fn`` (OCP e4m3, the gfx950 format) is accepted; its GEMM output is bf16.
+"""
+
+from __future__ import annotations
+
+from abc import ABC, abstractmethod
+from typing import Any, Dict, Mapping, Optional, Tuple
+
+from ddlb_amd.communicator import Communicator
+from ddlb_amd.utils.options import OptionsManager
+
+DTYPE_NAMES = ("float32", "float64", "float16", "bfloat16", "int32", "int64", "float8_e4m3fn")
+DTYPE_ALIASES = {"fp32": "float32", "fp64": "float64", "fp16": "float16", "half": "float16",
+                 "bf16": "bfloat16", "fp8": "float8_e4m3fn", "float8": "float8_e4m3fn",
+                 "e4m3": "float8_e4m3fn"}
+
+
+def canonical_dtype(name: str) -> str:
+    name = DTYPE_ALIASES.get(str(name), str(name))
+    if name not in DTYPE_NAMES:
+        raise ValueError(f"Unsupported dtype: {name}. Must be one of {list(DTYPE_NAMES)}")
+    return name
+
+
+def torch_dtype(name: str):
+    import torch
+
+    return {
+        "float32": torch.float32, "float64": torch.float64, "float16": torch.float16,
+        "bfloat16": torch.bfloat16, "int32": torch.int32, "int64": torch.int64,
+        "float8_e4m3fn": torch.float8_e4m3fn,
+    }[canonical_dtype(name)]
+
+
+def output_dtype(name: str):
+    """GEMM output dtype: fp8 inputs produce bf16, everything else keeps its dtype."""
+    import torch
+
+    name = canonical_dtype(name)
+    return torch.bfloat16 if name == "float8_e4m3fn" else torch_dtype(name)
+
+
+def atol_for(name: str, k: int) -> float:
+    name = canonical_dtype(name)
+    low = name in ("float16", "bfloat16", "float8_e4m3fn")
+    return (1e-3 if low else 1e-4) * k
+
+
+def uniform_pm1(shape, dtype_name: str, generator, device):
+    """U[-1, 1) in the benchmark dtype (ints: uniform in [-2, 2])."""
+    import torch
+
+    name = canonical_dtype(dtype_name)
+    if name in ("int32", "int64"):
+        return torch.randint(-2, 3, shape, generator=generator, device=device,
+                             dtype=torch_dtype(name))
+    x = torch.rand(shape, generator=generator, device=device, dtype=torch.float32)
+    x.mul_(2).sub_(1)
+    return x.to(torch_dtype(name))
+
+
+class Primitive(ABC):
+    """Common machinery of a distributed-GEMM primitive."""
+
+    NAME = "primitive"
+    DEFAULT_OPTIONS: Dict[str, Any] = {}
+    ALLOWED_VALUES: Dict[str, Any] = {}
+    OPTION_ALIASES: Dict[str, Dict[Any, Any]] = {}
+
+    def __init__(self, m: int, n: int, k: int, dtype: str = "float32", seed: int = 42,
+                 **kwargs):
+        import torch
+
+        self.communicator = Communicator()
+        self.m, self.n, self.k = int(m), int(n), int(k)
+        self.dtype = canonical_dtype(dtype)
+        self.torch_dtype = torch_dtype(self.dtype)
+        self.out_dtype = output_dtype(self.dtype)
+        self.seed = seed
+        self.rank = self.communicator.rank
+        self.world_size = self.communicator.world_size
+        self.device = self.communicator.device
+        self._check_shape()
+        torch.manual_seed(seed)
+        self.options = OptionsManager(self.DEFAULT_OPTIONS, self.ALLOWED_VALUES,
+                                      self.OPTION_ALIASES)
+        self.options.parse(kwargs)
+        self._generator = torch.Generator(device=self.device)
+        self._generator.manual_seed(seed)
+        self._input_setup()
+
+    # ----------------------------------------------------------------- interface
+    @abstractmethod
+    def _check_shape(self) -> None: ...
+
+    @abstractmethod
+    def _input_setup(self) -> None: ...
+
+    @abstractmethod
+    def run(self):
+        """Execute the primitive once; returns this rank's result tensor."""
+
+    @abstractmethod
+    def expected(self):
+        """fp32 reference for this rank's result (same shape as ``run()``'s output)."""
+
+    def get_inputs(self) -> Tuple[Any, Any]:
+        return self.A, self.B
+
+    @property
+    def flops(self) -> float:
+        """The harness FLOP count ``2*m*n*k`` (``ddlb/benchmark.py:211``)."""
+        return 2.0 * self.m * self.n * self.k
+
+    def validate(self, result) -> None:
+        import torch
+        from torch.testing import assert_close
+
+        ref = self.expected()
+        got = result.detach()
+        if got.shape != ref.shape:
+            raise AssertionError(f"result shape {tuple(got.shape)} != expected {tuple(ref.shape)}")
+        assert_close(got.to(torch.float32), ref.to(torch.float32), rtol=0,
+                     atol=atol_for(self.dtype, self.k))
+
+    def close(self) -> None:
+        """Release implementation resources (streams, plans, process groups)."""
+
+    # ----------------------------------------------------------------- helpers
+    def _ref_matmul(self, a, b):
+        import torch
+
+        if a.dtype in (torch.int32, torch.int64):
+            return (a.to(torch.float64) @ b.to(torch.float64)).to(torch.float32)
+        if self.device.type == "cpu" and a.dtype == torch.float64:
+            return (a @ b).to(torch.float32)
+        return a.to(torch.float32) @ b.to(torch.float32)
+
+    def option_items(self) -> Mapping[str, Any]:
+        return self.options.as_dict()
