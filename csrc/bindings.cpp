@@ -23,7 +23,10 @@ using namespace ddlb;
 namespace {
 
 void check(hipError_t e, const char* what) {
-  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+  if (e != hipSuccess) {
+    (void)hipGetLastError();  // keep torch's next error check clean
+    throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+  }
 }
 
 struct DLCtx {
@@ -143,6 +146,7 @@ PYBIND11_MODULE(_C, m) {
              b.open_peers(v, my_rank);
            })
       .def("close_peers", &SymmetricBuffer::close_peers)
+      .def("release", &SymmetricBuffer::release)
       .def("local", &SymmetricBuffer::local)
       .def("peer", &SymmetricBuffer::peer)
       .def("npeers", &SymmetricBuffer::npeers)

@@ -64,11 +64,15 @@ SymmetricBuffer::SymmetricBuffer(size_t bytes, int device) : bytes_(bytes), devi
   DDLB_HIP(hipDeviceSynchronize());
 }
 
-SymmetricBuffer::~SymmetricBuffer() {
+SymmetricBuffer::~SymmetricBuffer() { release(); }
+
+void SymmetricBuffer::release() {
   close_peers();
   if (ptr_ != nullptr) {
+    hipDeviceSynchronize();
     hipFree(ptr_);
     ptr_ = nullptr;
+    (void)hipGetLastError();
   }
 }
 

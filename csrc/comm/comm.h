@@ -12,9 +12,11 @@ namespace ddlb {
 #define DDLB_HIP(x)                                                                       \
   do {                                                                                    \
     hipError_t e_ = (x);                                                                  \
-    if (e_ != hipSuccess)                                                                 \
+    if (e_ != hipSuccess) {                                                               \
+      (void)hipGetLastError(); /* do not leave a stale error for torch's next check */    \
       throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(e_) + " at " + \
                                __FILE__ + ":" + std::to_string(__LINE__) + ": " #x);      \
+    }                                                                                     \
   } while (0)
 #define DDLB_NCCL(x)                                                                       \
   do {                                                                                     \
@@ -53,6 +55,9 @@ class SymmetricBuffer {
   std::string ipc_handle() const;                       // 64 raw bytes
   void open_peers(const std::vector<std::string>& handles, int my_rank);
   void close_peers();
+  // Free the local allocation now. Call only after EVERY rank closed its mapping of it
+  // (close_peers + barrier): freeing memory a peer still maps makes the next export fail.
+  void release();
   uintptr_t local() const { return (uintptr_t)ptr_; }
   uintptr_t peer(int r) const { return (uintptr_t)peers_.at(r); }
   size_t bytes() const { return bytes_; }

@@ -162,32 +162,34 @@ void PlanExecutor::exec(const int64_t* o, hipStream_t main) {
     }
     case OP_SIGNAL: {
       const int n = (int)o[2];
-      if (n < 1 || n > kMaxSignal || 4 + n > kOpWords) throw std::runtime_error("plan: bad signal");
+      if (n < 1 || n > kMaxSignal || 5 + n > kOpWords) throw std::runtime_error("plan: bad signal");
+      const unsigned value = (unsigned)((int64_t)epoch_ + o[4]);
       if (o[3] == 1) {
-        for (int i = 0; i < n; ++i)
-          DDLB_HIP(hipStreamWriteValue32(s, (void*)o[4 + i], epoch_, 0));
+        for (int i = 0; i < n; ++i) DDLB_HIP(hipStreamWriteValue32(s, (void*)o[5 + i], value, 0));
       } else {
         SignalArgs a;
         a.n = n;
-        a.value = epoch_;
-        for (int i = 0; i < n; ++i) a.ptr[i] = (unsigned*)o[4 + i];
+        a.value = value;
+        for (int i = 0; i < n; ++i) a.ptr[i] = (unsigned*)o[5 + i];
         DDLB_HIP(signal_launch(a, s));
       }
       return;
     }
     case OP_WAIT_SIGNAL: {
       const int n = (int)o[2];
-      if (n < 1 || n > kMaxSignal || 4 + n > kOpWords) throw std::runtime_error("plan: bad wait");
+      if (n < 1 || n > kMaxSignal || 5 + n > kOpWords) throw std::runtime_error("plan: bad wait");
+      const int64_t v = (int64_t)epoch_ + o[4];
+      if (v <= 0) return;  // nothing to wait for before the first epoch
       if (o[3] == 1) {
         for (int i = 0; i < n; ++i)
-          DDLB_HIP(hipStreamWaitValue32(s, (void*)o[4 + i], epoch_, hipStreamWaitValueGte,
+          DDLB_HIP(hipStreamWaitValue32(s, (void*)o[5 + i], (unsigned)v, hipStreamWaitValueGte,
                                         0xffffffffu));
       } else {
         WaitArgs a;
         a.n = n;
-        a.value = epoch_;
+        a.value = (unsigned)v;
         a.timeout_word = d_timeout_;
-        for (int i = 0; i < n; ++i) a.ptr[i] = (unsigned*)o[4 + i];
+        for (int i = 0; i < n; ++i) a.ptr[i] = (unsigned*)o[5 + i];
         DDLB_HIP(wait_launch(a, s));
       }
       return;

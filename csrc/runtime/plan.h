@@ -36,8 +36,10 @@ enum OpKind : int64_t {
   OP_GROUP_END = 9,
   OP_COPY = 10,       // 2 dst, 3 src, 4 bytes, 5 method (0 copy engine, 1 CU kernel),
                       // 6 max CU blocks (kernel method)
-  OP_SIGNAL = 11,     // 2 n, 3 method (0 kernel, 1 stream write), 4.. flag ptrs; value = epoch
-  OP_WAIT_SIGNAL = 12,  // 2 n, 3 method (0 kernel, 1 stream wait), 4.. flag ptrs; >= epoch
+  OP_SIGNAL = 11,     // 2 n, 3 method (0 kernel, 1 stream write), 4 delta, 5.. flag ptrs;
+                      //   stores value = epoch + delta
+  OP_WAIT_SIGNAL = 12,  // 2 n, 3 method (0 kernel, 1 stream wait), 4 delta, 5.. flag ptrs;
+                        //   waits until every flag >= epoch + delta
   OP_REDUCE = 13,     // 2 dst, 3 count, 4 dtype, 5 nsrc, 6.. src ptrs
   OP_MEMSET = 14,     // 2 dst, 3 bytes, 4 byte value
   OP_COPY_MULTI = 15, // 2 nseg, 3 max blocks, then (dst, src, bytes) triples from word 4

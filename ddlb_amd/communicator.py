@@ -47,7 +47,8 @@ class Communicator:
             raise RuntimeError("DDLB_DEVICE=cuda requested but no ROCm GPU is visible")
         if use_gpu:
             ndev = torch.cuda.device_count()
-            if self.local_size > ndev:
+            shared_ok = os.environ.get("DDLB_ALLOW_SHARED_GPU", "0") == "1"
+            if self.local_size > ndev and not shared_ok:
                 raise RuntimeError(f"local size {self.local_size} exceeds visible GPUs {ndev}")
             torch.cuda.set_device(self.local_rank % ndev)
             self.device = torch.device("cuda", self.local_rank % ndev)
@@ -63,6 +64,11 @@ class Communicator:
 
     @property
     def backend(self) -> str:
+        """Control-plane backend: RCCL on GPU, gloo on CPU. ``DDLB_PG_BACKEND=gloo`` forces gloo
+        (tests that put several ranks on one GPU, where RCCL refuses duplicate devices)."""
+        forced = os.environ.get("DDLB_PG_BACKEND")
+        if forced:
+            return forced
         return "nccl" if self.is_gpu else "gloo"
 
     # ------------------------------------------------------------------ process group
@@ -80,7 +86,7 @@ class Communicator:
                 init = f"tcp://{envs.get_master_addr()}:{envs.get_master_port()}"
         kwargs = dict(backend=self.backend, rank=self.rank, world_size=self.world_size,
                       init_method=init, timeout=datetime.timedelta(seconds=timeout_s))
-        if self.is_gpu:
+        if self.is_gpu and self.backend == "nccl":
             kwargs["device_id"] = self.device
         dist.init_process_group(**kwargs)
         return dist.group.WORLD
@@ -113,7 +119,7 @@ class Communicator:
 
         self.synchronize()
         if dist.is_available() and dist.is_initialized():
-            if self.is_gpu:
+            if self.is_gpu and dist.get_backend() == "nccl":
                 dist.barrier(device_ids=[self.device.index])
             else:
                 dist.barrier()
@@ -123,7 +129,12 @@ class Communicator:
 
         if self.world_size > 1 or dist.is_initialized():
             self.ensure_process_group()
-            dist.all_reduce(tensor, op=dist.ReduceOp.MAX)
+            if tensor.is_cuda and dist.get_backend() != "nccl":
+                host = tensor.cpu()
+                dist.all_reduce(host, op=dist.ReduceOp.MAX)
+                tensor.copy_(host)
+            else:
+                dist.all_reduce(tensor, op=dist.ReduceOp.MAX)
         return tensor
 
     # ------------------------------------------------------------------ data plane

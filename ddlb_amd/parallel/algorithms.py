@@ -1,0 +1,505 @@
+"""Distributed-GEMM algorithms as plan builders (the native replacements of the nvFuser slots).
+
+Reference semantics and where each is cited:
+
+TP-Columnwise  (C[m,n] = AllGather_M(A_r[m/d,k]) @ B[k,n], rows rank-major)
+  default        AG then GEMM                          ``TPColumnwise/fuser.py:16-57``
+  coll_pipeline  s stages of (AG of m/(ds) rows from every rank || GEMM of the previous stage)
+                                                        ``TPColumnwise/fuser.py:59-100``
+  p2p_pipeline   d steps; step j computes shard (r+j)%d when offset_stream_indexing_by_rank
+                                                        ``TPColumnwise/fuser.py:102-146``
+  order=AG_after GEMM the local shard, all-gather C     ``fuser.py:200-201``
+TP-Rowwise     (out_r[m/d,n] = ReduceScatter_M(A_r[m,k/d] @ B_r[k/d,n]))
+  default        GEMM then RS                          ``TPRowwise/fuser.py:15-60``
+  coll_pipeline  s stages of (GEMM of the d row blocks of stage j || RS of stage j-1). The native
+                 layout keeps the canonical contiguous output block per rank (SURVEY.md §2.6
+                 "Row coll_pipeline" native decision): stage j reads rows {r'*m/d + j*m/(sd) + i}
+                 of A through the GEMM's grouped-row addressing — no permutation copy.
+  p2p_pipeline   d steps; partial for destination (r+j)%d computed and shipped while the next
+                 is computed; the destination sums d partials (f32) in one fused kernel.
+                                                        ``TPRowwise/fuser.py:116-169``
+
+Backends: ``rccl`` = RCCL collectives / send-recv on our own communicator and HIP streams;
+``ipc`` = HIP IPC symmetric memory over xGMI, moved by the copy engines (SDMA, protocol
+``memcpy``/``batch_memcpy``) or by CU copy kernels (``kernel``, the stand-in for NVLS
+``multimem``), synchronised with cross-process flags (READY / ACK epochs).
+
+Stream map: 0 = caller/compute, 1 = RCCL comm (high priority), 2.. = one copy stream per peer.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
+
+from ddlb_amd.parallel.plan import (COPY_ENGINE, COPY_KERNEL, DT_SIZE, DT_U8, SIG_KERNEL,
+                                    SIG_STREAM, Plan, Ref)
+
+S_MAIN, S_COMM = 0, 1
+
+
+def _s_copy(i: int) -> int:
+    return 2 + i
+
+
+@dataclass
+class AlgoConfig:
+    algorithm: str = "default"          # default | coll_pipeline | p2p_pipeline
+    backend: str = "rccl"               # rccl | ipc
+    order: str = "AG_before"            # AG_before | AG_after (columnwise)
+    s: int = 8                          # coll_pipeline stages
+    ring: bool = True                   # offset_stream_indexing_by_rank
+    protocol: str = "memcpy"            # memcpy | batch_memcpy | kernel   (ipc)
+    inter_stream_sync: bool = False     # serialise the per-peer transfers
+    signal: int = SIG_STREAM            # flag ops: stream memops (default) or kernels
+    tile: int = 0                       # GEMM tile (0 = auto)
+    mode: int = 0                       # GEMM mode (0 auto, 2 MX-fp8)
+    copy_blocks: int = 64               # CU budget of the kernel copy protocol
+    fused: bool = False                 # p2p columnwise: one flag-gated GEMM launch
+
+
+@dataclass
+class TensorLoc:
+    buf: str
+    off: int
+    rows: int
+    cols: int
+    dtype: int
+
+
+@dataclass
+class PlanIO:
+    a: TensorLoc
+    b: TensorLoc
+    out: TensorLoc
+
+
+def _nstreams(d: int) -> int:
+    return 2 + max(d - 1, 1)
+
+
+def _peer_order(rank: int, d: int, ring: bool) -> List[int]:
+    """Order of the *other* ranks: (r+1)%d, (r+2)%d, ... with ring indexing, else ascending."""
+    if ring:
+        return [(rank + j) % d for j in range(1, d)]
+    return [p for p in range(d) if p != rank]
+
+
+def _shard_order(rank: int, d: int, ring: bool) -> List[int]:
+    """Compute order of the d shards: own first (ring) or 0..d-1 (reference without offset)."""
+    if ring:
+        return [(rank + j) % d for j in range(d)]
+    return list(range(d))
+
+
+class _Flags:
+    """Named slot table inside the symmetric ``flags`` buffer (uint32 words)."""
+
+    def __init__(self, plan: Plan, d: int, s: int):
+        self.d = d
+        self.slots: Dict[str, Tuple[int, int]] = {}
+        self.words = 0
+        for name, count in (("READY", d), ("ACK", d), ("CHUNK", s * d), ("ACKS", s * d),
+                            ("ARRIVE", d)):
+            self.slots[name] = (self.words, count)
+            self.words += count
+        nbytes = max(256, ((self.words * 4 + 255) // 256) * 256)
+        plan.buffer("flags", nbytes, symmetric=True, zero=True)
+
+    def ref(self, name: str, idx: int, owner: Optional[int] = None) -> Ref:
+        base, count = self.slots[name]
+        if not 0 <= idx < count:
+            raise IndexError(f"flag {name}[{idx}] out of range")
+        return Ref("flags", 4 * (base + idx), owner)
+
+
+def _chunks(flags: List[Ref], n: int = 16):
+    for i in range(0, len(flags), n):
+        yield flags[i:i + n]
+
+
+def _signal(plan: Plan, stream: int, flags: List[Ref], cfg: AlgoConfig, delta: int = 0):
+    for c in _chunks(flags):
+        plan.signal(stream, c, method=cfg.signal, delta=delta)
+
+
+def _wait(plan: Plan, stream: int, flags: List[Ref], cfg: AlgoConfig, delta: int = 0):
+    for c in _chunks(flags):
+        plan.wait_signal(stream, c, method=cfg.signal, delta=delta)
+
+
+# =====================================================================================
+#  TP-Columnwise
+# =====================================================================================
+def check_columnwise(d: int, m: int, n: int, k: int, cfg: AlgoConfig) -> None:
+    if m % d:
+        raise ValueError(f"m ({m}) must be divisible by world_size ({d})")
+    if cfg.algorithm == "coll_pipeline" and m % (d * cfg.s):
+        raise ValueError(f"m ({m}) must be divisible by s*world_size ({cfg.s}*{d}) for "
+                         "coll_pipeline")
+    if cfg.algorithm not in ("default", "coll_pipeline", "p2p_pipeline"):
+        raise ValueError(f"unknown algorithm {cfg.algorithm}")
+    if cfg.backend not in ("rccl", "ipc"):
+        raise ValueError(f"unknown backend {cfg.backend}")
+    if cfg.protocol not in ("memcpy", "batch_memcpy", "kernel"):
+        raise ValueError(f"unknown protocol {cfg.protocol}")
+    if d > 17:
+        raise ValueError("at most 17 ranks per node are supported by the flag/reduce ops")
+
+
+def build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, dout: int,
+                        cfg: AlgoConfig) -> Tuple[Plan, PlanIO]:
+    check_columnwise(d, m, n, k, cfg)
+    ein, eout = DT_SIZE[din], DT_SIZE[dout]
+    ml = m // d
+    plan = Plan(rank, d, nstreams=_nstreams(d), stream_priority=[0, 1] + [1] * max(d - 1, 1))
+    plan.meta.update(primitive="tp_columnwise", algorithm=cfg.algorithm, backend=cfg.backend,
+                     order=cfg.order)
+    A = plan.buffer("A_full", m * k * ein, symmetric=(cfg.backend == "ipc" or d > 1))
+    Bt = plan.buffer("Bt", n * k * ein)
+    flags = _Flags(plan, d, max(cfg.s, 1)) if cfg.backend == "ipc" and d > 1 else None
+    gdt = dict(din=din, dout=dout, tile=cfg.tile, mode=cfg.mode)
+    comm_dt = DT_U8 if ein == 1 else din   # fp8 moves as bytes
+
+    def arow(r0: int) -> Ref:
+        return A + r0 * k * ein
+
+    if cfg.order == "AG_after":
+        C = plan.buffer("C_full", m * n * eout, symmetric=True)
+        io = PlanIO(TensorLoc("A_full", rank * ml * k * ein, ml, k, din),
+                    TensorLoc("Bt", 0, n, k, din), TensorLoc("C_full", 0, m, n, dout))
+        _col_ag_after(plan, rank, d, m, n, k, ein, eout, dout, cfg, A, Bt, C, flags, gdt)
+        return plan, io
+
+    C = plan.buffer("C", m * n * eout)
+    io = PlanIO(TensorLoc("A_full", rank * ml * k * ein, ml, k, din),
+                TensorLoc("Bt", 0, n, k, din), TensorLoc("C", 0, m, n, dout))
+
+    def crow(r0: int) -> Ref:
+        return C + r0 * n * eout
+
+    def gemm(stream, a_ref, c_ref, M, **kw):
+        plan.gemm(stream, a_ref, Bt, c_ref, M=M, N=n, K=k, lda=k, ldb=k, ldc=n, **gdt, **kw)
+
+    if d == 1:
+        gemm(S_MAIN, A, C, m)
+        return plan, io
+
+    alg, be = cfg.algorithm, cfg.backend
+    if alg == "default" and be == "rccl":
+        plan.allgather(S_MAIN, arow(rank * ml), A, ml * k, comm_dt)
+        gemm(S_MAIN, A, C, m)
+    elif alg == "default" and be == "ipc":
+        done = _ipc_pull_shards(plan, rank, d, cfg, flags, [(p, [(p * ml, ml)]) for p in
+                                                             _peer_order(rank, d, cfg.ring)],
+                                lambda r0: arow(r0), k * ein)
+        for ev in done.values():
+            for e in ev:
+                plan.wait(S_MAIN, e)
+        gemm(S_MAIN, A, C, m)
+        _wait(plan, S_MAIN, [flags.ref("ACK", p) for p in range(d) if p != rank], cfg)
+    elif alg == "coll_pipeline" and be == "rccl":
+        rows = ml // cfg.s
+        for j in range(cfg.s):
+            stg = plan.buffer(f"STG{j}", d * rows * k * ein)
+            plan.allgather(S_COMM, arow(rank * ml + j * rows), stg, rows * k, comm_dt)
+            e = plan.event()
+            plan.record(S_COMM, e)
+            plan.wait(S_MAIN, e)
+            gemm(S_MAIN, stg, crow(j * rows), d * rows, c_grp=rows, c_gstride=ml)
+    elif alg == "coll_pipeline" and be == "ipc":
+        rows = ml // cfg.s
+        peers = _peer_order(rank, d, cfg.ring)
+        jobs = [(p, [(p * ml + j * rows, rows) for j in range(cfg.s)]) for p in peers]
+        done = _ipc_pull_shards(plan, rank, d, cfg, flags, jobs, lambda r0: arow(r0), k * ein)
+        for j in range(cfg.s):
+            for p in peers:
+                plan.wait(S_MAIN, done[p][j])
+            gemm(S_MAIN, arow(j * rows), crow(j * rows), d * rows, a_grp=rows, a_gstride=ml,
+                 c_grp=rows, c_gstride=ml)
+        _wait(plan, S_MAIN, [flags.ref("ACK", p) for p in range(d) if p != rank], cfg)
+    elif alg == "p2p_pipeline" and be == "ipc":
+        order = _shard_order(rank, d, cfg.ring)
+        peers = [p for p in order if p != rank]
+        done = _ipc_pull_shards(plan, rank, d, cfg, flags, [(p, [(p * ml, ml)]) for p in peers],
+                                lambda r0: arow(r0), k * ein,
+                                arrive=flags.ref if cfg.fused else None)
+        if cfg.fused:
+            _signal(plan, S_MAIN, [flags.ref("ARRIVE", rank)], cfg)
+            gemm(S_MAIN, A, C, m, flags=flags.ref("ARRIVE", 0), flag_rows=ml, nshards=d,
+                 first_shard=order[0], tile_order=1)
+        else:
+            for p in order:
+                if p != rank:
+                    plan.wait(S_MAIN, done[p][0])
+                gemm(S_MAIN, arow(p * ml), crow(p * ml), ml)
+        _wait(plan, S_MAIN, [flags.ref("ACK", p) for p in range(d) if p != rank], cfg)
+    elif alg == "p2p_pipeline" and be == "rccl":
+        # pairwise exchange steps: step j sends my shard to r-j, receives shard r+j
+        evs = {}
+        for j in range(1, d):
+            to, frm = (rank - j) % d, (rank + j) % d
+            plan.group_start(S_COMM)
+            plan.send(S_COMM, arow(rank * ml), ml * k, comm_dt, to)
+            plan.recv(S_COMM, arow(frm * ml), ml * k, comm_dt, frm)
+            plan.group_end(S_COMM)
+            e = plan.event()
+            plan.record(S_COMM, e)
+            evs[frm] = e
+        for p in [(rank + j) % d for j in range(d)]:
+            if p != rank:
+                plan.wait(S_MAIN, evs[p])
+            gemm(S_MAIN, arow(p * ml), crow(p * ml), ml)
+    else:  # pragma: no cover
+        raise ValueError(f"unsupported combination {alg}/{be}")
+    return plan, io
+
+
+def _ipc_pull_shards(plan: Plan, rank: int, d: int, cfg: AlgoConfig, flags: _Flags,
+                     jobs, row_ref, row_bytes: int, arrive=None):
+    """Pull row blocks of the symmetric buffer from peers into the same rows locally.
+
+    ``jobs`` = [(peer, [(row0, nrows), ...]), ...] in issue order. Returns
+    ``{peer: [event after block i]}``. Protocol: READY[peer] is waited before the first read of
+    that peer; ACK is sent to the peer after the last block has landed (the peer may then
+    overwrite its shard).
+    """
+    _signal(plan, S_MAIN, [flags.ref("READY", rank, owner=p) for p in range(d) if p != rank], cfg)
+    done: Dict[int, List[int]] = {}
+    if cfg.protocol == "kernel":
+        # one CU copy kernel per block index, reading every peer (copy_multi, <= 8 segments)
+        st = _s_copy(0)
+        _wait(plan, st, [flags.ref("READY", p) for p, _ in jobs], cfg)
+        nblk = len(jobs[0][1])
+        for b in range(nblk):
+            segs = []
+            for p, blocks in jobs:
+                r0, nr = blocks[b]
+                segs.append((row_ref(r0), row_ref(r0).at(p), nr * row_bytes))
+            for i in range(0, len(segs), 8):
+                plan.copy_multi(st, segs[i:i + 8], max_blocks=cfg.copy_blocks)
+            e = plan.event()
+            plan.record(st, e)
+            for p, _ in jobs:
+                done.setdefault(p, []).append(e)
+        if arrive is not None:
+            _signal(plan, st, [arrive("ARRIVE", p) for p, _ in jobs], cfg)
+        _signal(plan, st, [flags.ref("ACK", rank, owner=p) for p, _ in jobs], cfg)
+        return done
+    prev_last = None
+    for idx, (p, blocks) in enumerate(jobs):
+        st = _s_copy(0) if cfg.protocol == "batch_memcpy" else _s_copy(idx)
+        if cfg.inter_stream_sync and prev_last is not None and cfg.protocol != "batch_memcpy":
+            plan.wait(st, prev_last)
+        _wait(plan, st, [flags.ref("READY", p)], cfg)
+        for (r0, nr) in blocks:
+            plan.copy(st, row_ref(r0), row_ref(r0).at(p), nr * row_bytes, method=COPY_ENGINE)
+            e = plan.event()
+            plan.record(st, e)
+            done.setdefault(p, []).append(e)
+        prev_last = done[p][-1]
+        if arrive is not None:
+            _signal(plan, st, [arrive("ARRIVE", p)], cfg)
+        _signal(plan, st, [flags.ref("ACK", rank, owner=p)], cfg)
+    return done
+
+
+def _col_ag_after(plan, rank, d, m, n, k, ein, eout, dout, cfg, A, Bt, C, flags, gdt):
+    ml = m // d
+    comm_dt = dout
+
+    def gemm(stream, r0, M):
+        plan.gemm(stream, A + r0 * k * ein, Bt, C + r0 * n * eout, M=M, N=n, K=k, lda=k, ldb=k,
+                  ldc=n, **gdt)
+
+    if d == 1:
+        gemm(S_MAIN, 0, m)
+        return
+    alg, be = cfg.algorithm, cfg.backend
+    nch = cfg.s if alg == "coll_pipeline" else 1
+    if alg == "coll_pipeline" and ml % nch:
+        raise ValueError("m/d must be divisible by s")
+    rows = ml // nch
+    if be == "rccl":
+        if alg == "default":
+            gemm(S_MAIN, rank * ml, ml)
+            plan.allgather(S_MAIN, C + rank * ml * n * eout, C, ml * n, comm_dt)
+            return
+        for j in range(nch):
+            gemm(S_MAIN, rank * ml + j * rows, rows)
+            plan.edge(S_MAIN, S_COMM)
+            plan.group_start(S_COMM)
+            for p in range(d):
+                if p == rank:
+                    continue
+                plan.send(S_COMM, C + (rank * ml + j * rows) * n * eout, rows * n, comm_dt, p)
+                plan.recv(S_COMM, C + (p * ml + j * rows) * n * eout, rows * n, comm_dt, p)
+            plan.group_end(S_COMM)
+        return
+    # ipc: chunk-ready flags per chunk, peers pull the chunk rows of C
+    peers = _peer_order(rank, d, cfg.ring)
+    _wait(plan, S_MAIN, [flags.ref("ACK", p) for p in peers], cfg, delta=-1)
+    for j in range(nch):
+        gemm(S_MAIN, rank * ml + j * rows, rows)
+        _signal(plan, S_MAIN, [flags.ref("CHUNK", j * d + rank, owner=p) for p in peers], cfg)
+    evs = []
+    for idx, p in enumerate(peers):
+        st = _s_copy(0) if cfg.protocol == "batch_memcpy" else _s_copy(idx)
+        for j in range(nch):
+            _wait(plan, st, [flags.ref("CHUNK", j * d + p)], cfg)
+            r0 = p * ml + j * rows
+            off = r0 * n * eout
+            if cfg.protocol == "kernel":
+                plan.copy(st, C + off, (C + off).at(p), rows * n * eout, method=COPY_KERNEL,
+                          max_blocks=cfg.copy_blocks)
+            else:
+                plan.copy(st, C + off, (C + off).at(p), rows * n * eout)
+        _signal(plan, st, [flags.ref("ACK", rank, owner=p)], cfg)
+        e = plan.event()
+        plan.record(st, e)
+        evs.append(e)
+    for e in evs:
+        plan.wait(S_MAIN, e)
+
+
+# =====================================================================================
+#  TP-Rowwise
+# =====================================================================================
+def check_rowwise(d: int, m: int, n: int, k: int, cfg: AlgoConfig) -> None:
+    if m % d or k % d:
+        raise ValueError(f"m ({m}) and k ({k}) must be divisible by world_size ({d})")
+    if cfg.algorithm == "coll_pipeline" and m % (d * cfg.s):
+        raise ValueError(f"m ({m}) must be divisible by s*world_size ({cfg.s}*{d})")
+    if cfg.algorithm not in ("default", "coll_pipeline", "p2p_pipeline"):
+        raise ValueError(f"unknown algorithm {cfg.algorithm}")
+    if cfg.backend not in ("rccl", "ipc"):
+        raise ValueError(f"unknown backend {cfg.backend}")
+    if d > 16:
+        raise ValueError("at most 16 ranks per node are supported by the reduce op")
+
+
+def build_tp_rowwise(rank: int, d: int, m: int, n: int, k: int, din: int, dout: int,
+                     cfg: AlgoConfig) -> Tuple[Plan, PlanIO]:
+    check_rowwise(d, m, n, k, cfg)
+    ein, eout = DT_SIZE[din], DT_SIZE[dout]
+    kl, ml = k // d, m // d
+    plan = Plan(rank, d, nstreams=_nstreams(d), stream_priority=[0, 1] + [1] * max(d - 1, 1))
+    plan.meta.update(primitive="tp_rowwise", algorithm=cfg.algorithm, backend=cfg.backend)
+    A = plan.buffer("A", m * kl * ein)
+    Bt = plan.buffer("Bt", n * kl * ein)
+    OUT = plan.buffer("OUT", ml * n * eout)
+    io = PlanIO(TensorLoc("A", 0, m, kl, din), TensorLoc("Bt", 0, n, kl, din),
+                TensorLoc("OUT", 0, ml, n, dout))
+    flags = _Flags(plan, d, max(cfg.s, 1)) if cfg.backend == "ipc" and d > 1 else None
+    gdt = dict(din=din, dout=dout, tile=cfg.tile, mode=cfg.mode)
+    blk = ml * n * eout   # bytes of one [m/d, n] output block
+
+    def gemm(stream, a_row0, c_ref, M, **kw):
+        plan.gemm(stream, A + a_row0 * kl * ein, Bt, c_ref, M=M, N=n, K=kl, lda=kl, ldb=kl, ldc=n,
+                  **gdt, **kw)
+
+    if d == 1:
+        gemm(S_MAIN, 0, OUT, m)
+        return plan, io
+    alg, be = cfg.algorithm, cfg.backend
+    peers = _peer_order(rank, d, cfg.ring)
+    if alg == "default" and be == "rccl":
+        P = plan.buffer("P", m * n * eout)
+        gemm(S_MAIN, 0, P, m)
+        plan.reduce_scatter(S_MAIN, P, OUT, ml * n, dout)
+    elif alg == "default" and be == "ipc":
+        P = plan.buffer("P", m * n * eout, symmetric=True)
+        _wait(plan, S_MAIN, [flags.ref("ACK", p) for p in peers], cfg, delta=-1)
+        gemm(S_MAIN, 0, P, m)
+        _signal(plan, S_MAIN, [flags.ref("READY", rank, owner=p) for p in peers], cfg)
+        _wait(plan, S_MAIN, [flags.ref("READY", p) for p in peers], cfg)
+        srcs = _row_gather_sources(plan, rank, d, cfg, P + rank * blk, blk, peers, "RCV")
+        plan.reduce(S_MAIN, OUT, srcs, ml * n, dout)
+        _signal(plan, S_MAIN, [flags.ref("ACK", rank, owner=p) for p in peers], cfg)
+    elif alg == "coll_pipeline" and be == "rccl":
+        rows = ml // cfg.s
+        for j in range(cfg.s):
+            stg = plan.buffer(f"STG{j}", d * rows * n * eout)
+            gemm(S_MAIN, j * rows, stg, d * rows, a_grp=rows, a_gstride=ml)
+            plan.edge(S_MAIN, S_COMM)
+            plan.reduce_scatter(S_COMM, stg, OUT + j * rows * n * eout, rows * n, dout)
+    elif alg == "coll_pipeline" and be == "ipc":
+        rows = ml // cfg.s
+        sblk = rows * n * eout
+        for j in range(cfg.s):
+            stg = plan.buffer(f"STG{j}", d * sblk, symmetric=True)
+            _wait(plan, S_MAIN, [flags.ref("ACKS", j * d + p) for p in peers], cfg, delta=-1)
+            gemm(S_MAIN, j * rows, stg, d * rows, a_grp=rows, a_gstride=ml)
+            plan.edge(S_MAIN, S_COMM)
+            _signal(plan, S_COMM, [flags.ref("CHUNK", j * d + rank, owner=p) for p in peers], cfg)
+            _wait(plan, S_COMM, [flags.ref("CHUNK", j * d + p) for p in peers], cfg)
+            srcs = [stg + rank * sblk] + [(stg + rank * sblk).at(p) for p in peers]
+            plan.reduce(S_COMM, OUT + j * sblk, srcs, rows * n, dout)
+            _signal(plan, S_COMM, [flags.ref("ACKS", j * d + rank, owner=p) for p in peers], cfg)
+    elif alg == "p2p_pipeline" and be == "ipc":
+        PST = plan.buffer("PST", d * blk)
+        RECV = plan.buffer("RECV", d * blk, symmetric=True)
+        evs = {}
+        for p in peers:                        # peers' partials first, shipped as they finish
+            gemm(S_MAIN, p * ml, PST + p * blk, ml)
+            e = plan.event()
+            plan.record(S_MAIN, e)
+            evs[p] = e
+        prev = None
+        for idx, p in enumerate(peers):
+            st = _s_copy(0) if cfg.protocol == "batch_memcpy" else _s_copy(idx)
+            plan.wait(st, evs[p])
+            if cfg.inter_stream_sync and prev is not None and cfg.protocol != "batch_memcpy":
+                plan.wait(st, prev)
+            _wait(plan, st, [flags.ref("ACK", p)], cfg, delta=-1)
+            method = COPY_KERNEL if cfg.protocol == "kernel" else COPY_ENGINE
+            plan.copy(st, (RECV + rank * blk).at(p), PST + p * blk, blk, method=method,
+                      max_blocks=cfg.copy_blocks)
+            _signal(plan, st, [flags.ref("READY", rank, owner=p)], cfg)
+            prev = plan.event()
+            plan.record(st, prev)
+        gemm(S_MAIN, rank * ml, RECV + rank * blk, ml)   # own block last, straight into RECV
+        _wait(plan, S_MAIN, [flags.ref("READY", p) for p in peers], cfg)
+        plan.reduce(S_MAIN, OUT, [RECV + q * blk for q in range(d)], ml * n, dout)
+        _signal(plan, S_MAIN, [flags.ref("ACK", rank, owner=p) for p in peers], cfg)
+    elif alg == "p2p_pipeline" and be == "rccl":
+        PST = plan.buffer("PST", d * blk)
+        RECV = plan.buffer("RECV", d * blk)
+        evs = {}
+        for j in range(1, d):
+            dst = (rank + j) % d
+            gemm(S_MAIN, dst * ml, PST + dst * blk, ml)
+            e = plan.event()
+            plan.record(S_MAIN, e)
+            evs[j] = e
+        for j in range(1, d):
+            to, frm = (rank + j) % d, (rank - j) % d
+            plan.wait(S_COMM, evs[j])
+            plan.group_start(S_COMM)
+            plan.send(S_COMM, PST + to * blk, ml * n, dout, to)
+            plan.recv(S_COMM, RECV + frm * blk, ml * n, dout, frm)
+            plan.group_end(S_COMM)
+        gemm(S_MAIN, rank * ml, RECV + rank * blk, ml)
+        plan.edge(S_COMM, S_MAIN)
+        plan.reduce(S_MAIN, OUT, [RECV + q * blk for q in range(d)], ml * n, dout)
+    else:  # pragma: no cover
+        raise ValueError(f"unsupported combination {alg}/{be}")
+    return plan, io
+
+
+def _row_gather_sources(plan, rank, d, cfg, own_ref, blk, peers, stage_name):
+    """Sources of this rank's output block: direct peer reads (kernel) or SDMA pulls (memcpy)."""
+    if cfg.protocol == "kernel":
+        return [own_ref] + [own_ref.at(p) for p in peers]
+    R = plan.buffer(stage_name, d * blk)
+    evs = []
+    for idx, p in enumerate(peers):
+        st = _s_copy(0) if cfg.protocol == "batch_memcpy" else _s_copy(idx)
+        plan.edge(S_MAIN, st)
+        plan.copy(st, R + p * blk, own_ref.at(p), blk)
+        e = plan.event()
+        plan.record(st, e)
+        evs.append(e)
+    for e in evs:
+        plan.wait(S_MAIN, e)
+    return [own_ref] + [R + p * blk for p in peers]

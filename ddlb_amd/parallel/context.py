@@ -1,0 +1,179 @@
+"""Native data-plane context: our RCCL communicator, IPC symmetric buffers, bound plans.
+
+* :class:`NativeContext` — per-process; the RCCL ``ncclUniqueId`` and the IPC handles are exchanged
+  over the control-plane process group (torch.distributed), the data plane never touches it.
+* :class:`SymmetricBuffer` — one ``hipMalloc`` per rank, every peer's copy IPC-mapped (HIP IPC,
+  dmabuf mode), exposed to torch through DLPack.
+* :class:`BoundPlan` — a :class:`~ddlb_amd.parallel.plan.Plan` with its buffers allocated, its
+  symbolic refs resolved to device addresses and loaded into a C++ ``PlanExecutor``; ``run()`` is
+  a single native call that enqueues the whole schedule behind the caller's HIP stream.
+"""
+
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+from ddlb_amd.parallel.plan import (OP_ALLGATHER, OP_RECV, OP_REDUCE_SCATTER, OP_SEND, DT_SIZE,
+                                    Plan, Ref)
+from ddlb_amd.parallel.sim import TORCH_DT
+
+
+class SymmetricBuffer:
+    def __init__(self, ctx: "NativeContext", nbytes: int, zero: bool = True):
+        import torch
+        import torch.distributed as dist
+
+        self.ctx = ctx
+        self.nbytes = int(nbytes)
+        C = ctx.C
+        self.h = C.SymmetricBuffer(self.nbytes, ctx.device_index)  # zero-filled by hipMemset
+        handles: List = [None] * ctx.world
+        mine = bytes(self.h.ipc_handle())
+        if ctx.world > 1:
+            dist.all_gather_object(handles, mine)
+        else:
+            handles = [mine]
+        self.h.open_peers(handles, ctx.rank)
+        self.tensor = torch.from_dlpack(C.buffer_dlpack(self.h, ctx.device_index))
+
+    def ptr(self, owner: Optional[int] = None) -> int:
+        return self.h.local() if owner is None or owner == self.ctx.rank else self.h.peer(owner)
+
+    def close_peers(self) -> None:
+        if self.h is not None:
+            self.h.close_peers()
+
+    def release(self) -> None:
+        """Free now. Every rank must have closed its mapping first (see BoundPlan.close)."""
+        self.tensor = None
+        if self.h is not None:
+            self.h.release()
+            self.h = None
+
+    def close(self) -> None:
+        self.close_peers()
+        self.release()
+
+
+class NativeContext:
+    def __init__(self, communicator):
+        from ddlb_amd.ops import load
+
+        if not communicator.is_gpu:
+            raise RuntimeError("the native data plane needs a ROCm GPU")
+        self.C = load()
+        self.comm = communicator
+        self.rank = communicator.rank
+        self.world = communicator.world_size
+        self.device_index = communicator.device.index
+        self._rccl = None
+        self._owned: List = []
+
+    def rccl(self):
+        """Our own RCCL communicator (lazily created, collective over all ranks)."""
+        import torch.distributed as dist
+
+        if self._rccl is None:
+            obj = [bytes(self.C.RcclComm.unique_id()) if self.rank == 0 else None]
+            if self.world > 1:
+                dist.broadcast_object_list(obj, src=0)
+            self._rccl = self.C.RcclComm(obj[0], self.world, self.rank, self.device_index)
+        return self._rccl
+
+    def symmetric(self, nbytes: int) -> SymmetricBuffer:
+        buf = SymmetricBuffer(self, nbytes)
+        self._owned.append(buf)
+        return buf
+
+    def release_symmetric(self, bufs) -> None:
+        """Collective teardown: unmap peers everywhere, barrier, then free locally."""
+        import torch
+
+        torch.cuda.synchronize()
+        for b in bufs:
+            b.close_peers()
+        if self.world > 1:
+            self.comm.barrier()
+        for b in bufs:
+            b.release()
+        self._owned = [b for b in self._owned if b.h is not None]
+
+    def bind(self, plan: Plan) -> "BoundPlan":
+        return BoundPlan(self, plan)
+
+    def close(self) -> None:
+        for b in self._owned:
+            b.close()
+        self._owned = []
+        if self._rccl is not None:
+            try:
+                self._rccl.destroy()
+            finally:
+                self._rccl = None
+
+
+class BoundPlan:
+    def __init__(self, ctx: NativeContext, plan: Plan):
+        import torch
+
+        self.ctx, self.plan = ctx, plan
+        self.local: Dict[str, torch.Tensor] = {}
+        self.sym: Dict[str, SymmetricBuffer] = {}
+        dev = torch.device("cuda", ctx.device_index)
+        for name, spec in plan.buffers.items():  # dict order == identical on every rank
+            if spec.symmetric:
+                self.sym[name] = ctx.symmetric(spec.nbytes)
+            else:
+                self.local[name] = torch.zeros(max(spec.nbytes, 16), dtype=torch.uint8,
+                                               device=dev)
+        words = plan.encode(self.resolve)
+        C = ctx.C
+        self.ex = C.PlanExecutor(ctx.device_index, plan.nstreams, max(plan.nevents, 1),
+                                 list(plan.stream_priority))
+        self.ex.load(words)
+        if any(op.kind in (OP_ALLGATHER, OP_REDUCE_SCATTER, OP_SEND, OP_RECV) for op in plan.ops):
+            self.ex.set_comm(ctx.rccl())
+        torch.cuda.synchronize(dev)
+
+    def resolve(self, ref: Ref) -> int:
+        if ref.buf in self.sym:
+            base = self.sym[ref.buf].ptr(ref.owner)
+            size = self.sym[ref.buf].nbytes
+        else:
+            if ref.owner is not None and ref.owner != self.ctx.rank:
+                raise ValueError(f"buffer {ref.buf} is local; cannot address rank {ref.owner}")
+            base = self.local[ref.buf].data_ptr()
+            size = self.local[ref.buf].numel()
+        if not 0 <= ref.off <= size:
+            raise ValueError(f"ref {ref} outside buffer of {size} bytes")
+        return base + ref.off
+
+    def buffer(self, name: str):
+        return self.sym[name].tensor if name in self.sym else self.local[name]
+
+    def view(self, loc):
+        """Typed ``[rows, cols]`` tensor view of a :class:`TensorLoc`."""
+        raw = self.buffer(loc.buf)
+        n = loc.rows * loc.cols * DT_SIZE[loc.dtype]
+        return raw[loc.off:loc.off + n].view(TORCH_DT[loc.dtype]).view(loc.rows, loc.cols)
+
+    def run(self, stream: Optional[int] = None) -> int:
+        import torch
+
+        if stream is None:
+            stream = torch.cuda.current_stream().cuda_stream
+        return self.ex.run(stream)
+
+    def check_health(self) -> None:
+        code = self.ex.read_timeout()
+        if code:
+            raise RuntimeError(f"native plan: a bounded spin gave up (code {code}); a peer did not "
+                               "signal in time")
+
+    def close(self) -> None:
+        import torch
+
+        torch.cuda.synchronize()
+        self.ex = None
+        self.ctx.release_symmetric(list(self.sym.values()))
+        self.sym, self.local = {}, {}

@@ -1,0 +1,243 @@
+"""Plan IR: the host-side schedule of a distributed-GEMM algorithm.
+
+The reference expresses its pipelines as nvFuser fusions that the MultiDeviceExecutor lowers to a
+host IR of per-stream collectives + matmuls (``ddlb/primitives/TPColumnwise/fuser.py:59-146``,
+``TPRowwise/fuser.py:62-169``). Here an algorithm is a Python function that emits a :class:`Plan`:
+a flat op list over **named buffers** and a fixed set of HIP streams. The same plan is
+
+* encoded to int64 words and executed by the native C++ ``PlanExecutor`` (one call per run), and
+* interpreted by :mod:`ddlb_amd.parallel.sim` on the CPU (d simulated ranks, byte-exact
+  buffers) with a happens-before race checker — the test bed for the layout math when no
+  multi-GPU node is at hand.
+
+Pointers are symbolic :class:`Ref` ``(buffer, byte offset, owner rank)``; ``owner=None`` means the
+local copy, an integer means that peer's copy of a *symmetric* buffer (IPC-mapped).
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+OP_WORDS = 32
+(OP_NOP, OP_GEMM, OP_RECORD, OP_WAIT, OP_ALLGATHER, OP_REDUCE_SCATTER, OP_SEND, OP_RECV,
+ OP_GROUP_START, OP_GROUP_END, OP_COPY, OP_SIGNAL, OP_WAIT_SIGNAL, OP_REDUCE, OP_MEMSET,
+ OP_COPY_MULTI) = range(16)
+OP_NAMES = {OP_NOP: "nop", OP_GEMM: "gemm", OP_RECORD: "record", OP_WAIT: "wait",
+            OP_ALLGATHER: "allgather", OP_REDUCE_SCATTER: "reduce_scatter", OP_SEND: "send",
+            OP_RECV: "recv", OP_GROUP_START: "group_start", OP_GROUP_END: "group_end",
+            OP_COPY: "copy", OP_SIGNAL: "signal", OP_WAIT_SIGNAL: "wait_signal",
+            OP_REDUCE: "reduce", OP_MEMSET: "memset", OP_COPY_MULTI: "copy_multi"}
+
+# dtype codes (csrc/gemm/gemm.h)
+DT_F32, DT_F16, DT_BF16, DT_FP8, DT_F64, DT_U8 = 0, 1, 2, 3, 4, 5
+DT_SIZE = {DT_F32: 4, DT_F16: 2, DT_BF16: 2, DT_FP8: 1, DT_F64: 8, DT_U8: 1}
+DT_NAME = {DT_F32: "float32", DT_F16: "float16", DT_BF16: "bfloat16", DT_FP8: "float8_e4m3fn",
+           DT_F64: "float64", DT_U8: "uint8"}
+NAME_DT = {v: k for k, v in DT_NAME.items()}
+
+# copy / signal methods
+COPY_ENGINE, COPY_KERNEL = 0, 1
+SIG_KERNEL, SIG_STREAM = 0, 1
+
+
+@dataclass(frozen=True)
+class Ref:
+    buf: str
+    off: int = 0          # bytes
+    owner: Optional[int] = None  # None = local; rank = that rank's copy (symmetric buffers)
+
+    def __add__(self, nbytes: int) -> "Ref":
+        return Ref(self.buf, self.off + int(nbytes), self.owner)
+
+    def at(self, owner: Optional[int]) -> "Ref":
+        return Ref(self.buf, self.off, owner)
+
+
+@dataclass
+class BufferSpec:
+    name: str
+    nbytes: int
+    symmetric: bool = False
+    zero: bool = False          # must start zeroed (flags)
+
+
+@dataclass
+class Op:
+    kind: int
+    stream: int
+    args: Dict = field(default_factory=dict)
+
+    @property
+    def name(self) -> str:
+        return OP_NAMES[self.kind]
+
+
+class Plan:
+    """Op list + buffer declarations for ONE rank."""
+
+    def __init__(self, rank: int, world: int, nstreams: int = 1,
+                 stream_priority: Optional[Sequence[int]] = None):
+        self.rank, self.world = rank, world
+        self.nstreams = nstreams
+        self.stream_priority = list(stream_priority or [0] * nstreams)
+        self.ops: List[Op] = []
+        self.buffers: Dict[str, BufferSpec] = {}
+        self.nevents = 0
+        self.meta: Dict = {}
+
+    # ------------------------------------------------------------------ declarations
+    def buffer(self, name: str, nbytes: int, symmetric: bool = False, zero: bool = False) -> Ref:
+        nbytes = int(nbytes)
+        if name in self.buffers:
+            b = self.buffers[name]
+            if b.nbytes != nbytes or b.symmetric != symmetric:
+                raise ValueError(f"buffer {name} redeclared differently")
+        else:
+            self.buffers[name] = BufferSpec(name, nbytes, symmetric, zero)
+        return Ref(name, 0, None)
+
+    def event(self) -> int:
+        self.nevents += 1
+        return self.nevents - 1
+
+    def _add(self, kind, stream, **args) -> Op:
+        if not 0 <= stream < self.nstreams:
+            raise ValueError(f"stream {stream} out of range (nstreams={self.nstreams})")
+        op = Op(kind, stream, args)
+        self.ops.append(op)
+        return op
+
+    # ------------------------------------------------------------------ ops
+    def gemm(self, stream: int, a: Ref, b: Ref, c: Ref, *, M: int, N: int, K: int, lda: int,
+             ldb: int, ldc: int, din: int, dout: int, a_grp: int = 0, a_gstride: int = 0,
+             c_grp: int = 0, c_gstride: int = 0, tile: int = 0, mode: int = 0,
+             flags: Optional[Ref] = None, flag_rows: int = 0, nshards: int = 1,
+             first_shard: int = 0, tile_order: int = 0) -> Op:
+        return self._add(OP_GEMM, stream, a=a, b=b, c=c, M=M, N=N, K=K, lda=lda, ldb=ldb, ldc=ldc,
+                         din=din, dout=dout, a_grp=a_grp, a_gstride=a_gstride, c_grp=c_grp,
+                         c_gstride=c_gstride, tile=tile, mode=mode, flags=flags,
+                         flag_rows=flag_rows, nshards=nshards, first_shard=first_shard,
+                         tile_order=tile_order)
+
+    def record(self, stream: int, event: int) -> Op:
+        return self._add(OP_RECORD, stream, event=event)
+
+    def wait(self, stream: int, event: int) -> Op:
+        return self._add(OP_WAIT, stream, event=event)
+
+    def edge(self, src_stream: int, dst_stream: int) -> None:
+        """Make everything queued so far on ``src_stream`` precede later ops of ``dst_stream``."""
+        if src_stream == dst_stream:
+            return
+        e = self.event()
+        self.record(src_stream, e)
+        self.wait(dst_stream, e)
+
+    def allgather(self, stream: int, send: Ref, recv: Ref, count: int, dtype: int) -> Op:
+        return self._add(OP_ALLGATHER, stream, send=send, recv=recv, count=count, dtype=dtype)
+
+    def reduce_scatter(self, stream: int, send: Ref, recv: Ref, count: int, dtype: int) -> Op:
+        return self._add(OP_REDUCE_SCATTER, stream, send=send, recv=recv, count=count, dtype=dtype)
+
+    def send(self, stream: int, buf: Ref, count: int, dtype: int, peer: int) -> Op:
+        return self._add(OP_SEND, stream, buf=buf, count=count, dtype=dtype, peer=peer)
+
+    def recv(self, stream: int, buf: Ref, count: int, dtype: int, peer: int) -> Op:
+        return self._add(OP_RECV, stream, buf=buf, count=count, dtype=dtype, peer=peer)
+
+    def group_start(self, stream: int) -> Op:
+        return self._add(OP_GROUP_START, stream)
+
+    def group_end(self, stream: int) -> Op:
+        return self._add(OP_GROUP_END, stream)
+
+    def copy(self, stream: int, dst: Ref, src: Ref, nbytes: int, method: int = COPY_ENGINE,
+             max_blocks: int = 0) -> Op:
+        return self._add(OP_COPY, stream, dst=dst, src=src, nbytes=int(nbytes), method=method,
+                         max_blocks=max_blocks)
+
+    def copy_multi(self, stream: int, segs: Sequence[Tuple[Ref, Ref, int]],
+                   max_blocks: int = 0) -> Op:
+        if not 1 <= len(segs) <= 8:
+            raise ValueError("copy_multi takes 1..8 segments")
+        return self._add(OP_COPY_MULTI, stream, segs=list(segs), max_blocks=max_blocks)
+
+    def signal(self, stream: int, flags: Sequence[Ref], method: int = SIG_STREAM,
+               delta: int = 0) -> Op:
+        if not 1 <= len(flags) <= 16:
+            raise ValueError("signal takes 1..16 flags")
+        return self._add(OP_SIGNAL, stream, flags=list(flags), method=method, delta=delta)
+
+    def wait_signal(self, stream: int, flags: Sequence[Ref], method: int = SIG_STREAM,
+                    delta: int = 0) -> Op:
+        if not 1 <= len(flags) <= 16:
+            raise ValueError("wait_signal takes 1..16 flags")
+        return self._add(OP_WAIT_SIGNAL, stream, flags=list(flags), method=method, delta=delta)
+
+    def reduce(self, stream: int, dst: Ref, srcs: Sequence[Ref], count: int, dtype: int) -> Op:
+        if not 1 <= len(srcs) <= 16:
+            raise ValueError("reduce takes 1..16 sources")
+        return self._add(OP_REDUCE, stream, dst=dst, srcs=list(srcs), count=count, dtype=dtype)
+
+    def memset(self, stream: int, dst: Ref, nbytes: int, value: int = 0) -> Op:
+        return self._add(OP_MEMSET, stream, dst=dst, nbytes=nbytes, value=value)
+
+    # ------------------------------------------------------------------ encoding
+    def encode(self, resolve: Callable[[Ref], int]) -> List[int]:
+        """Flatten to ``OP_WORDS`` int64 per op; ``resolve`` maps a Ref to a device address."""
+        words: List[int] = []
+        for op in self.ops:
+            w = [0] * OP_WORDS
+            w[0], w[1] = op.kind, op.stream
+            a = op.args
+            k = op.kind
+            if k == OP_GEMM:
+                w[2:12] = [resolve(a["a"]), resolve(a["b"]), resolve(a["c"]), a["lda"], a["ldb"],
+                           a["ldc"], a["a_grp"], a["a_gstride"], a["c_grp"], a["c_gstride"]]
+                w[12:19] = [a["M"], a["N"], a["K"], a["din"], a["dout"], a["tile"], a["mode"]]
+                w[19] = resolve(a["flags"]) if a["flags"] is not None else 0
+                w[20:24] = [a["flag_rows"], a["nshards"], a["first_shard"], a["tile_order"]]
+            elif k in (OP_RECORD, OP_WAIT):
+                w[2] = a["event"]
+            elif k in (OP_ALLGATHER, OP_REDUCE_SCATTER):
+                w[2:6] = [resolve(a["send"]), resolve(a["recv"]), a["count"], a["dtype"]]
+            elif k in (OP_SEND, OP_RECV):
+                w[2:6] = [resolve(a["buf"]), a["count"], a["dtype"], a["peer"]]
+            elif k == OP_COPY:
+                w[2:7] = [resolve(a["dst"]), resolve(a["src"]), a["nbytes"], a["method"],
+                          a["max_blocks"]]
+            elif k == OP_COPY_MULTI:
+                w[2], w[3] = len(a["segs"]), a["max_blocks"]
+                for i, (d, s, n) in enumerate(a["segs"]):
+                    w[4 + 3 * i:7 + 3 * i] = [resolve(d), resolve(s), n]
+            elif k in (OP_SIGNAL, OP_WAIT_SIGNAL):
+                w[2], w[3], w[4] = len(a["flags"]), a["method"], a["delta"]
+                for i, f in enumerate(a["flags"]):
+                    w[5 + i] = resolve(f)
+            elif k == OP_REDUCE:
+                w[2:6] = [resolve(a["dst"]), a["count"], a["dtype"], len(a["srcs"])]
+                for i, s in enumerate(a["srcs"]):
+                    w[6 + i] = resolve(s)
+            elif k == OP_MEMSET:
+                w[2:5] = [resolve(a["dst"]), a["nbytes"], a["value"]]
+            words.extend(int(x) for x in w)
+        return words
+
+    def describe(self) -> str:
+        """Human-readable listing (``python -m ddlb_amd.parallel.explain`` prints this)."""
+        lines = [f"plan rank={self.rank}/{self.world} streams={self.nstreams} "
+                 f"events={self.nevents} ops={len(self.ops)}"]
+        for name, b in self.buffers.items():
+            lines.append(f"  buffer {name}: {b.nbytes} B{' symmetric' if b.symmetric else ''}")
+        for i, op in enumerate(self.ops):
+            parts = []
+            for key, v in op.args.items():
+                if isinstance(v, Ref):
+                    v = f"{v.buf}+{v.off}" + (f"@{v.owner}" if v.owner is not None else "")
+                elif isinstance(v, list) and v and isinstance(v[0], Ref):
+                    v = "[" + ",".join(f"{x.buf}+{x.off}" + (f"@{x.owner}" if x.owner is not None
+                                                             else "") for x in v) + "]"
+                parts.append(f"{key}={v}")
+            lines.append(f"  {i:3d} s{op.stream} {op.name:14s} " + " ".join(parts))
+        return "\n".join(lines)

@@ -1,0 +1,92 @@
+"""Option schema shared by the native TP-Columnwise / TP-Rowwise implementations.
+
+Keeps the reference ``fuser`` option names (``ddlb/primitives/TPColumnwise/fuser.py:160-178``,
+``TPRowwise/fuser.py:182-198``) so reference JSON configs run unchanged:
+
+=================================  ===============================================================
+option                             meaning here
+=================================  ===============================================================
+backend                            ``rccl`` (alias ``nccl``) RCCL collectives on our own comm and
+                                   streams; ``ipc`` (alias ``cuda``) HIP IPC symmetric memory over
+                                   xGMI. ``ucc*`` -> explicit error.
+algorithm                          ``default`` | ``coll_pipeline`` | ``p2p_pipeline``
+s                                  coll_pipeline stages (>= 1)
+offset_stream_indexing_by_rank     ring order: step j works on shard (r+j)%d
+multicast_protocol                 ipc data movement: ``memcpy`` (copy engines, one queue per
+                                   peer; = ``default``), ``batch_memcpy`` (all peers on one queue),
+                                   ``kernel`` (CU copy kernel; ``multimem`` maps here: MI355X has
+                                   no NVLS multicast)
+inter_stream_synchronization       serialise the per-peer transfers
+=================================  ===============================================================
+
+Native-only: ``signal`` (``stream`` = hipStreamWrite/WaitValue32 memops, ``kernel`` = tiny spin
+kernels), ``tile`` (GEMM tile or ``auto``), ``gemm_mode`` (``auto`` | ``mx`` for block-scaled fp8),
+``copy_blocks`` (CU budget of the kernel protocol), ``fused`` (p2p: one arrival-flag-gated GEMM).
+"""
+
+from __future__ import annotations
+
+from ddlb_amd.parallel.algorithms import AlgoConfig
+from ddlb_amd.parallel.plan import SIG_KERNEL, SIG_STREAM
+from ddlb_amd.primitives.backends import UCC_BACKENDS, BackendUnavailable
+
+COMMON_DEFAULTS = {
+    "backend": "rccl",
+    "algorithm": "default",
+    "s": 8,
+    "offset_stream_indexing_by_rank": True,
+    "multicast_protocol": "memcpy",
+    "inter_stream_synchronization": False,
+    "signal": "stream",
+    "tile": "auto",
+    "gemm_mode": "auto",
+    "copy_blocks": 64,
+    "fused": False,
+}
+COMMON_ALLOWED = {
+    "backend": ["rccl", "ipc", *UCC_BACKENDS],
+    "algorithm": ["default", "coll_pipeline", "p2p_pipeline"],
+    "s": (1, 1 << 20),
+    "offset_stream_indexing_by_rank": [True, False],
+    "multicast_protocol": ["memcpy", "batch_memcpy", "kernel"],
+    "inter_stream_synchronization": [True, False],
+    "signal": ["stream", "kernel"],
+    "tile": ["auto", "256x256", "256x128", "128x256", "128x128"],
+    "gemm_mode": ["auto", "mx", "generic"],
+    "copy_blocks": (1, 4096),
+    "fused": [True, False],
+}
+COMMON_ALIASES = {
+    "backend": {"nccl": "rccl", "cuda": "ipc"},
+    "multicast_protocol": {"default": "memcpy", "multimem": "kernel"},
+}
+
+TILE_CODE = {"auto": 0, "256x256": 1, "256x128": 2, "128x256": 3, "128x128": 4}
+MODE_CODE = {"auto": 0, "generic": 1, "mx": 2}
+
+
+def algo_config(options, order: str = "AG_before") -> AlgoConfig:
+    backend = options["backend"]
+    if backend in UCC_BACKENDS:
+        raise BackendUnavailable(
+            f"backend '{backend}' needs UCC/UCX, which the MI355X stack does not ship; use "
+            "backend=rccl (alias nccl) or backend=ipc (alias cuda)")
+    if options["fused"] and options["multicast_protocol"] == "kernel":
+        raise ValueError("fused=True spins GEMM tiles on arrival flags; it needs copy-engine "
+                         "transfers (multicast_protocol=memcpy|batch_memcpy), not CU copies")
+    return AlgoConfig(
+        algorithm=options["algorithm"], backend=backend, order=order, s=int(options["s"]),
+        ring=bool(options["offset_stream_indexing_by_rank"]),
+        protocol=options["multicast_protocol"],
+        inter_stream_sync=bool(options["inter_stream_synchronization"]),
+        signal=SIG_STREAM if options["signal"] == "stream" else SIG_KERNEL,
+        tile=TILE_CODE[options["tile"]], mode=MODE_CODE[options["gemm_mode"]],
+        copy_blocks=int(options["copy_blocks"]), fused=bool(options["fused"]))
+
+
+def dtype_codes(dtype_name: str):
+    from ddlb_amd.parallel.plan import NAME_DT, DT_BF16, DT_FP8
+
+    din = NAME_DT[dtype_name]
+    dout = DT_BF16 if din == DT_FP8 else din
+    return din, dout

@@ -1,0 +1,131 @@
+"""Native implementations on the GPU.
+
+* world=1: every primitive x algorithm x backend through the plan executor, validated.
+* 2 and 3 ranks sharing the box's single GPU (separate processes, HIP IPC between them — legal
+  on one device, unlike RCCL): the IPC algorithms with every protocol / signal method, 4
+  iterations each, validated. This exercises the real handle exchange, peer mappings, copy
+  engines, CU copies, cross-process flags and the epoch protocol.
+"""
+
+import itertools
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def comm():
+    from conftest import free_port
+    from ddlb_amd.communicator import Communicator
+
+    os.environ["DDLB_CHILD_INIT_METHOD"] = f"tcp://127.0.0.1:{free_port()}"
+    c = Communicator()
+    c.ensure_process_group()
+    yield c
+    Communicator.reset()
+    os.environ.pop("DDLB_CHILD_INIT_METHOD", None)
+
+
+@pytest.mark.parametrize("alg,backend", itertools.product(
+    ["default", "coll_pipeline", "p2p_pipeline"], ["rccl", "ipc"]))
+@pytest.mark.parametrize("dtype", ["bfloat16", "float16", "float32", "float8_e4m3fn"])
+def test_native_world1(comm, alg, backend, dtype):
+    from ddlb_amd.primitives.tp_columnwise.native import NativeTPColumnwise
+    from ddlb_amd.primitives.tp_rowwise.native import NativeTPRowwise
+
+    for cls in (NativeTPColumnwise, NativeTPRowwise):
+        impl = cls(m=1024, n=512, k=512, dtype=dtype, algorithm=alg, backend=backend, s=2)
+        for _ in range(2):
+            out = impl.run()
+        torch.cuda.synchronize()
+        impl.validate(out)
+        impl.close()
+
+
+def test_native_fp8_mx_world1(comm):
+    from ddlb_amd.primitives.tp_columnwise.native import NativeTPColumnwise
+
+    impl = NativeTPColumnwise(m=2048, n=1024, k=1024, dtype="float8_e4m3fn", gemm_mode="mx")
+    out = impl.run()
+    torch.cuda.synchronize()
+    impl.validate(out)
+    impl.close()
+
+
+def test_compute_only_and_pytorch_world1(comm):
+    from ddlb_amd.primitives.registry import resolve
+
+    for prim in ("tp_columnwise", "tp_rowwise"):
+        for impl_name, opts in (("compute_only", {"size": "unsharded"}),
+                                ("compute_only", {"size": "sharded", "gemm": "torch"}),
+                                ("pytorch", {"empty_cache": False})):
+            cls, o, _ = resolve(prim, impl_name, opts)
+            impl = cls(m=1024, n=256, k=512, dtype="bfloat16", **o)
+            out = impl.run()
+            torch.cuda.synchronize()
+            impl.validate(out)
+            impl.close()
+
+
+def _ipc_cfgs():
+    cfgs = []
+    for alg in ("default", "coll_pipeline", "p2p_pipeline"):
+        for proto in ("memcpy", "batch_memcpy", "kernel"):
+            for sig in ("stream", "kernel"):
+                for prim in ("col", "row"):
+                    cfgs.append((f"{prim}/{alg}/{proto}/{sig}", prim,
+                                 dict(algorithm=alg, backend="ipc", multicast_protocol=proto,
+                                      signal=sig, s=2)))
+    cfgs.append(("col/default/ipc/AG_after", "col",
+                 dict(algorithm="default", backend="ipc", order="AG_after")))
+    cfgs.append(("col/coll/ipc/AG_after", "col",
+                 dict(algorithm="coll_pipeline", backend="ipc", order="AG_after", s=2)))
+    cfgs.append(("col/p2p/fused", "col", dict(algorithm="p2p_pipeline", backend="ipc",
+                                              fused=True)))
+    cfgs.append(("col/p2p/noring", "col", dict(algorithm="p2p_pipeline", backend="ipc",
+                                               offset_stream_indexing_by_rank=False)))
+    cfgs.append(("col/p2p/fp8", "col", dict(algorithm="p2p_pipeline", backend="ipc",
+                                            dtype="float8_e4m3fn")))
+    return cfgs
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ipc_shared_gpu(world):
+    from conftest import free_port
+
+    port = free_port()
+    cfgs = _ipc_cfgs()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world),
+                   LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   DDLB_PG_BACKEND="gloo", DDLB_ALLOW_SHARED_GPU="1",
+                   DDLB_TEST_CFGS=json.dumps(cfgs))
+        env.pop("DDLB_CHILD_INIT_METHOD", None)
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests",
+                                                                    "_ipc_worker.py")],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                      text=True))
+    outs = []
+    for p in procs:
+        try:
+            o, _ = p.communicate(timeout=420)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            pytest.fail("IPC workers timed out")
+        outs.append(o)
+    codes = [p.returncode for p in procs]
+    line = [ln for ln in outs[0].splitlines() if ln.startswith("RESULT ")]
+    assert line, f"rank 0 printed no result (codes {codes}):\n{outs[0][-3000:]}"
+    res = json.loads(line[0][len("RESULT "):])
+    bad = {k: v for k, v in res.items() if v != "ok"}
+    assert not bad, json.dumps(bad, indent=1)
+    assert all(c == 0 for c in codes), (codes, outs[1][-2000:])

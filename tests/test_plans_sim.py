@@ -1,0 +1,104 @@
+"""Every native algorithm, simulated on the CPU for d ranks: layout math, synchronisation
+protocol (no deadlock, no unordered conflicting access) and numerics vs an fp32 reference."""
+
+import itertools
+
+import pytest
+import torch
+
+from ddlb_amd.parallel.algorithms import AlgoConfig, build_tp_columnwise, build_tp_rowwise
+from ddlb_amd.parallel.plan import DT_BF16, DT_F32, SIG_KERNEL, SIG_STREAM
+from ddlb_amd.parallel.sim import Simulator, make_buffers, read_tensor, write_tensor
+
+ALGS = ["default", "coll_pipeline", "p2p_pipeline"]
+BACKENDS = ["rccl", "ipc"]
+PROTOCOLS = ["memcpy", "batch_memcpy", "kernel"]
+
+
+def _inputs(m, n, k, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    A = torch.randint(-3, 4, (m, k), generator=g).float()
+    B = torch.randint(-3, 4, (k, n), generator=g).float()
+    return A, B
+
+
+def _run_col(d, m, n, k, cfg, epochs=3, dt=DT_F32):
+    A, B = _inputs(m, n, k)
+    tdt = torch.float32 if dt == DT_F32 else torch.bfloat16
+    built = [build_tp_columnwise(r, d, m, n, k, dt, dt, cfg) for r in range(d)]
+    plans = [p for p, _ in built]
+    bufs = make_buffers(plans)
+    ml = m // d
+    for r, (_, io) in enumerate(built):
+        write_tensor(bufs[r], io.a, A[r * ml:(r + 1) * ml].to(tdt))
+        write_tensor(bufs[r], io.b, B.t().contiguous().to(tdt))
+    sim = Simulator(plans, bufs)
+    for _ in range(epochs):
+        sim.run_epoch()
+    ref = A @ B
+    for r, (_, io) in enumerate(built):
+        out = read_tensor(bufs[r], io.out).float()
+        torch.testing.assert_close(out, ref, rtol=0, atol=0)
+
+
+def _run_row(d, m, n, k, cfg, epochs=3, dt=DT_F32):
+    A, B = _inputs(m, n, k, seed=1)
+    tdt = torch.float32 if dt == DT_F32 else torch.bfloat16
+    built = [build_tp_rowwise(r, d, m, n, k, dt, dt, cfg) for r in range(d)]
+    plans = [p for p, _ in built]
+    bufs = make_buffers(plans)
+    kl, ml = k // d, m // d
+    for r, (_, io) in enumerate(built):
+        write_tensor(bufs[r], io.a, A[:, r * kl:(r + 1) * kl].contiguous().to(tdt))
+        write_tensor(bufs[r], io.b, B[r * kl:(r + 1) * kl].t().contiguous().to(tdt))
+    sim = Simulator(plans, bufs)
+    for _ in range(epochs):
+        sim.run_epoch()
+    ref = A @ B
+    for r, (_, io) in enumerate(built):
+        out = read_tensor(bufs[r], io.out).float()
+        torch.testing.assert_close(out, ref[r * ml:(r + 1) * ml], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("d", [1, 2, 3, 4])
+@pytest.mark.parametrize("alg,backend", list(itertools.product(ALGS, BACKENDS)))
+@pytest.mark.parametrize("order", ["AG_before", "AG_after"])
+def test_columnwise_plans(d, alg, backend, order):
+    cfg = AlgoConfig(algorithm=alg, backend=backend, order=order, s=2)
+    _run_col(d, m=16 * d, n=8, k=12, cfg=cfg)
+
+
+@pytest.mark.parametrize("d", [1, 2, 3, 4])
+@pytest.mark.parametrize("alg,backend", list(itertools.product(ALGS, BACKENDS)))
+def test_rowwise_plans(d, alg, backend):
+    cfg = AlgoConfig(algorithm=alg, backend=backend, s=2)
+    _run_row(d, m=16 * d, n=8, k=4 * d, cfg=cfg)
+
+
+@pytest.mark.parametrize("protocol", PROTOCOLS)
+@pytest.mark.parametrize("alg", ALGS)
+@pytest.mark.parametrize("ring", [True, False])
+@pytest.mark.parametrize("sig", [SIG_STREAM, SIG_KERNEL])
+def test_ipc_protocols(protocol, alg, ring, sig):
+    cfg = AlgoConfig(algorithm=alg, backend="ipc", protocol=protocol, ring=ring, signal=sig, s=2,
+                     inter_stream_sync=ring)
+    _run_col(3, m=24, n=8, k=8, cfg=cfg)
+    _run_row(3, m=24, n=8, k=9, cfg=cfg)
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_p2p_fused_plan(fused):
+    cfg = AlgoConfig(algorithm="p2p_pipeline", backend="ipc", fused=fused)
+    _run_col(4, m=32, n=8, k=8, cfg=cfg)
+
+
+def test_bf16_plans_round_like_hardware():
+    cfg = AlgoConfig(algorithm="coll_pipeline", backend="rccl", s=2)
+    _run_col(2, m=16, n=8, k=8, cfg=cfg, dt=DT_BF16)
+
+
+def test_invalid_configs():
+    with pytest.raises(ValueError):
+        build_tp_columnwise(0, 2, 30, 8, 8, DT_F32, DT_F32, AlgoConfig(algorithm="coll_pipeline", s=4))
+    with pytest.raises(ValueError):
+        build_tp_rowwise(0, 2, 16, 8, 7, DT_F32, DT_F32, AlgoConfig())
