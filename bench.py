@@ -12,10 +12,14 @@ Contract (driver):  python bench.py --gpus N --steps K --warmup W
     (every rank computes the full [m,k]x[k,n] on its own N-slice of the weight: weak scaling in
     N); ``per_gpu_tflops`` is the reference harness's per-GPU number (``ddlb/benchmark.py:211``).
 
-Before timing, an autotuner (N>1) runs every candidate native algorithm a few times, MAX-reduces
-their times over ranks so every rank picks the same winner, and validates the winner against an
-fp32 reference. The candidate timings are reported in the JSON (``autotune``). Synthetic
-U[-1,1) inputs of the named shape (no datasets exist offline).
+Process model (robust by construction): the launched processes never touch the GPU. They form
+a gloo group and run every measurement in a child process per rank (fresh HIP context, its own
+rendezvous port, a hard timeout). With N>1 an autotuner first times each candidate native
+algorithm in its own children (MAX over ranks), then the winner runs the timed measurement; a
+candidate that fails or hangs is killed and skipped on every rank, so one bad path cannot hang
+the job. Candidate timings are reported in the JSON (``autotune_ms``). Synthetic U[-1,1) inputs
+of the named shape (no datasets exist offline); the result is validated against an fp32
+reference.
 """
 
 from __future__ import annotations
@@ -23,37 +27,151 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
-import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-CANDIDATES = [  # (label, impl options) tried in this order
-    ("p2p_pipeline/ipc/memcpy", dict(algorithm="p2p_pipeline", backend="ipc",
-                                     multicast_protocol="memcpy")),
-    ("coll_pipeline/ipc/memcpy/s4", dict(algorithm="coll_pipeline", backend="ipc",
-                                         multicast_protocol="memcpy", s=4)),
-    ("default/ipc/kernel", dict(algorithm="default", backend="ipc", multicast_protocol="kernel",
-                                copy_blocks=128)),
-    ("coll_pipeline/rccl/s4", dict(algorithm="coll_pipeline", backend="rccl", s=4)),
-    ("coll_pipeline/rccl/s8", dict(algorithm="coll_pipeline", backend="rccl", s=8)),
-    ("default/rccl", dict(algorithm="default", backend="rccl")),
+# (label, impl, options), tried in this order; RCCL paths first (most mature transport).
+CANDIDATES = [
+    ("coll_pipeline/rccl/s4", "native", dict(algorithm="coll_pipeline", backend="rccl", s=4)),
+    ("default/rccl", "native", dict(algorithm="default", backend="rccl")),
+    ("p2p_pipeline/ipc/memcpy", "native", dict(algorithm="p2p_pipeline", backend="ipc",
+                                                multicast_protocol="memcpy")),
+    ("p2p_pipeline/ipc/memcpy/fused", "native", dict(algorithm="p2p_pipeline", backend="ipc",
+                                                      multicast_protocol="memcpy", fused=True)),
+    ("coll_pipeline/ipc/memcpy/s4", "native", dict(algorithm="coll_pipeline", backend="ipc",
+                                                    multicast_protocol="memcpy", s=4)),
+    ("default/ipc/kernel", "native", dict(algorithm="default", backend="ipc",
+                                           multicast_protocol="kernel", copy_blocks=128)),
+    ("coll_pipeline/rccl/s8", "native", dict(algorithm="coll_pipeline", backend="rccl", s=8)),
+    ("pytorch(rccl+hipblaslt)", "pytorch", dict(backend="nccl", empty_cache=False)),
 ]
 
 
-def _watchdog(seconds: float, rank: int):
-    def fire():
-        sys.stderr.write(f"[bench] rank {rank}: watchdog fired after {seconds:.0f}s, aborting\n")
-        sys.stderr.flush()
-        os._exit(3)
+# ------------------------------------------------------------------------------- child
+def child_main(a) -> int:
+    """One measurement on this rank's GPU; writes a JSON result file (rank 0 aggregates)."""
+    import torch
 
-    t = threading.Timer(seconds, fire)
-    t.daemon = True
-    t.start()
-    return t
+    from ddlb_amd.communicator import Communicator
+    from ddlb_amd.primitives.registry import resolve
+
+    res = {"ok": False}
+    try:
+        comm = Communicator()
+        comm.ensure_process_group(timeout_s=a.child_timeout)
+        cls, opts, _ = resolve("tp_columnwise", a.child_impl, json.loads(a.child_opts))
+        impl = cls(m=a.m, n=a.n, k=a.k, dtype=a.dtype, **opts)
+        valid = None
+        if a.validate:
+            out = impl.run()
+            comm.synchronize()
+            try:
+                impl.validate(out)
+                valid = True
+            except AssertionError as e:
+                valid = False
+                res["validation"] = str(e).splitlines()[0][:200]
+        for _ in range(a.warmup):
+            impl.run()
+        comm.barrier()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            impl.run()
+        comm.synchronize()
+        t1 = time.perf_counter()
+        comm.barrier()
+        t = torch.tensor([(t1 - t0) * 1e3 / a.steps], dtype=torch.float64, device=comm.device)
+        comm.all_reduce_max(t)
+        res.update(ok=True, ms=float(t.item()), valid=valid)
+        impl.close()
+        comm.destroy()
+    except Exception as e:  # reported to the parent, never raised
+        res["error"] = f"{type(e).__name__}: {str(e)[:300]}"
+    with open(a.child_out, "w") as f:
+        json.dump(res, f)
+    return 0
+
+
+# ------------------------------------------------------------------------------- parent
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class Job:
+    def __init__(self, a):
+        self.a = a
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.pg = None
+        if self.world > 1:
+            import datetime
+
+            import torch.distributed as dist
+
+            dist.init_process_group("gloo", init_method="env://", rank=self.rank,
+                                    world_size=self.world,
+                                    timeout=datetime.timedelta(seconds=3 * 3600))
+            self.pg = dist
+        self.tmp = os.environ.get("TMPDIR", "/tmp")
+        self.counter = 0
+
+    def bcast(self, obj):
+        if self.pg is None:
+            return obj
+        box = [obj]
+        self.pg.broadcast_object_list(box, src=0)
+        return box[0]
+
+    def gather(self, obj):
+        if self.pg is None:
+            return [obj]
+        out = [None] * self.world
+        self.pg.all_gather_object(out, obj)
+        return out
+
+    def measure(self, impl: str, opts: dict, steps: int, warmup: int, validate: bool,
+                timeout: float) -> dict:
+        """Run one measurement in a child per rank; every rank returns the same dict."""
+        self.counter += 1
+        port = self.bcast(_free_port() if self.rank == 0 else None)
+        out = os.path.join(self.tmp, f"ddlb_bench_{os.getpid()}_{self.counter}.json")
+        env = dict(os.environ)
+        env["DDLB_CHILD_INIT_METHOD"] = f"tcp://127.0.0.1:{port}"
+        cmd = [sys.executable, os.path.abspath(__file__), "--child", "--child-out", out,
+               "--child-impl", impl, "--child-opts", json.dumps(opts), "--steps", str(steps),
+               "--warmup", str(warmup), "-m", str(self.a.m), "-n", str(self.a.n), "-k",
+               str(self.a.k), "--dtype", self.a.dtype, "--child-timeout", str(timeout)]
+        if validate:
+            cmd.append("--validate")
+        proc = subprocess.Popen(cmd, env=env)
+        try:
+            proc.wait(timeout=timeout)
+            local = json.load(open(out)) if os.path.exists(out) else {
+                "ok": False, "error": f"child exit {proc.returncode}"}
+        except subprocess.TimeoutExpired:
+            proc.kill()
+            proc.wait()
+            local = {"ok": False, "error": f"timeout after {timeout:.0f}s"}
+        finally:
+            if os.path.exists(out):
+                os.remove(out)
+        results = self.gather(local)
+        if all(r.get("ok") for r in results):
+            ms = max(r["ms"] for r in results)
+            valid = all(r.get("valid") is not False for r in results)
+            return {"ok": True, "ms": ms, "valid": valid if validate else None}
+        errs = [r.get("error") for r in results if not r.get("ok")]
+        return {"ok": False, "error": errs[0] if errs else "unknown"}
 
 
 def main(argv=None) -> int:
@@ -65,125 +183,72 @@ def main(argv=None) -> int:
     p.add_argument("-n", type=int, default=1024)
     p.add_argument("-k", type=int, default=1024)
     p.add_argument("--dtype", default="bfloat16")
-    p.add_argument("--impl", default="native", choices=["native", "pytorch"])
     p.add_argument("--algorithm", default="auto",
-                   help="auto | one of the candidate labels | default|coll_pipeline|p2p_pipeline")
-    p.add_argument("--backend", default="rccl")
-    p.add_argument("--s", type=int, default=4)
-    p.add_argument("--tune-steps", type=int, default=6)
-    p.add_argument("--timeout", type=float, default=float(os.environ.get("DDLB_BENCH_TIMEOUT",
-                                                                        900)))
-    p.add_argument("--no-validate", action="store_true")
+                   help="auto | a candidate label (see CANDIDATES)")
+    p.add_argument("--tune-steps", type=int, default=10)
+    p.add_argument("--candidate-timeout", type=float, default=180.0)
+    p.add_argument("--no-validate", dest="validate", action="store_false", default=True)
+    # child-mode arguments (internal)
+    p.add_argument("--child", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--child-out", help=argparse.SUPPRESS)
+    p.add_argument("--child-impl", default="native", help=argparse.SUPPRESS)
+    p.add_argument("--child-opts", default="{}", help=argparse.SUPPRESS)
+    p.add_argument("--child-timeout", type=float, default=600.0, help=argparse.SUPPRESS)
+    p.add_argument("--validate", dest="validate", action="store_true", help=argparse.SUPPRESS)
     a = p.parse_args(argv)
+    if a.child:
+        return child_main(a)
 
-    world_env = int(os.environ.get("WORLD_SIZE", "1"))
-    rank_env = int(os.environ.get("RANK", "0"))
-    if a.gpus != world_env:
-        if world_env == 1 and a.gpus > 1:
-            sys.stderr.write("bench.py: --gpus > 1 must be launched with torch.distributed.run\n")
-            return 2
-    dog = _watchdog(a.timeout, rank_env)
-    if world_env == 1 and "MASTER_PORT" not in os.environ:
-        import socket
-
-        s = socket.socket()
-        s.bind(("127.0.0.1", 0))
-        os.environ["DDLB_CHILD_INIT_METHOD"] = f"tcp://127.0.0.1:{s.getsockname()[1]}"
-        s.close()
-
-    import torch
-    import torch.distributed as dist
-
-    from ddlb_amd.communicator import Communicator
-    from ddlb_amd.primitives.registry import resolve
-
-    comm = Communicator()
-    comm.ensure_process_group()
-    rank, world = comm.rank, comm.world_size
-    m, n, k = a.m, a.n, a.k
-
-    def build(opts):
-        cls, o, _ = resolve("tp_columnwise", a.impl, opts)
-        return cls(m=m, n=n, k=k, dtype=a.dtype, **o)
-
-    def time_impl(impl, steps, warm):
-        for _ in range(warm):
-            impl.run()
-        comm.barrier()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            impl.run()
-        comm.synchronize()
-        t1 = time.perf_counter()
-        comm.barrier()
-        t = torch.tensor([(t1 - t0) * 1e3 / steps], dtype=torch.float64, device=comm.device)
-        comm.all_reduce_max(t)
-        return float(t.item())
-
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus > 1 and world == 1:
+        sys.stderr.write("bench.py: --gpus > 1 must be launched with torch.distributed.run\n")
+        return 2
+    job = Job(a)
     tune = {}
-    if a.impl == "pytorch":
-        chosen = ("pytorch/rccl+hipblaslt", dict(backend="nccl", empty_cache=False))
-    elif world == 1:
-        chosen = ("gemm (world=1)", dict(algorithm="default", backend="rccl"))
-    elif a.algorithm == "auto":
-        best = None
-        for label, opts in CANDIDATES:
-            try:
-                impl = build(opts)
-                ms = time_impl(impl, a.tune_steps, 2)
-                impl.close()
-                del impl
-                tune[label] = round(ms, 4)
-                if best is None or ms < best[0]:
-                    best = (ms, label, opts)
-            except Exception as e:  # a failing candidate is skipped on every rank
-                tune[label] = f"error: {type(e).__name__}: {str(e)[:120]}"
-                try:
-                    comm.barrier()
-                except Exception:
-                    pass
-            torch.cuda.empty_cache()
-        if best is None:
-            raise RuntimeError(f"every candidate failed: {tune}")
-        chosen = (best[1], best[2])
-    else:
+    if a.algorithm != "auto":
         match = [c for c in CANDIDATES if c[0] == a.algorithm]
-        chosen = match[0] if match else (a.algorithm, dict(algorithm=a.algorithm,
-                                                          backend=a.backend, s=a.s))
-
-    impl = build(chosen[1])
-    valid = None
-    if not a.no_validate:
-        out = impl.run()
-        comm.synchronize()
-        try:
-            impl.validate(out)
-            valid = True
-        except AssertionError:
-            valid = False
-        del out
-    ms = time_impl(impl, a.steps, a.warmup)
-    flop = 2.0 * m * n * k
+        if not match:
+            raise SystemExit(f"unknown --algorithm {a.algorithm}; choose from "
+                             f"{[c[0] for c in CANDIDATES]}")
+        chosen = match[0]
+    elif world == 1:
+        chosen = ("gemm (world=1)", "native", dict(algorithm="default", backend="rccl"))
+    else:
+        best = None
+        for label, impl, opts in CANDIDATES:
+            r = job.measure(impl, opts, a.tune_steps, 3, False, a.candidate_timeout)
+            tune[label] = round(r["ms"], 4) if r["ok"] else r["error"][:160]
+            if r["ok"] and impl == "native" and (best is None or r["ms"] < best[0]):
+                best = (r["ms"], (label, impl, opts))
+        if best is None:
+            sys.stderr.write(f"every native candidate failed: {json.dumps(tune)}\n")
+            return 1
+        chosen = best[1]
+    final = job.measure(chosen[1], chosen[2], a.steps, a.warmup, a.validate,
+                        a.candidate_timeout + a.steps * 0.05)
+    if not final["ok"]:
+        sys.stderr.write(f"final measurement failed: {final['error']}\n")
+        return 1
+    ms = final["ms"]
+    flop = 2.0 * a.m * a.n * a.k
     per_gpu = flop / (ms * 1e-3) / 1e12
-    total = per_gpu * world
-    if rank == 0:
+    if job.rank == 0:
         line = {
             "metric": "tp_columnwise AG+GEMM effective TFLOP/s (whole job, m=65536 bf16)",
-            "value": round(total, 3), "unit": "TFLOP/s", "n_gpus": world, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(ms, 5), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if a.dtype == "bfloat16"
-            else a.dtype, "data": "synthetic",
-            "config": {"model": f"tp_columnwise AG+GEMM m={m} n={n} k={k}", "global_batch": 1,
-                       "seq_len": m, "parallelism": f"tp{world}-sp",
-                       "implementation": a.impl, "algorithm": chosen[0]},
-            "per_gpu_tflops": round(per_gpu, 3), "valid": valid,
+            "value": round(per_gpu * world, 6), "unit": "TFLOP/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 5),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16" if a.dtype == "bfloat16" else a.dtype, "data": "synthetic",
+            "config": {"model": f"tp_columnwise AG+GEMM m={a.m} n={a.n} k={a.k}",
+                       "global_batch": 1, "seq_len": a.m, "parallelism": f"tp{world}-sp",
+                       "implementation": chosen[1], "algorithm": chosen[0]},
+            "per_gpu_tflops": round(per_gpu, 6), "valid": final.get("valid"),
             "autotune_ms": tune,
         }
         print(json.dumps(line), flush=True)
-    impl.close()
-    dog.cancel()
-    comm.destroy()
-    return 0 if valid is not False else 1
+    if job.pg is not None:
+        job.pg.destroy_process_group()
+    return 0 if final.get("valid") is not False else 1
 
 
 if __name__ == "__main__":

@@ -271,6 +271,172 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_kernel(const GemmArgs p) 
   }
 }
 
+// ---------------------------------------------------------------- 256x256 ping-pong kernel
+// 8 waves = 2 groups (wr = 0: waves 0-3, wr = 1: waves 4-7; every SIMD hosts one wave of each)
+// x 4 column waves. Each wave owns a 128x64 output tile = 2x2 quadrants of 64x32 and runs, per
+// 64-deep K-tile, 4 phases of {LOAD section: ds_read the quadrant's fragments (+ LDS-DMA of the
+// next K-tile) | barrier | COMP section: 16 MFMAs | barrier}. Group 1 starts one barrier later,
+// so in every interval between two barriers one group computes while the other loads
+// (cdna guide §5 "256^2 8-phase template", T3/T4/T5).
+//
+// Sections of group 0 are numbered s = 8t + {0 L1, 1 C1, 2 L2, 3 C2, 4 L3, 5 C3, 6 L4, 7 C4} and
+// run between barriers B[s+1] and B[s+2]; group 1's section s runs between B[s+2] and B[s+3].
+//  * tile t+1 -> buffer (t+1)&1: group 1 issues its DMA in L1, L2 of tile t, group 0 in L2, L3.
+//    WAR: the last reads of tile t-1 (both groups' L4) retire in their C4, i.e. by B[8t+2],
+//    and group 1's L1 of tile t starts at B[8t+2].
+//  * RAW: group 0 waits vmcnt(0) at the end of C4 (before B[8t+9]), group 1 at the end of its
+//    L4 (before B[8t+9]); the first read of tile t+1 (group 0's L1) starts after B[8t+9].
+//  * Barrier balance: group 1 executes one extra barrier before the loop, group 0 one after it.
+template <class Mma, int OUT>
+__global__ __launch_bounds__(512) void gemm_tn_pp256_kernel(const GemmArgs p) {
+  constexpr int BM = 256, BN = 256, ROWB = 128;
+  constexpr int A_BYTES = BM * ROWB, STAGE = A_BYTES + BN * ROWB;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
+  const int wg = tile_index(p, tiles_m * tiles_n);
+  const int tm = wg / tiles_n, tn = wg % tiles_n;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int esz = Mma::kElem;
+
+  // LDS-DMA sources: this wave stages rows [32*wave, 32*wave+32) of A and of B (4 x 8 rows each)
+  const char* aptr[4];
+  const char* bptr[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (wave * 4 + i) * 8 + (lane >> 3);
+    int64_t gr = m0 + row;
+    gr = gr < p.M ? gr : p.M - 1;
+    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+    aptr[i] = (const char*)p.a + map_row(gr, p.a_grp, p.a_gstride) * p.lda * esz + chunk * 16;
+    int64_t gc = n0 + row;
+    gc = gc < p.N ? gc : p.N - 1;
+    bptr[i] = (const char*)p.b + gc * p.ldb * esz + chunk * 16;
+  }
+  wait_flag(p, map_row(m0, p.a_grp, p.a_gstride));
+
+  // part 0: A rows 0-15 + B rows 0-15 of this wave's 32; part 1: the other 16 of each
+  auto stage_part = [&](int buf, int kt, int part) {
+    char* base = smem + buf * STAGE;
+    const int64_t koff = (int64_t)kt * ROWB;
+#pragma unroll
+    for (int i = 2 * part; i < 2 * part + 2; ++i) {
+      glds16(aptr[i] + koff, base + (wave * 4 + i) * 1024);
+      glds16(bptr[i] + koff, base + A_BYTES + (wave * 4 + i) * 1024);
+    }
+  };
+
+  const int swz = (lane & 15) >> 1, frow = lane & 15, fq = lane >> 4;
+  const int c0 = ((0 + fq) ^ swz) * 16, c1 = ((4 + fq) ^ swz) * 16;
+  const int arow0 = (wr * 128 + frow) * ROWB, brow0 = (wc * 64 + frow) * ROWB;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  i32x4 aR[4][2], bR[2][2];
+
+  auto loadA = [&](const char* As, int mq) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const char* r = As + arow0 + (mq * 64 + f * 16) * ROWB;
+      aR[f][0] = *(const i32x4*)(r + c0);
+      aR[f][1] = *(const i32x4*)(r + c1);
+    }
+  };
+  auto loadB = [&](const char* Bs, int nq) {
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      const char* r = Bs + brow0 + (nq * 32 + f * 16) * ROWB;
+      bR[f][0] = *(const i32x4*)(r + c0);
+      bR[f][1] = *(const i32x4*)(r + c1);
+    }
+  };
+  auto comp = [&](int mq, int nq) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) Mma::step(acc[mq * 4 + f][nq * 2 + g], bR[g][kk], aR[f][kk]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+#define PP_BAR()                            \
+  do {                                      \
+    __builtin_amdgcn_sched_barrier(0);      \
+    __builtin_amdgcn_s_barrier();           \
+    __builtin_amdgcn_sched_barrier(0);      \
+  } while (0)
+#define PP_VM0() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+
+  const int nk = p.K * esz / ROWB;
+  stage_part(0, 0, 0);
+  stage_part(0, 0, 1);
+  PP_VM0();
+  PP_BAR();
+  const bool g1 = wr == 1;  // wave-uniform (wave came through readfirstlane)
+  if (g1) PP_BAR();
+  for (int t = 0; t < nk; ++t) {
+    const char* As = smem + (t & 1) * STAGE;
+    const char* Bs = As + A_BYTES;
+    const int nb = (t + 1) & 1;
+    const bool nxt = t + 1 < nk;
+    // L1
+    loadA(As, 0);
+    loadB(Bs, 0);
+    if (g1 && nxt) stage_part(nb, t + 1, 0);
+    PP_BAR();
+    comp(0, 0);
+    PP_BAR();
+    // L2
+    loadB(Bs, 1);
+    if (nxt) stage_part(nb, t + 1, g1 ? 1 : 0);
+    PP_BAR();
+    comp(0, 1);
+    PP_BAR();
+    // L3
+    loadA(As, 1);
+    if (!g1 && nxt) stage_part(nb, t + 1, 1);
+    PP_BAR();
+    comp(1, 1);
+    PP_BAR();
+    // L4
+    loadB(Bs, 0);
+    if (g1) PP_VM0();
+    PP_BAR();
+    comp(1, 0);
+    if (!g1) PP_VM0();
+    PP_BAR();
+  }
+  if (!g1) PP_BAR();
+#undef PP_BAR
+#undef PP_VM0
+
+  constexpr int OSZ = out_size<OUT>();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int64_t row = m0 + wr * 128 + (i >> 2) * 64 + (i & 3) * 16 + frow;
+    if (row >= p.M) continue;
+    char* crow = (char*)p.c + map_row(row, p.c_grp, p.c_gstride) * p.ldc * OSZ;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t col = n0 + wc * 64 + (j >> 1) * 32 + (j & 1) * 16 + fq * 4;
+      if (col + 3 < p.N) {
+        Store4<OUT>::st(crow + col * OSZ, acc[i][j]);
+      } else {
+        const float v[4] = {acc[i][j].x, acc[i][j].y, acc[i][j].z, acc[i][j].w};
+        for (int r = 0; r < 4; ++r)
+          if (col + r < p.N) Store4<OUT>::st1(crow + (col + r) * OSZ, v[r]);
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------- MX-fp8 (block-scaled) kernel
 // One v_mfma_scale_f32_16x16x128_f8f6f4 per 128-byte K-row (unit E8M0 scales = 127): 2x the bf16
 // MFMA rate (MI355X_MICROARCH.md "Matrix cores"). Same staging as above.
@@ -457,22 +623,35 @@ hipError_t launch_mx(const GemmArgs& p, hipStream_t s) {
 }
 
 template <class Mma, int OUT>
+hipError_t launch_pp256(const GemmArgs& p, hipStream_t s) {
+  const int tiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
+  hipLaunchKernelGGL((gemm_tn_pp256_kernel<Mma, OUT>), dim3(tiles), dim3(512), 0, s, p);
+  return hipGetLastError();
+}
+
+template <class Mma, int OUT>
 hipError_t launch_cfg(const GemmArgs& p, int tile, hipStream_t s) {
   switch (tile) {
+    case TILE_PP256: return launch_pp256<Mma, OUT>(p, s);
     case TILE_256x256: return launch_tiled<Mma, OUT, 256, 256, 2, 4>(p, s);
     case TILE_256x128: return launch_tiled<Mma, OUT, 256, 128, 4, 2>(p, s);
     case TILE_128x256: return launch_tiled<Mma, OUT, 128, 256, 2, 4>(p, s);
     case TILE_128x128: return launch_tiled<Mma, OUT, 128, 128, 2, 2>(p, s);
+    case TILE_256x256_W4: return launch_tiled<Mma, OUT, 256, 256, 2, 2>(p, s);
+    case TILE_256x128_W4: return launch_tiled<Mma, OUT, 256, 128, 2, 2>(p, s);
     default: return hipErrorInvalidValue;
   }
 }
 template <int OUT>
 hipError_t launch_mx_cfg(const GemmArgs& p, int tile, hipStream_t s) {
   switch (tile) {
+    case TILE_PP256:
     case TILE_256x256: return launch_mx<OUT, 256, 256, 2, 4>(p, s);
     case TILE_256x128: return launch_mx<OUT, 256, 128, 4, 2>(p, s);
     case TILE_128x256: return launch_mx<OUT, 128, 256, 2, 4>(p, s);
     case TILE_128x128: return launch_mx<OUT, 128, 128, 2, 2>(p, s);
+    case TILE_256x256_W4: return launch_mx<OUT, 256, 256, 2, 2>(p, s);
+    case TILE_256x128_W4: return launch_mx<OUT, 256, 128, 2, 2>(p, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -490,7 +669,9 @@ hipError_t launch_generic_t(const GemmArgs& p, hipStream_t s) {
 }  // namespace
 
 int tile_rows(int tile) { return (tile == TILE_128x128 || tile == TILE_128x256) ? 128 : 256; }
-int tile_cols(int tile) { return (tile == TILE_256x128 || tile == TILE_128x128) ? 128 : 256; }
+int tile_cols(int tile) {
+  return (tile == TILE_256x128 || tile == TILE_128x128 || tile == TILE_256x128_W4) ? 128 : 256;
+}
 
 bool gemm_fast_path_ok(const GemmArgs& p, int din, int dout) {
   const int esz = dtype_size(din);
@@ -507,7 +688,7 @@ bool gemm_fast_path_ok(const GemmArgs& p, int din, int dout) {
 int choose_tile(int64_t M, int64_t N, int din) {
   // Fill the 256 CUs: prefer the big tile while it yields >= ~1.5 waves of blocks.
   auto tiles = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
-  if (tiles(256, 256) >= 384) return TILE_256x256;
+  if (tiles(256, 256) >= 384) return TILE_PP256;
   if (tiles(256, 128) >= 384) return TILE_256x128;
   if (tiles(128, 256) >= 384) return TILE_128x256;
   return TILE_128x128;

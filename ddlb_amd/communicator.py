@@ -88,7 +88,16 @@ class Communicator:
                       init_method=init, timeout=datetime.timedelta(seconds=timeout_s))
         if self.is_gpu and self.backend == "nccl":
             kwargs["device_id"] = self.device
-        dist.init_process_group(**kwargs)
+        saved = None
+        if not init.startswith("env://"):
+            # Under torchrun, TORCHELASTIC_USE_AGENT_STORE makes every tcp:// rendezvous assume
+            # the agent hosts the store; our per-child stores are hosted by rank 0 instead.
+            saved = os.environ.pop("TORCHELASTIC_USE_AGENT_STORE", None)
+        try:
+            dist.init_process_group(**kwargs)
+        finally:
+            if saved is not None:
+                os.environ["TORCHELASTIC_USE_AGENT_STORE"] = saved
         return dist.group.WORLD
 
     def destroy(self) -> None:

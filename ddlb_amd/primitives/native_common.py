@@ -51,7 +51,8 @@ COMMON_ALLOWED = {
     "multicast_protocol": ["memcpy", "batch_memcpy", "kernel"],
     "inter_stream_synchronization": [True, False],
     "signal": ["stream", "kernel"],
-    "tile": ["auto", "256x256", "256x128", "128x256", "128x128"],
+    "tile": ["auto", "pp256", "256x256", "256x128", "128x256", "128x128", "256x256w4",
+             "256x128w4"],
     "gemm_mode": ["auto", "mx", "generic"],
     "copy_blocks": (1, 4096),
     "fused": [True, False],
@@ -61,7 +62,8 @@ COMMON_ALIASES = {
     "multicast_protocol": {"default": "memcpy", "multimem": "kernel"},
 }
 
-TILE_CODE = {"auto": 0, "256x256": 1, "256x128": 2, "128x256": 3, "128x128": 4}
+TILE_CODE = {"auto": 0, "256x256": 1, "256x128": 2, "128x256": 3, "128x128": 4, "pp256": 5,
+             "256x256w4": 6, "256x128w4": 7}
 MODE_CODE = {"auto": 0, "generic": 1, "mx": 2}
 
 

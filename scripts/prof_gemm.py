@@ -1,0 +1,38 @@
+"""Run one GEMM variant N times (for rocprofv3 --kernel-trace / --pmc profiles)."""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import torch
+
+    from ddlb_amd.ops.gemm import gemm
+
+    p = argparse.ArgumentParser()
+    p.add_argument("-m", type=int, default=65536)
+    p.add_argument("-n", type=int, default=1024)
+    p.add_argument("-k", type=int, default=1024)
+    p.add_argument("--tiles", default="256x256,pp256,128x128")
+    p.add_argument("--hipblaslt", action="store_true")
+    p.add_argument("--iters", type=int, default=20)
+    a = p.parse_args()
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0)
+    A = (torch.rand((a.m, a.k), generator=g, device="cuda") * 2 - 1).bfloat16()
+    W = (torch.rand((a.n, a.k), generator=g, device="cuda") * 2 - 1).bfloat16()
+    out = torch.empty((a.m, a.n), dtype=torch.bfloat16, device="cuda")
+    for t in a.tiles.split(","):
+        for _ in range(a.iters):
+            gemm(A, W, out, tile=t)
+    if a.hipblaslt:
+        Bkn = W.t().contiguous()
+        for _ in range(a.iters):
+            torch.matmul(A, Bkn, out=out)
+    torch.cuda.synchronize()
+
+
+if __name__ == "__main__":
+    main()

@@ -35,7 +35,7 @@ def gen():
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
-@pytest.mark.parametrize("tile", ["256x256", "256x128", "128x256", "128x128"])
+@pytest.mark.parametrize("tile", ["256x256", "256x128", "128x256", "128x128", "pp256", "256x256w4", "256x128w4"])
 def test_gemm_tiles(dtype, tile, gen):
     from ddlb_amd.ops.gemm import gemm
 
@@ -96,16 +96,17 @@ def test_gemm_fp8(mode, odt, gen):
     torch.testing.assert_close(out.float(), _ref(a, w), rtol=0, atol=_tol(torch.float8_e4m3fn, K))
 
 
-def test_fp8_integer_exact(gen):
+@pytest.mark.parametrize("tile", ["auto", "pp256", "128x128", "256x256w4", "256x128w4"])
+def test_fp8_integer_exact(gen, tile):
     """Small integers are exact in e4m3: both fp8 paths must match bit for bit."""
     from ddlb_amd.ops.gemm import gemm
 
-    M, N, K = 256, 256, 256
+    M, N, K = 512, 256, 512
     a = torch.randint(-3, 4, (M, K), device=DEV, generator=gen).float().to(torch.float8_e4m3fn)
     w = torch.randint(-3, 4, (N, K), device=DEV, generator=gen).float().to(torch.float8_e4m3fn)
     ref = _ref(a, w)
     for mode in ("auto", "mx"):
-        out = gemm(a, w, out_dtype=torch.float32, mode=mode)
+        out = gemm(a, w, out_dtype=torch.float32, mode=mode, tile=tile)
         torch.cuda.synchronize()
         assert torch.equal(out, ref), mode
 
@@ -132,16 +133,18 @@ def test_grouped_rows(gen):
     assert torch.count_nonzero(C[untouched].float()) == 0
 
 
-def test_repeat_race_screen(gen):
+@pytest.mark.parametrize("tile", ["auto", "pp256", "128x128", "256x256w4", "256x128w4"])
+@pytest.mark.parametrize("shape", [(2048, 1024, 1024), (4096, 2048, 2048), (768, 512, 192)])
+def test_repeat_race_screen(gen, tile, shape):
     """Same inputs, 20 launches: identical bits every time (LDS-DMA/barrier race screen)."""
     from ddlb_amd.ops.gemm import gemm
 
-    M, N, K = 2048, 1024, 1024
+    M, N, K = shape
     a, w = _rand((M, K), torch.bfloat16, gen), _rand((N, K), torch.bfloat16, gen)
-    first = gemm(a, w).clone()
+    first = gemm(a, w, tile=tile).clone()
     out = torch.empty_like(first)
     for _ in range(20):
-        gemm(a, w, out)
+        gemm(a, w, out, tile=tile)
         torch.cuda.synchronize()
         assert torch.equal(out, first)
     torch.testing.assert_close(first.float(), _ref(a, w), rtol=0, atol=_tol(torch.bfloat16, K))
