@@ -18,7 +18,10 @@ inline int dtype_size(int dt) {
 }
 
 enum Tile : int { TILE_AUTO = 0, TILE_256x256 = 1, TILE_256x128 = 2, TILE_128x256 = 3,
-                  TILE_128x128 = 4, TILE_PP256 = 5, TILE_256x256_W4 = 6, TILE_256x128_W4 = 7 };
+                  TILE_128x128 = 4, TILE_PP256 = 5, TILE_256x256_W4 = 6, TILE_256x128_W4 = 7,
+                  TILE_P256 = 8, TILE_P128 = 9,     // P*: persistent streaming variants
+                  TILE_I256 = 10, TILE_I128 = 11,    // I*: DMA interleaved into the MFMAs
+                  TILE_I256W4 = 12 };
 enum GemmMode : int { GEMM_MODE_AUTO = 0, GEMM_MODE_GENERIC = 1, GEMM_MODE_MX = 2 };
 
 // C[M,N] = A[M,K] * Bt[N,K]^T. Leading dimensions in ELEMENTS.

@@ -72,6 +72,14 @@ __device__ __forceinline__ int tile_index(const GemmArgs& p, int nwg) {
   return shard * per + xcd_remap(local, per);
 }
 
+__device__ __forceinline__ int tile_index_virtual(const GemmArgs& p, int vid, int nwg) {
+  if (!p.tile_order) return xcd_remap(vid, nwg);
+  const int per = nwg / p.nshards;
+  const int j = vid / per, local = vid % per;
+  const int shard = (p.first_shard + j) % p.nshards;
+  return shard * per + xcd_remap(local, per);
+}
+
 // ---------------------------------------------------------------- MFMA "consume 16 bytes" ops
 struct MmaBF16 {
   static constexpr int kElem = 2;
@@ -106,6 +114,21 @@ struct MmaF32 {  // exact f32 MFMA; 4 instructions per 16 B
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(bf.y, af.y, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(bf.z, af.z, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(bf.w, af.w, acc, 0, 0, 0);
+  }
+};
+
+// Compile-time emission of the {PER x MFMA, 1 x VMEM, n_g x DS_READ} interleave pattern
+// (sched_group_barrier arguments must be literal constants).
+template <int G, int NG, int PER, int NRD, int NDMA>
+struct IlvPattern {
+  static __device__ __forceinline__ void emit() {
+    if constexpr (G < NG) {
+      __builtin_amdgcn_sched_group_barrier(0x008, PER, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      constexpr int nrd = ((G + 1) * NRD) / NDMA - (G * NRD) / NDMA;
+      if constexpr (nrd > 0) __builtin_amdgcn_sched_group_barrier(0x100, nrd, 0);
+      IlvPattern<G + 1, NG, PER, NRD, NDMA>::emit();
+    }
   }
 };
 
@@ -155,7 +178,7 @@ __device__ __forceinline__ void wait_flag(const GemmArgs& p, int64_t row) {
 }
 
 // ---------------------------------------------------------------- the tiled kernel
-template <class Mma, int OUT, int BM, int BN, int WM, int WN>
+template <class Mma, int OUT, int BM, int BN, int WM, int WN, bool ILV = false>
 __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_kernel(const GemmArgs p) {
   constexpr int NT = WM * WN * 64, NW = WM * WN;
   constexpr int ROWB = 128;  // bytes per row per K-tile
@@ -236,14 +259,69 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_kernel(const GemmArgs p) 
     }
   };
 
+  // Interleaved variant: the next tile's LDS-DMA is issued INSIDE the first MFMA cluster (one
+  // DMA per MR*NR/(LA+LB) MFMAs), so its issue cost hides behind the matrix pipe instead of
+  // forming a burst at the top of every K-tile (cdna guide: "the per-phase interleave is the
+  // lever"). The DMA writes the other LDS buffer, so it may be placed after this tile's reads.
+  auto compute_ilv = [&](int buf, int next_kt) {
+    // First half: MFMAs on the c4=0 fragments, with the next tile's LDS-DMA (1 per PER MFMAs)
+    // and the c4=4 fragment reads (into a second register set) interleaved between them.
+    constexpr int NDMA = LA + LB, NRD = MR + NR, NQ = MR * NR;
+    constexpr int PER = NQ / NDMA > 0 ? NQ / NDMA : 1;
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + A_BYTES;
+    char* nbase = smem + (buf ^ 1) * STAGE;
+    const int64_t koff = (int64_t)next_kt * ROWB;
+    const int ch0 = ((0 + fq) ^ swz) * 16, ch1 = ((4 + fq) ^ swz) * 16;
+    i32x4 af0[MR], bf0[NR], af1[MR], bf1[NR];
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+      af0[i] = *(const i32x4*)(As + (wm * TM + i * 16 + frow) * ROWB + ch0);
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+      bf0[j] = *(const i32x4*)(Bs + (wn * TN + j * 16 + frow) * ROWB + ch0);
+    auto rd1 = [&](int r) {
+      if (r < MR) af1[r] = *(const i32x4*)(As + (wm * TM + r * 16 + frow) * ROWB + ch1);
+      else bf1[r - MR] = *(const i32x4*)(Bs + (wn * TN + (r - MR) * 16 + frow) * ROWB + ch1);
+    };
+    auto dma = [&](int d) {
+      if (d < LA) glds16(aptr[d] + koff, nbase + (wave * LA + d) * 1024);
+      else glds16(bptr[d - LA] + koff, nbase + A_BYTES + (wave * LB + d - LA) * 1024);
+    };
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      Mma::step(acc[q / NR][q % NR], bf0[q % NR], af0[q / NR]);
+      if ((q % PER) == PER - 1) {
+        const int g = q / PER;
+        if (g < NDMA) dma(g);
+        // spread the NRD second-half reads over the NDMA groups
+#pragma unroll
+        for (int r = (g * NRD) / NDMA; r < ((g + 1) * NRD) / NDMA; ++r) rd1(r);
+      }
+    }
+#pragma unroll
+    for (int d = NQ / PER; d < NDMA; ++d) dma(d);
+#pragma unroll
+    for (int r = ((NQ / PER) * NRD) / NDMA; r < NRD; ++r) rd1(r);
+    IlvPattern<0, (NDMA < NQ / PER ? NDMA : NQ / PER), PER, NRD, NDMA>::emit();
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) Mma::step(acc[q / NR][q % NR], bf1[q % NR], af1[q / NR]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
   const int nk = p.K * esz / ROWB;
   stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   int cur = 0;
   for (int kt = 0; kt < nk - 1; ++kt) {
-    stage(cur ^ 1, kt + 1);
-    compute(cur);
+    if constexpr (ILV) {
+      compute_ilv(cur, kt + 1);
+    } else {
+      stage(cur ^ 1, kt + 1);
+      compute(cur);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     cur ^= 1;
@@ -268,6 +346,134 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_kernel(const GemmArgs p) 
           if (col + r < p.N) Store4<OUT>::st1(crow + (col + r) * OSZ, v[r]);
       }
     }
+  }
+}
+
+// ---------------------------------------------------------------- persistent streaming kernel
+// Same tile / staging / MFMA body as gemm_tn_kernel, but a fixed grid (one block per CU) walks
+// the tiles, and the (tile, k-step) pairs form ONE continuous stream: the last k-step of tile i
+// already stages k-step 0 of tile i+1, the epilogue of tile i issues its C stores, and the wait
+// before the next compute is a COUNTED vmcnt(NSTORE) — LDS-DMA and stores share the in-order
+// vmcnt queue, so waiting for "at most NSTORE outstanding" retires the (older) DMA while the C
+// stores keep draining under tile i+1's MFMAs. Exactly NSTORE stores must be issued per tile, so
+// this kernel is used only for full tiles (M % BM == 0, N % BN == 0): no store is predicated.
+template <class Mma, int OUT, int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(WM* WN * 64) void gemm_tn_persist_kernel(const GemmArgs p) {
+  constexpr int NW = WM * WN, ROWB = 128;
+  constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, STAGE = A_BYTES + B_BYTES;
+  constexpr int TM = BM / WM, TN = BN / WN, MR = TM / 16, NR = TN / 16;
+  constexpr int LA = BM / 8 / NW, LB = BN / 8 / NW;
+  constexpr int NSTORE = MR * NR;
+  static_assert(NSTORE <= 63, "vmcnt is a 6-bit counter");
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles_n = p.N / BN, tiles_m = p.M / BM, ntiles = tiles_m * tiles_n;
+  const int esz = Mma::kElem;
+  const int nk = p.K * esz / ROWB;
+  const int my_tiles = ((int)blockIdx.x < ntiles) ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int total = my_tiles * nk;
+  if (total == 0) return;
+
+  const char* aptr[LA];
+  const char* bptr[LB];
+  int cur_tile = -1;
+  auto set_tile = [&](int i) {  // i-th tile of this block -> source pointers
+    const int wg = tile_index_virtual(p, (int)blockIdx.x + i * (int)gridDim.x, ntiles);
+    const int64_t m0 = (int64_t)(wg / tiles_n) * BM, n0 = (int64_t)(wg % tiles_n) * BN;
+#pragma unroll
+    for (int r = 0; r < LA; ++r) {
+      const int row = (wave * LA + r) * 8 + (lane >> 3);
+      const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+      aptr[r] = (const char*)p.a + map_row(m0 + row, p.a_grp, p.a_gstride) * p.lda * esz +
+                chunk * 16;
+    }
+#pragma unroll
+    for (int r = 0; r < LB; ++r) {
+      const int row = (wave * LB + r) * 8 + (lane >> 3);
+      const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+      bptr[r] = (const char*)p.b + (n0 + row) * p.ldb * esz + chunk * 16;
+    }
+  };
+  auto stage = [&](int buf, int g) {
+    const int ti = g / nk, kt = g - ti * nk;
+    if (ti != cur_tile) {
+      set_tile(ti);
+      cur_tile = ti;
+    }
+    char* base = smem + buf * STAGE;
+    const int64_t koff = (int64_t)kt * ROWB;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) glds16(aptr[i] + koff, base + (wave * LA + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < LB; ++i) glds16(bptr[i] + koff, base + A_BYTES + (wave * LB + i) * 1024);
+  };
+
+  const int wm = wave / WN, wn = wave % WN;
+  const int swz = (lane & 15) >> 1, frow = lane & 15, fq = lane >> 4;
+  f32x4 acc[MR][NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf) {
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int c4 = 0; c4 < 8; c4 += 4) {
+      const int choff = ((c4 + fq) ^ swz) * 16;
+      i32x4 af[MR], bfr[NR];
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+        af[i] = *(const i32x4*)(As + (wm * TM + i * 16 + frow) * ROWB + choff);
+#pragma unroll
+      for (int j = 0; j < NR; ++j)
+        bfr[j] = *(const i32x4*)(Bs + (wn * TN + j * 16 + frow) * ROWB + choff);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j) Mma::step(acc[i][j], bfr[j], af[i]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  };
+  constexpr int OSZ = out_size<OUT>();
+  auto epilogue = [&](int ti) {
+    const int wg = tile_index_virtual(p, (int)blockIdx.x + ti * (int)gridDim.x, ntiles);
+    const int64_t m0 = (int64_t)(wg / tiles_n) * BM, n0 = (int64_t)(wg % tiles_n) * BN;
+#pragma unroll
+    for (int i = 0; i < MR; ++i) {
+      const int64_t row = m0 + wm * TM + i * 16 + frow;
+      char* crow = (char*)p.c + map_row(row, p.c_grp, p.c_gstride) * p.ldc * OSZ;
+#pragma unroll
+      for (int j = 0; j < NR; ++j) {
+        const int64_t col = n0 + wn * TN + j * 16 + fq * 4;
+        Store4<OUT>::st(crow + col * OSZ, acc[i][j]);
+        acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  int cur = 0;
+  for (int g = 0; g < total; ++g) {
+    const bool more = g + 1 < total;
+    if (more) stage(cur ^ 1, g + 1);
+    compute(cur);
+    const bool last_k = (g % nk) == nk - 1;
+    if (last_k) {
+      __builtin_amdgcn_sched_barrier(0);
+      epilogue(g / nk);
+      __builtin_amdgcn_sched_barrier(0);
+      if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSTORE) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    cur ^= 1;
   }
 }
 
@@ -607,17 +813,40 @@ __global__ __launch_bounds__(256) void gemm_generic_kernel(const GemmArgs p) {
 }
 
 // ---------------------------------------------------------------- dispatch
-template <class Mma, int OUT, int BM, int BN, int WM, int WN>
+template <class Mma, int OUT, int BM, int BN, int WM, int WN, bool ILV = false>
 hipError_t launch_tiled(const GemmArgs& p, hipStream_t s) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_tn_kernel<Mma, OUT, BM, BN, WM, WN>), dim3(tiles), dim3(WM * WN * 64),
-                     0, s, p);
+  hipLaunchKernelGGL((gemm_tn_kernel<Mma, OUT, BM, BN, WM, WN, ILV>), dim3(tiles),
+                     dim3(WM * WN * 64), 0, s, p);
   return hipGetLastError();
 }
 template <int OUT, int BM, int BN, int WM, int WN>
 hipError_t launch_mx(const GemmArgs& p, hipStream_t s) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
   hipLaunchKernelGGL((gemm_tn_mxfp8_kernel<OUT, BM, BN, WM, WN>), dim3(tiles),
+                     dim3(WM * WN * 64), 0, s, p);
+  return hipGetLastError();
+}
+
+int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+template <class Mma, int OUT, int BM, int BN, int WM, int WN>
+hipError_t launch_persist(const GemmArgs& p, int blocks_per_cu, hipStream_t s) {
+  const int tiles = (p.M / BM) * (p.N / BN);
+  int grid = num_cus() * blocks_per_cu;
+  grid = (grid / 8) * 8;  // keep blockIdx % 8 == XCD group for every virtual tile id
+  if (grid > tiles) grid = tiles;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL((gemm_tn_persist_kernel<Mma, OUT, BM, BN, WM, WN>), dim3(grid),
                      dim3(WM * WN * 64), 0, s, p);
   return hipGetLastError();
 }
@@ -639,6 +868,17 @@ hipError_t launch_cfg(const GemmArgs& p, int tile, hipStream_t s) {
     case TILE_128x128: return launch_tiled<Mma, OUT, 128, 128, 2, 2>(p, s);
     case TILE_256x256_W4: return launch_tiled<Mma, OUT, 256, 256, 2, 2>(p, s);
     case TILE_256x128_W4: return launch_tiled<Mma, OUT, 256, 128, 2, 2>(p, s);
+    case TILE_I256: return launch_tiled<Mma, OUT, 256, 256, 2, 4, true>(p, s);
+    case TILE_I128: return launch_tiled<Mma, OUT, 128, 128, 2, 2, true>(p, s);
+    case TILE_I256W4: return launch_tiled<Mma, OUT, 256, 256, 2, 2, true>(p, s);
+    case TILE_P256:
+      if (p.M % 256 == 0 && p.N % 256 == 0 && p.flags == nullptr)
+        return launch_persist<Mma, OUT, 256, 256, 2, 4>(p, 1, s);
+      return launch_tiled<Mma, OUT, 256, 256, 2, 4>(p, s);
+    case TILE_P128:
+      if (p.M % 128 == 0 && p.N % 128 == 0 && p.flags == nullptr)
+        return launch_persist<Mma, OUT, 128, 128, 2, 2>(p, 2, s);
+      return launch_tiled<Mma, OUT, 128, 128, 2, 2>(p, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -651,6 +891,10 @@ hipError_t launch_mx_cfg(const GemmArgs& p, int tile, hipStream_t s) {
     case TILE_128x256: return launch_mx<OUT, 128, 256, 2, 4>(p, s);
     case TILE_128x128: return launch_mx<OUT, 128, 128, 2, 2>(p, s);
     case TILE_256x256_W4: return launch_mx<OUT, 256, 256, 2, 2>(p, s);
+    case TILE_P256: case TILE_I256: return launch_mx<OUT, 256, 256, 2, 4>(p, s);
+    case TILE_I128: return launch_mx<OUT, 128, 128, 2, 2>(p, s);
+    case TILE_I256W4: return launch_mx<OUT, 256, 256, 2, 2>(p, s);
+    case TILE_P128: return launch_mx<OUT, 128, 128, 2, 2>(p, s);
     case TILE_256x128_W4: return launch_mx<OUT, 256, 128, 2, 2>(p, s);
     default: return hipErrorInvalidValue;
   }
@@ -668,9 +912,13 @@ hipError_t launch_generic_t(const GemmArgs& p, hipStream_t s) {
 
 }  // namespace
 
-int tile_rows(int tile) { return (tile == TILE_128x128 || tile == TILE_128x256) ? 128 : 256; }
+int tile_rows(int tile) {
+  return (tile == TILE_128x128 || tile == TILE_128x256 || tile == TILE_P128 || tile == TILE_I128)
+             ? 128 : 256;
+}
 int tile_cols(int tile) {
-  return (tile == TILE_256x128 || tile == TILE_128x128 || tile == TILE_256x128_W4) ? 128 : 256;
+  return (tile == TILE_256x128 || tile == TILE_128x128 || tile == TILE_256x128_W4 ||
+          tile == TILE_P128 || tile == TILE_I128) ? 128 : 256;
 }
 
 bool gemm_fast_path_ok(const GemmArgs& p, int din, int dout) {
@@ -688,7 +936,7 @@ bool gemm_fast_path_ok(const GemmArgs& p, int din, int dout) {
 int choose_tile(int64_t M, int64_t N, int din) {
   // Fill the 256 CUs: prefer the big tile while it yields >= ~1.5 waves of blocks.
   auto tiles = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
-  if (tiles(256, 256) >= 384) return TILE_PP256;
+  if (tiles(256, 256) >= 384) return TILE_I256;
   if (tiles(256, 128) >= 384) return TILE_256x128;
   if (tiles(128, 256) >= 384) return TILE_128x256;
   return TILE_128x128;

@@ -35,7 +35,7 @@ def gen():
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
-@pytest.mark.parametrize("tile", ["256x256", "256x128", "128x256", "128x128", "pp256", "256x256w4", "256x128w4"])
+@pytest.mark.parametrize("tile", ["256x256", "256x128", "128x256", "128x128", "pp256", "256x256w4", "256x128w4", "p256", "p128", "i256", "i128"])
 def test_gemm_tiles(dtype, tile, gen):
     from ddlb_amd.ops.gemm import gemm
 
@@ -96,7 +96,7 @@ def test_gemm_fp8(mode, odt, gen):
     torch.testing.assert_close(out.float(), _ref(a, w), rtol=0, atol=_tol(torch.float8_e4m3fn, K))
 
 
-@pytest.mark.parametrize("tile", ["auto", "pp256", "128x128", "256x256w4", "256x128w4"])
+@pytest.mark.parametrize("tile", ["auto", "pp256", "128x128", "256x256w4", "256x128w4", "p256", "p128", "i256", "i128"])
 def test_fp8_integer_exact(gen, tile):
     """Small integers are exact in e4m3: both fp8 paths must match bit for bit."""
     from ddlb_amd.ops.gemm import gemm
@@ -133,7 +133,7 @@ def test_grouped_rows(gen):
     assert torch.count_nonzero(C[untouched].float()) == 0
 
 
-@pytest.mark.parametrize("tile", ["auto", "pp256", "128x128", "256x256w4", "256x128w4"])
+@pytest.mark.parametrize("tile", ["auto", "pp256", "128x128", "256x256w4", "256x128w4", "p256", "p128", "i256", "i128"])
 @pytest.mark.parametrize("shape", [(2048, 1024, 1024), (4096, 2048, 2048), (768, 512, 192)])
 def test_repeat_race_screen(gen, tile, shape):
     """Same inputs, 20 launches: identical bits every time (LDS-DMA/barrier race screen)."""
@@ -159,3 +159,25 @@ def test_host_checks_reject_bad_shapes(gen):
         gemm(a, w)
     with pytest.raises(ValueError):
         gemm(a, _rand((64, 128), torch.bfloat16, gen), M=128)
+
+
+@pytest.mark.parametrize("tile", ["p256", "p128"])
+def test_persistent_many_tiles_grouped(gen, tile):
+    """Persistent streaming kernel: more tiles than blocks, grouped C rows, repeat-identical."""
+    from ddlb_amd.ops.gemm import gemm
+
+    M, N, K = 8192, 1024, 512
+    a, w = _rand((M, K), torch.bfloat16, gen), _rand((N, K), torch.bfloat16, gen)
+    out = torch.zeros((2 * M, N), dtype=torch.bfloat16, device=DEV)
+    gemm(a, w, out, tile=tile, c_grp=1024, c_gstride=2048)
+    torch.cuda.synchronize()
+    ref = _ref(a, w)
+    for blk in range(M // 1024):
+        torch.testing.assert_close(out[blk * 2048:blk * 2048 + 1024].float(),
+                                   ref[blk * 1024:(blk + 1) * 1024], rtol=0, atol=_tol(torch.bfloat16, K))
+        assert torch.count_nonzero(out[blk * 2048 + 1024:(blk + 1) * 2048]) == 0
+    first = out.clone()
+    for _ in range(10):
+        gemm(a, w, out, tile=tile, c_grp=1024, c_gstride=2048)
+    torch.cuda.synchronize()
+    assert torch.equal(out, first)
