@@ -49,6 +49,8 @@ CANDIDATES = [
     ("default/ipc/kernel", "native", dict(algorithm="default", backend="ipc",
                                            multicast_protocol="kernel", copy_blocks=128)),
     ("coll_pipeline/rccl/s8", "native", dict(algorithm="coll_pipeline", backend="rccl", s=8)),
+    ("coll_pipeline/rccl/s4/graph", "native", dict(algorithm="coll_pipeline", backend="rccl", s=4,
+                                                    graph=True)),
     ("pytorch(rccl+hipblaslt)", "pytorch", dict(backend="nccl", empty_cache=False)),
 ]
 

@@ -84,15 +84,17 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm",
         [](uintptr_t a, uintptr_t b, uintptr_t c, int64_t lda, int64_t ldb, int64_t ldc, int M,
            int N, int K, int din, int dout, int tile, int mode, int64_t a_grp, int64_t a_gstride,
-           int64_t c_grp, int64_t c_gstride, uintptr_t stream) {
+           int64_t c_grp, int64_t c_gstride, uintptr_t stream, int act) {
           GemmArgs g = make_args(a, b, c, lda, ldb, ldc, M, N, K, a_grp, a_gstride, c_grp,
                                  c_gstride);
+          g.act = act;
           check(gemm_launch(g, din, dout, tile, mode, (hipStream_t)stream), "gemm_launch");
         },
         py::arg("a"), py::arg("b"), py::arg("c"), py::arg("lda"), py::arg("ldb"), py::arg("ldc"),
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("din"), py::arg("dout"),
         py::arg("tile") = 0, py::arg("mode") = 0, py::arg("a_grp") = 0, py::arg("a_gstride") = 0,
-        py::arg("c_grp") = 0, py::arg("c_gstride") = 0, py::arg("stream") = 0);
+        py::arg("c_grp") = 0, py::arg("c_gstride") = 0, py::arg("stream") = 0,
+        py::arg("act") = 0);
   m.def("gemm_fast_path_ok",
         [](uintptr_t a, uintptr_t b, uintptr_t c, int64_t lda, int64_t ldb, int64_t ldc, int M,
            int N, int K, int din, int dout) {
@@ -163,5 +165,8 @@ PYBIND11_MODULE(_C, m) {
       .def("nops", &PlanExecutor::nops)
       .def("stream", &PlanExecutor::stream)
       .def("timeout_word", &PlanExecutor::timeout_word)
-      .def("read_timeout", &PlanExecutor::read_timeout);
+      .def("read_timeout", &PlanExecutor::read_timeout)
+      .def("enable_graph", &PlanExecutor::enable_graph)
+      .def("graph_enabled", &PlanExecutor::graph_enabled)
+      .def("graph_capturable", &PlanExecutor::graph_capturable);
 }

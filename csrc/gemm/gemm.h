@@ -21,7 +21,7 @@ enum Tile : int { TILE_AUTO = 0, TILE_256x256 = 1, TILE_256x128 = 2, TILE_128x25
                   TILE_128x128 = 4, TILE_PP256 = 5, TILE_256x256_W4 = 6, TILE_256x128_W4 = 7,
                   TILE_P256 = 8, TILE_P128 = 9,     // P*: persistent streaming variants
                   TILE_I256 = 10, TILE_I128 = 11,    // I*: DMA interleaved into the MFMAs
-                  TILE_I256W4 = 12 };
+                  TILE_I256W4 = 12, TILE_PI256 = 13 };
 enum GemmMode : int { GEMM_MODE_AUTO = 0, GEMM_MODE_GENERIC = 1, GEMM_MODE_MX = 2 };
 
 // C[M,N] = A[M,K] * Bt[N,K]^T. Leading dimensions in ELEMENTS.
@@ -40,7 +40,9 @@ struct GemmArgs {
   int64_t flag_rows = 1;            // physical A rows per shard
   unsigned* timeout_word = nullptr; // set to 1 if a spin gave up
   int tile_order = 0, nshards = 1, first_shard = 0;
+  int act = 0;                      // fused epilogue activation: ACT_* below
 };
+enum Act : int { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_SILU = 3 };
 
 hipError_t gemm_launch(const GemmArgs& p, int din, int dout, int tile, int mode, hipStream_t s);
 bool gemm_fast_path_ok(const GemmArgs& p, int din, int dout);

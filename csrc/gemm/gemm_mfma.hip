@@ -132,6 +132,23 @@ struct IlvPattern {
   }
 };
 
+// ---------------------------------------------------------------- fused epilogue activation
+__device__ __forceinline__ float act1(float x, int act) {
+  switch (act) {
+    case ACT_GELU: {  // tanh approximation (what Megatron / TE use for GPT-style MLPs)
+      const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+      return 0.5f * x * (1.f + tanhf(u));
+    }
+    case ACT_RELU: return x > 0.f ? x : 0.f;
+    case ACT_SILU: return x / (1.f + __expf(-x));
+    default: return x;
+  }
+}
+__device__ __forceinline__ f32x4 act4(f32x4 v, int act) {
+  if (act == ACT_NONE) return v;
+  return f32x4{act1(v.x, act), act1(v.y, act), act1(v.z, act), act1(v.w, act)};
+}
+
 // ---------------------------------------------------------------- output conversion
 template <int OUT> struct Store4;
 template <> struct Store4<DT_BF16> {
@@ -339,9 +356,10 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_kernel(const GemmArgs p) 
     for (int j = 0; j < NR; ++j) {
       const int64_t col = n0 + wn * TN + j * 16 + fq * 4;
       if (col + 3 < p.N) {
-        Store4<OUT>::st(crow + col * OSZ, acc[i][j]);
+        Store4<OUT>::st(crow + col * OSZ, act4(acc[i][j], p.act));
       } else {
-        const float v[4] = {acc[i][j].x, acc[i][j].y, acc[i][j].z, acc[i][j].w};
+        const f32x4 a4 = act4(acc[i][j], p.act);
+        const float v[4] = {a4.x, a4.y, a4.z, a4.w};
         for (int r = 0; r < 4; ++r)
           if (col + r < p.N) Store4<OUT>::st1(crow + (col + r) * OSZ, v[r]);
       }
@@ -357,7 +375,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_kernel(const GemmArgs p) 
 // vmcnt queue, so waiting for "at most NSTORE outstanding" retires the (older) DMA while the C
 // stores keep draining under tile i+1's MFMAs. Exactly NSTORE stores must be issued per tile, so
 // this kernel is used only for full tiles (M % BM == 0, N % BN == 0): no store is predicated.
-template <class Mma, int OUT, int BM, int BN, int WM, int WN>
+template <class Mma, int OUT, int BM, int BN, int WM, int WN, bool ILV = false>
 __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_persist_kernel(const GemmArgs p) {
   constexpr int NW = WM * WN, ROWB = 128;
   constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, STAGE = A_BYTES + B_BYTES;
@@ -449,10 +467,55 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_persist_kernel(const Gemm
 #pragma unroll
       for (int j = 0; j < NR; ++j) {
         const int64_t col = n0 + wn * TN + j * 16 + fq * 4;
-        Store4<OUT>::st(crow + col * OSZ, acc[i][j]);
+        Store4<OUT>::st(crow + col * OSZ, act4(acc[i][j], p.act));
         acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
+  };
+
+  // interleaved compute (see gemm_tn_kernel::compute_ilv): next step's DMA + second-half
+  // fragment reads issued between the first-half MFMAs
+  auto compute_ilv = [&](int buf, int64_t koff) {
+    constexpr int NDMA = LA + LB, NRD = MR + NR, NQ = MR * NR;
+    constexpr int PER = NQ / NDMA > 0 ? NQ / NDMA : 1;
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + A_BYTES;
+    char* nbase = smem + (buf ^ 1) * STAGE;
+    const int ch0 = ((0 + fq) ^ swz) * 16, ch1 = ((4 + fq) ^ swz) * 16;
+    i32x4 af0[MR], bf0[NR], af1[MR], bf1[NR];
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+      af0[i] = *(const i32x4*)(As + (wm * TM + i * 16 + frow) * ROWB + ch0);
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+      bf0[j] = *(const i32x4*)(Bs + (wn * TN + j * 16 + frow) * ROWB + ch0);
+    auto rd1 = [&](int r) {
+      if (r < MR) af1[r] = *(const i32x4*)(As + (wm * TM + r * 16 + frow) * ROWB + ch1);
+      else bf1[r - MR] = *(const i32x4*)(Bs + (wn * TN + (r - MR) * 16 + frow) * ROWB + ch1);
+    };
+    auto dma = [&](int d) {
+      if (d < LA) glds16(aptr[d] + koff, nbase + (wave * LA + d) * 1024);
+      else glds16(bptr[d - LA] + koff, nbase + A_BYTES + (wave * LB + d - LA) * 1024);
+    };
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      Mma::step(acc[q / NR][q % NR], bf0[q % NR], af0[q / NR]);
+      if ((q % PER) == PER - 1) {
+        const int gg = q / PER;
+        if (gg < NDMA) dma(gg);
+#pragma unroll
+        for (int r = (gg * NRD) / NDMA; r < ((gg + 1) * NRD) / NDMA; ++r) rd1(r);
+      }
+    }
+#pragma unroll
+    for (int d = NQ / PER; d < NDMA; ++d) dma(d);
+#pragma unroll
+    for (int r = ((NQ / PER) * NRD) / NDMA; r < NRD; ++r) rd1(r);
+    IlvPattern<0, (NDMA < NQ / PER ? NDMA : NQ / PER), PER, NRD, NDMA>::emit();
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) Mma::step(acc[q / NR][q % NR], bf1[q % NR], af1[q / NR]);
+    __builtin_amdgcn_s_setprio(0);
   };
 
   stage(0, 0);
@@ -461,8 +524,19 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_persist_kernel(const Gemm
   int cur = 0;
   for (int g = 0; g < total; ++g) {
     const bool more = g + 1 < total;
-    if (more) stage(cur ^ 1, g + 1);
-    compute(cur);
+    if constexpr (ILV) {
+      // last step of the stream: re-stage the current k-step into the idle buffer (never read)
+      const int gn = more ? g + 1 : g;
+      const int ti = gn / nk;
+      if (ti != cur_tile) {
+        set_tile(ti);
+        cur_tile = ti;
+      }
+      compute_ilv(cur, (int64_t)(gn - ti * nk) * ROWB);
+    } else {
+      if (more) stage(cur ^ 1, g + 1);
+      compute(cur);
+    }
     const bool last_k = (g % nk) == nk - 1;
     if (last_k) {
       __builtin_amdgcn_sched_barrier(0);
@@ -475,6 +549,8 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_persist_kernel(const Gemm
     __builtin_amdgcn_s_barrier();
     cur ^= 1;
   }
+  // never leave an LDS-DMA in flight past the end of the workgroup (its LDS is reassigned)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // ---------------------------------------------------------------- 256x256 ping-pong kernel
@@ -633,9 +709,10 @@ __global__ __launch_bounds__(512) void gemm_tn_pp256_kernel(const GemmArgs p) {
     for (int j = 0; j < 4; ++j) {
       const int64_t col = n0 + wc * 64 + (j >> 1) * 32 + (j & 1) * 16 + fq * 4;
       if (col + 3 < p.N) {
-        Store4<OUT>::st(crow + col * OSZ, acc[i][j]);
+        Store4<OUT>::st(crow + col * OSZ, act4(acc[i][j], p.act));
       } else {
-        const float v[4] = {acc[i][j].x, acc[i][j].y, acc[i][j].z, acc[i][j].w};
+        const f32x4 a4 = act4(acc[i][j], p.act);
+        const float v[4] = {a4.x, a4.y, a4.z, a4.w};
         for (int r = 0; r < 4; ++r)
           if (col + r < p.N) Store4<OUT>::st1(crow + (col + r) * OSZ, v[r]);
       }
@@ -742,9 +819,10 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_mxfp8_kernel(const GemmAr
     for (int j = 0; j < NR; ++j) {
       const int64_t col = n0 + wn * TN + j * 16 + fq * 4;
       if (col + 3 < p.N) {
-        Store4<OUT>::st(crow + col * OSZ, acc[i][j]);
+        Store4<OUT>::st(crow + col * OSZ, act4(acc[i][j], p.act));
       } else {
-        const float v[4] = {acc[i][j].x, acc[i][j].y, acc[i][j].z, acc[i][j].w};
+        const f32x4 a4 = act4(acc[i][j], p.act);
+        const float v[4] = {a4.x, a4.y, a4.z, a4.w};
         for (int r = 0; r < 4; ++r)
           if (col + r < p.N) Store4<OUT>::st1(crow + (col + r) * OSZ, v[r]);
       }
@@ -807,7 +885,7 @@ __global__ __launch_bounds__(256) void gemm_generic_kernel(const GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int64_t c = (int64_t)tn * 64 + tx * 4 + j;
-      if (c < p.N) store_elem<DOUT>(C, rp + c, (double)acc[i][j]);
+      if (c < p.N) store_elem<DOUT>(C, rp + c, (double)act1((float)acc[i][j], p.act));
     }
   }
 }
@@ -839,14 +917,14 @@ int num_cus() {
   return n;
 }
 
-template <class Mma, int OUT, int BM, int BN, int WM, int WN>
+template <class Mma, int OUT, int BM, int BN, int WM, int WN, bool ILV = false>
 hipError_t launch_persist(const GemmArgs& p, int blocks_per_cu, hipStream_t s) {
   const int tiles = (p.M / BM) * (p.N / BN);
   int grid = num_cus() * blocks_per_cu;
   grid = (grid / 8) * 8;  // keep blockIdx % 8 == XCD group for every virtual tile id
   if (grid > tiles) grid = tiles;
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL((gemm_tn_persist_kernel<Mma, OUT, BM, BN, WM, WN>), dim3(grid),
+  hipLaunchKernelGGL((gemm_tn_persist_kernel<Mma, OUT, BM, BN, WM, WN, ILV>), dim3(grid),
                      dim3(WM * WN * 64), 0, s, p);
   return hipGetLastError();
 }
@@ -871,6 +949,10 @@ hipError_t launch_cfg(const GemmArgs& p, int tile, hipStream_t s) {
     case TILE_I256: return launch_tiled<Mma, OUT, 256, 256, 2, 4, true>(p, s);
     case TILE_I128: return launch_tiled<Mma, OUT, 128, 128, 2, 2, true>(p, s);
     case TILE_I256W4: return launch_tiled<Mma, OUT, 256, 256, 2, 2, true>(p, s);
+    case TILE_PI256:
+      if (p.M % 256 == 0 && p.N % 256 == 0 && p.flags == nullptr)
+        return launch_persist<Mma, OUT, 256, 256, 2, 4, true>(p, 1, s);
+      return launch_tiled<Mma, OUT, 256, 256, 2, 4, true>(p, s);
     case TILE_P256:
       if (p.M % 256 == 0 && p.N % 256 == 0 && p.flags == nullptr)
         return launch_persist<Mma, OUT, 256, 256, 2, 4>(p, 1, s);
@@ -894,6 +976,7 @@ hipError_t launch_mx_cfg(const GemmArgs& p, int tile, hipStream_t s) {
     case TILE_P256: case TILE_I256: return launch_mx<OUT, 256, 256, 2, 4>(p, s);
     case TILE_I128: return launch_mx<OUT, 128, 128, 2, 2>(p, s);
     case TILE_I256W4: return launch_mx<OUT, 256, 256, 2, 2>(p, s);
+    case TILE_PI256: return launch_mx<OUT, 256, 256, 2, 4>(p, s);
     case TILE_P128: return launch_mx<OUT, 128, 128, 2, 2>(p, s);
     case TILE_256x128_W4: return launch_mx<OUT, 256, 128, 2, 2>(p, s);
     default: return hipErrorInvalidValue;

@@ -33,6 +33,9 @@ PlanExecutor::PlanExecutor(int device, int nstreams, int nevents,
 
 PlanExecutor::~PlanExecutor() {
   hipSetDevice(device_);
+  if (graph_exec_) hipGraphExecDestroy(graph_exec_);
+  if (graph_) hipGraphDestroy(graph_);
+  if (cap_stream_) hipStreamDestroy(cap_stream_);
   for (size_t i = 1; i < streams_.size(); ++i)
     if (streams_[i]) {
       hipStreamSynchronize(streams_[i]);
@@ -62,6 +65,28 @@ void PlanExecutor::load(const std::vector<int64_t>& ops) {
     }
   }
   ops_ = ops;
+  any_side_ = false;
+  for (size_t i = 1; i < used_.size(); ++i) any_side_ = any_side_ || used_[i];
+  if (graph_exec_) { hipGraphExecDestroy(graph_exec_); graph_exec_ = nullptr; }
+  if (graph_) { hipGraphDestroy(graph_); graph_ = nullptr; }
+}
+
+bool PlanExecutor::graph_capturable() const {
+  for (size_t i = 0; i < ops_.size(); i += kOpWords) {
+    const int64_t k = ops_[i];
+    if (k == OP_SIGNAL || k == OP_WAIT_SIGNAL) return false;
+    if (k == OP_GEMM && ops_[i + 19] != 0) return false;
+  }
+  return true;
+}
+
+void PlanExecutor::enable_graph(bool on) {
+  if (on && !graph_capturable())
+    throw std::runtime_error("plan has epoch-dependent ops (signals / arrival flags): "
+                             "it cannot be replayed from a hipGraph");
+  graph_on_ = on;
+  if (on && cap_stream_ == nullptr)
+    DDLB_HIP(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking));
 }
 
 unsigned PlanExecutor::read_timeout() {
@@ -70,20 +95,45 @@ unsigned PlanExecutor::read_timeout() {
   return v;
 }
 
+void PlanExecutor::enqueue(hipStream_t main) {
+  if (any_side_) {
+    // fork: every used side stream waits for everything already queued on `main`
+    DDLB_HIP(hipEventRecord(fork_join_[0], main));
+    for (size_t i = 1; i < streams_.size(); ++i)
+      if (used_[i]) DDLB_HIP(hipStreamWaitEvent(streams_[i], fork_join_[0], 0));
+  }
+  for (size_t i = 0; i < ops_.size(); i += kOpWords) exec(&ops_[i], main);
+  if (any_side_) {  // join
+    for (size_t i = 1; i < streams_.size(); ++i)
+      if (used_[i]) {
+        DDLB_HIP(hipEventRecord(fork_join_[streams_.size() + i], streams_[i]));
+        DDLB_HIP(hipStreamWaitEvent(main, fork_join_[streams_.size() + i], 0));
+      }
+  }
+}
+
 unsigned PlanExecutor::run(uintptr_t main_stream) {
   hipStream_t main = (hipStream_t)main_stream;
   ++epoch_;
-  // fork: every used side stream waits for everything already queued on the caller's stream
-  DDLB_HIP(hipEventRecord(fork_join_[0], main));
-  for (size_t i = 1; i < streams_.size(); ++i)
-    if (used_[i]) DDLB_HIP(hipStreamWaitEvent(streams_[i], fork_join_[0], 0));
-  for (size_t i = 0; i < ops_.size(); i += kOpWords) exec(&ops_[i], main);
-  // join
-  for (size_t i = 1; i < streams_.size(); ++i)
-    if (used_[i]) {
-      DDLB_HIP(hipEventRecord(fork_join_[streams_.size() + i], streams_[i]));
-      DDLB_HIP(hipStreamWaitEvent(main, fork_join_[streams_.size() + i], 0));
+  if (!graph_on_) {
+    enqueue(main);
+    return epoch_;
+  }
+  if (graph_exec_ == nullptr) {
+    // capture on a private stream (the caller's may be the legacy null stream)
+    DDLB_HIP(hipStreamBeginCapture(cap_stream_, hipStreamCaptureModeRelaxed));
+    try {
+      enqueue(cap_stream_);
+    } catch (...) {
+      hipGraph_t g = nullptr;
+      hipStreamEndCapture(cap_stream_, &g);
+      if (g) hipGraphDestroy(g);
+      throw;
     }
+    DDLB_HIP(hipStreamEndCapture(cap_stream_, &graph_));
+    DDLB_HIP(hipGraphInstantiate(&graph_exec_, graph_, nullptr, nullptr, 0));
+  }
+  DDLB_HIP(hipGraphLaunch(graph_exec_, main));
   return epoch_;
 }
 
@@ -106,6 +156,7 @@ void PlanExecutor::exec(const int64_t* o, hipStream_t main) {
       g.nshards = o[21] > 0 ? (int)o[21] : 1;
       g.first_shard = (int)o[22];
       g.tile_order = (int)o[23];
+      g.act = (int)o[24];
       g.timeout_word = d_timeout_;
       DDLB_HIP(gemm_launch(g, (int)o[15], (int)o[16], (int)o[17], (int)o[18], s));
       return;

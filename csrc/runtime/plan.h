@@ -25,7 +25,7 @@ enum OpKind : int64_t {
   OP_GEMM = 1,        // 2 a, 3 b, 4 c, 5 lda, 6 ldb, 7 ldc, 8 a_grp, 9 a_gstride, 10 c_grp,
                       // 11 c_gstride, 12 M, 13 N, 14 K, 15 din, 16 dout, 17 tile, 18 mode,
                       // 19 flags ptr (0 = none), 20 flag_rows, 21 nshards, 22 first_shard,
-                      // 23 tile_order
+                      // 23 tile_order, 24 fused epilogue activation
   OP_RECORD = 2,      // 2 event
   OP_WAIT = 3,        // 2 event
   OP_ALLGATHER = 4,   // 2 send, 3 recv, 4 count per rank, 5 dtype
@@ -58,9 +58,21 @@ class PlanExecutor {
   uintptr_t timeout_word() const { return (uintptr_t)d_timeout_; }
   unsigned read_timeout();  // synchronous; 0 = healthy
   uintptr_t stream(int i) const { return (uintptr_t)streams_.at(i); }
+  // hipGraph mode: the plan is captured once (on a private stream) and replayed with one
+  // hipGraphLaunch behind the caller's stream. Only for plans without epoch-dependent ops
+  // (cross-process signals / arrival-flag GEMMs read the epoch at enqueue time).
+  void enable_graph(bool on);
+  bool graph_enabled() const { return graph_on_; }
+  bool graph_capturable() const;
 
  private:
   void exec(const int64_t* op, hipStream_t main);
+  void enqueue(hipStream_t main);
+  bool any_side_ = false;
+  bool graph_on_ = false;
+  hipStream_t cap_stream_ = nullptr;
+  hipGraph_t graph_ = nullptr;
+  hipGraphExec_t graph_exec_ = nullptr;
   hipStream_t S(int64_t idx, hipStream_t main) const {
     return idx == 0 ? main : streams_.at((size_t)idx);
   }

@@ -20,8 +20,9 @@ from ddlb_amd.ops import load
 DT_F32, DT_F16, DT_BF16, DT_FP8, DT_F64, DT_U8 = 0, 1, 2, 3, 4, 5
 TILES = {"auto": 0, "256x256": 1, "256x128": 2, "128x256": 3, "128x128": 4, "pp256": 5, "256x256w4": 6,
          "256x128w4": 7, "p256": 8, "p128": 9,
-         "i256": 10, "i128": 11, "i256w4": 12}
+         "i256": 10, "i128": 11, "i256w4": 12, "pi256": 13}
 MODES = {"auto": 0, "generic": 1, "mx": 2}
+ACTS = {"none": 0, "gelu": 1, "relu": 2, "silu": 3}
 
 SUPPORTED_IN = ("float32", "float16", "bfloat16", "float8_e4m3fn", "float64")
 
@@ -83,8 +84,9 @@ def _phys_rows(M: int, grp: int, gstride: int, base_rows: int = 0) -> int:
 
 def gemm(a, w, out=None, *, out_dtype=None, tile: str = "auto", mode: str = "auto",
          M: Optional[int] = None, a_grp: int = 0, a_gstride: int = 0, c_grp: int = 0,
-         c_gstride: int = 0, stream=None):
-    """``out[:M] = a[:M] @ w.T`` on the current HIP stream (grouped-row addressing optional)."""
+         c_gstride: int = 0, stream=None, act: str = "none"):
+    """``out[:M] = act(a[:M] @ w.T)`` on the current HIP stream (grouped-row addressing and a
+    fused epilogue activation — none / gelu (tanh) / relu / silu — optional)."""
     import torch
 
     C = load()
@@ -108,7 +110,7 @@ def gemm(a, w, out=None, *, out_dtype=None, tile: str = "auto", mode: str = "aut
     s = stream if stream is not None else torch.cuda.current_stream(a.device).cuda_stream
     C.gemm(a.data_ptr(), w.data_ptr(), out.data_ptr(), a.stride(0), w.stride(0), out.stride(0),
            M, N, K, dtype_code(a.dtype), dtype_code(out.dtype), TILES[tile], MODES[mode],
-           a_grp, a_gstride, c_grp, c_gstride, s)
+           a_grp, a_gstride, c_grp, c_gstride, s, ACTS[act])
     return out
 
 

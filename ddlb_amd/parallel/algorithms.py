@@ -56,6 +56,7 @@ class AlgoConfig:
     mode: int = 0                       # GEMM mode (0 auto, 2 MX-fp8)
     copy_blocks: int = 64               # CU budget of the kernel copy protocol
     fused: bool = False                 # p2p columnwise: one flag-gated GEMM launch
+    act: int = 0                        # columnwise: fused GEMM epilogue activation (ACT_*)
 
 
 @dataclass
@@ -155,17 +156,17 @@ def build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, dou
     plan = Plan(rank, d, nstreams=_nstreams(d), stream_priority=[0, 1] + [1] * max(d - 1, 1))
     plan.meta.update(primitive="tp_columnwise", algorithm=cfg.algorithm, backend=cfg.backend,
                      order=cfg.order)
-    A = plan.buffer("A_full", m * k * ein, symmetric=(cfg.backend == "ipc" or d > 1))
+    A = plan.buffer("A_full", m * k * ein, symmetric=(cfg.backend == "ipc"))
     Bt = plan.buffer("Bt", n * k * ein)
     flags = _Flags(plan, d, max(cfg.s, 1)) if cfg.backend == "ipc" and d > 1 else None
-    gdt = dict(din=din, dout=dout, tile=cfg.tile, mode=cfg.mode)
+    gdt = dict(din=din, dout=dout, tile=cfg.tile, mode=cfg.mode, act=cfg.act)
     comm_dt = DT_U8 if ein == 1 else din   # fp8 moves as bytes
 
     def arow(r0: int) -> Ref:
         return A + r0 * k * ein
 
     if cfg.order == "AG_after":
-        C = plan.buffer("C_full", m * n * eout, symmetric=True)
+        C = plan.buffer("C_full", m * n * eout, symmetric=(cfg.backend == "ipc"))
         io = PlanIO(TensorLoc("A_full", rank * ml * k * ein, ml, k, din),
                     TensorLoc("Bt", 0, n, k, din), TensorLoc("C_full", 0, m, n, dout))
         _col_ag_after(plan, rank, d, m, n, k, ein, eout, dout, cfg, A, Bt, C, flags, gdt)

@@ -18,6 +18,16 @@ from ddlb_amd.parallel.plan import (OP_ALLGATHER, OP_RECV, OP_REDUCE_SCATTER, OP
 from ddlb_amd.parallel.sim import TORCH_DT
 
 
+def _raw_stream(device_index: int) -> int:
+    """The caller's current HIP stream handle, without building a torch Stream object."""
+    import torch
+
+    getter = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+    if getter is not None:
+        return getter(device_index)
+    return torch.cuda.current_stream(device_index).cuda_stream
+
+
 class SymmetricBuffer:
     def __init__(self, ctx: "NativeContext", nbytes: int, zero: bool = True):
         import torch
@@ -98,8 +108,8 @@ class NativeContext:
             b.release()
         self._owned = [b for b in self._owned if b.h is not None]
 
-    def bind(self, plan: Plan) -> "BoundPlan":
-        return BoundPlan(self, plan)
+    def bind(self, plan: Plan, externals=None) -> "BoundPlan":
+        return BoundPlan(self, plan, externals)
 
     def close(self) -> None:
         for b in self._owned:
@@ -113,19 +123,35 @@ class NativeContext:
 
 
 class BoundPlan:
-    def __init__(self, ctx: NativeContext, plan: Plan):
+    """``externals`` maps a LOCAL buffer name to an existing device tensor that backs it
+    (zero-copy chaining: e.g. the columnwise output feeding the rowwise input of an MLP)."""
+
+    def __init__(self, ctx: NativeContext, plan: Plan, externals=None):
         import torch
 
         self.ctx, self.plan = ctx, plan
         self.local: Dict[str, torch.Tensor] = {}
         self.sym: Dict[str, SymmetricBuffer] = {}
         dev = torch.device("cuda", ctx.device_index)
+        externals = dict(externals or {})
         for name, spec in plan.buffers.items():  # dict order == identical on every rank
-            if spec.symmetric:
+            if name in externals:
+                t = externals.pop(name)
+                if spec.symmetric:
+                    raise ValueError(f"buffer {name} is symmetric; it cannot be external")
+                if not t.is_contiguous() or t.device != dev:
+                    raise ValueError(f"external {name} must be a contiguous tensor on {dev}")
+                raw = t.view(-1).view(torch.uint8)
+                if raw.numel() < spec.nbytes:
+                    raise ValueError(f"external {name}: {raw.numel()} B < {spec.nbytes} B needed")
+                self.local[name] = raw
+            elif spec.symmetric:
                 self.sym[name] = ctx.symmetric(spec.nbytes)
             else:
                 self.local[name] = torch.zeros(max(spec.nbytes, 16), dtype=torch.uint8,
                                                device=dev)
+        if externals:
+            raise ValueError(f"externals {sorted(externals)} are not buffers of this plan")
         words = plan.encode(self.resolve)
         C = ctx.C
         self.ex = C.PlanExecutor(ctx.device_index, plan.nstreams, max(plan.nevents, 1),
@@ -157,11 +183,13 @@ class BoundPlan:
         n = loc.rows * loc.cols * DT_SIZE[loc.dtype]
         return raw[loc.off:loc.off + n].view(TORCH_DT[loc.dtype]).view(loc.rows, loc.cols)
 
-    def run(self, stream: Optional[int] = None) -> int:
-        import torch
+    def enable_graph(self, on: bool = True) -> None:
+        """Replay the whole plan from one captured hipGraph (plans without signals only)."""
+        self.ex.enable_graph(on)
 
+    def run(self, stream: Optional[int] = None) -> int:
         if stream is None:
-            stream = torch.cuda.current_stream().cuda_stream
+            stream = _raw_stream(self.ctx.device_index)
         return self.ex.run(stream)
 
     def check_health(self) -> None:

@@ -36,6 +36,10 @@ DT_NAME = {DT_F32: "float32", DT_F16: "float16", DT_BF16: "bfloat16", DT_FP8: "f
            DT_F64: "float64", DT_U8: "uint8"}
 NAME_DT = {v: k for k, v in DT_NAME.items()}
 
+# fused GEMM epilogue activations (csrc/gemm/gemm.h ACT_*)
+ACT_NONE, ACT_GELU, ACT_RELU, ACT_SILU = 0, 1, 2, 3
+ACT_CODE = {"none": ACT_NONE, "gelu": ACT_GELU, "relu": ACT_RELU, "silu": ACT_SILU}
+
 # copy / signal methods
 COPY_ENGINE, COPY_KERNEL = 0, 1
 SIG_KERNEL, SIG_STREAM = 0, 1
@@ -113,12 +117,12 @@ class Plan:
              ldb: int, ldc: int, din: int, dout: int, a_grp: int = 0, a_gstride: int = 0,
              c_grp: int = 0, c_gstride: int = 0, tile: int = 0, mode: int = 0,
              flags: Optional[Ref] = None, flag_rows: int = 0, nshards: int = 1,
-             first_shard: int = 0, tile_order: int = 0) -> Op:
+             first_shard: int = 0, tile_order: int = 0, act: int = 0) -> Op:
         return self._add(OP_GEMM, stream, a=a, b=b, c=c, M=M, N=N, K=K, lda=lda, ldb=ldb, ldc=ldc,
                          din=din, dout=dout, a_grp=a_grp, a_gstride=a_gstride, c_grp=c_grp,
                          c_gstride=c_gstride, tile=tile, mode=mode, flags=flags,
                          flag_rows=flag_rows, nshards=nshards, first_shard=first_shard,
-                         tile_order=tile_order)
+                         tile_order=tile_order, act=act)
 
     def record(self, stream: int, event: int) -> Op:
         return self._add(OP_RECORD, stream, event=event)
@@ -197,7 +201,8 @@ class Plan:
                            a["ldc"], a["a_grp"], a["a_gstride"], a["c_grp"], a["c_gstride"]]
                 w[12:19] = [a["M"], a["N"], a["K"], a["din"], a["dout"], a["tile"], a["mode"]]
                 w[19] = resolve(a["flags"]) if a["flags"] is not None else 0
-                w[20:24] = [a["flag_rows"], a["nshards"], a["first_shard"], a["tile_order"]]
+                w[20:25] = [a["flag_rows"], a["nshards"], a["first_shard"], a["tile_order"],
+                            a.get("act", 0)]
             elif k in (OP_RECORD, OP_WAIT):
                 w[2] = a["event"]
             elif k in (OP_ALLGATHER, OP_REDUCE_SCATTER):

@@ -36,6 +36,17 @@ TORCH_DT = {DT_F32: torch.float32, DT_F16: torch.float16, DT_BF16: torch.bfloat1
             DT_FP8: torch.float8_e4m3fn, DT_F64: torch.float64, DT_U8: torch.uint8}
 
 
+def apply_act(x: torch.Tensor, act: int) -> torch.Tensor:
+    """f32 reference of the fused GEMM epilogue activations (csrc/gemm/gemm_mfma.hip act1)."""
+    if act == 1:
+        return torch.nn.functional.gelu(x, approximate="tanh")
+    if act == 2:
+        return torch.relu(x)
+    if act == 3:
+        return torch.nn.functional.silu(x)
+    return x
+
+
 class Deadlock(RuntimeError):
     pass
 
@@ -157,7 +168,7 @@ class Simulator:
                                   a["a_gstride"], a["lda"], a["K"], a["din"]).float()
             Bt = _view(self._buf(r, a["b"]), a["b"].off, (a["N"] - 1) * a["ldb"] + a["K"],
                        a["din"]).as_strided((a["N"], a["K"]), (a["ldb"], 1)).float()
-            Cv = A @ Bt.t()
+            Cv = apply_act(A @ Bt.t(), a.get("act", 0))
             self._scatter_rows(self._buf(r, a["c"]), a["c"].off, a["M"], a["c_grp"], a["c_gstride"],
                                a["ldc"], a["N"], a["dout"], Cv)
         elif k == OP_COPY:

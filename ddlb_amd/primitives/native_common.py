@@ -21,7 +21,9 @@ inter_stream_synchronization       serialise the per-peer transfers
 
 Native-only: ``signal`` (``stream`` = hipStreamWrite/WaitValue32 memops, ``kernel`` = tiny spin
 kernels), ``tile`` (GEMM tile or ``auto``), ``gemm_mode`` (``auto`` | ``mx`` for block-scaled fp8),
-``copy_blocks`` (CU budget of the kernel protocol), ``fused`` (p2p: one arrival-flag-gated GEMM).
+``copy_blocks`` (CU budget of the kernel protocol), ``fused`` (p2p: one arrival-flag-gated GEMM),
+``graph`` (capture the plan once and replay it as one hipGraph launch; ``auto`` = whenever the
+plan has no cross-process signals).
 """
 
 from __future__ import annotations
@@ -42,6 +44,7 @@ COMMON_DEFAULTS = {
     "gemm_mode": "auto",
     "copy_blocks": 64,
     "fused": False,
+    "graph": False,
 }
 COMMON_ALLOWED = {
     "backend": ["rccl", "ipc", *UCC_BACKENDS],
@@ -52,10 +55,11 @@ COMMON_ALLOWED = {
     "inter_stream_synchronization": [True, False],
     "signal": ["stream", "kernel"],
     "tile": ["auto", "pp256", "256x256", "256x128", "128x256", "128x128", "256x256w4",
-             "256x128w4", "p256", "p128", "i256", "i128", "i256w4"],
+             "256x128w4", "p256", "p128", "i256", "i128", "i256w4", "pi256"],
     "gemm_mode": ["auto", "mx", "generic"],
     "copy_blocks": (1, 4096),
     "fused": [True, False],
+    "graph": [True, False, "auto"],
 }
 COMMON_ALIASES = {
     "backend": {"nccl": "rccl", "cuda": "ipc"},
@@ -64,7 +68,7 @@ COMMON_ALIASES = {
 
 TILE_CODE = {"auto": 0, "256x256": 1, "256x128": 2, "128x256": 3, "128x128": 4, "pp256": 5,
              "256x256w4": 6, "256x128w4": 7, "p256": 8, "p128": 9, "i256": 10,
-             "i128": 11, "i256w4": 12}
+             "i128": 11, "i256w4": 12, "pi256": 13}
 MODE_CODE = {"auto": 0, "generic": 1, "mx": 2}
 
 
@@ -93,3 +97,14 @@ def dtype_codes(dtype_name: str):
     din = NAME_DT[dtype_name]
     dout = DT_BF16 if din == DT_FP8 else din
     return din, dout
+
+
+def maybe_enable_graph(bound, option) -> bool:
+    """Apply the ``graph`` option to a bound plan; returns whether graph replay is on."""
+    if option is True or option == "true":
+        bound.enable_graph(True)
+        return True
+    if option == "auto" and bound.ex.graph_capturable():
+        bound.enable_graph(True)
+        return True
+    return False

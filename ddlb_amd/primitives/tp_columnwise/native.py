@@ -14,7 +14,7 @@ from __future__ import annotations
 
 from ddlb_amd.parallel.algorithms import build_tp_columnwise
 from ddlb_amd.primitives.native_common import (COMMON_ALIASES, COMMON_ALLOWED, COMMON_DEFAULTS,
-                                               algo_config, dtype_codes)
+                                               algo_config, dtype_codes, maybe_enable_graph)
 from ddlb_amd.primitives.tp_columnwise.base import TPColumnwise
 
 
@@ -40,6 +40,7 @@ class NativeTPColumnwise(TPColumnwise):
                                                  self.k, din, dout, self.cfg)
         self.ctx = self.communicator.native()
         self.bound = self.ctx.bind(self.plan)
+        self.graph = maybe_enable_graph(self.bound, self.options["graph"])
         self.a_slot = self.bound.view(self.io.a)
         self.a_slot.copy_(self.A)
         self.bound.view(self.io.b).copy_(self.B.t())

@@ -10,7 +10,7 @@ from __future__ import annotations
 
 from ddlb_amd.parallel.algorithms import build_tp_rowwise
 from ddlb_amd.primitives.native_common import (COMMON_ALIASES, COMMON_ALLOWED, COMMON_DEFAULTS,
-                                               algo_config, dtype_codes)
+                                               algo_config, dtype_codes, maybe_enable_graph)
 from ddlb_amd.primitives.tp_rowwise.base import TPRowwise
 
 
@@ -34,6 +34,7 @@ class NativeTPRowwise(TPRowwise):
                                               din, dout, self.cfg)
         self.ctx = self.communicator.native()
         self.bound = self.ctx.bind(self.plan)
+        self.graph = maybe_enable_graph(self.bound, self.options["graph"])
         self.bound.view(self.io.a).copy_(self.A)
         self.bound.view(self.io.b).copy_(self.B.t())
         self.out = self.bound.view(self.io.out)

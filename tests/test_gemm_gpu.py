@@ -35,7 +35,7 @@ def gen():
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
-@pytest.mark.parametrize("tile", ["256x256", "256x128", "128x256", "128x128", "pp256", "256x256w4", "256x128w4", "p256", "p128", "i256", "i128"])
+@pytest.mark.parametrize("tile", ["256x256", "256x128", "128x256", "128x128", "pp256", "256x256w4", "256x128w4", "p256", "p128", "i256", "i128", "i256w4", "pi256"])
 def test_gemm_tiles(dtype, tile, gen):
     from ddlb_amd.ops.gemm import gemm
 
@@ -96,7 +96,7 @@ def test_gemm_fp8(mode, odt, gen):
     torch.testing.assert_close(out.float(), _ref(a, w), rtol=0, atol=_tol(torch.float8_e4m3fn, K))
 
 
-@pytest.mark.parametrize("tile", ["auto", "pp256", "128x128", "256x256w4", "256x128w4", "p256", "p128", "i256", "i128"])
+@pytest.mark.parametrize("tile", ["auto", "pp256", "128x128", "256x256w4", "256x128w4", "p256", "p128", "i256", "i128", "i256w4", "pi256"])
 def test_fp8_integer_exact(gen, tile):
     """Small integers are exact in e4m3: both fp8 paths must match bit for bit."""
     from ddlb_amd.ops.gemm import gemm
@@ -133,7 +133,7 @@ def test_grouped_rows(gen):
     assert torch.count_nonzero(C[untouched].float()) == 0
 
 
-@pytest.mark.parametrize("tile", ["auto", "pp256", "128x128", "256x256w4", "256x128w4", "p256", "p128", "i256", "i128"])
+@pytest.mark.parametrize("tile", ["auto", "pp256", "128x128", "256x256w4", "256x128w4", "p256", "p128", "i256", "i128", "i256w4", "pi256"])
 @pytest.mark.parametrize("shape", [(2048, 1024, 1024), (4096, 2048, 2048), (768, 512, 192)])
 def test_repeat_race_screen(gen, tile, shape):
     """Same inputs, 20 launches: identical bits every time (LDS-DMA/barrier race screen)."""
@@ -161,7 +161,7 @@ def test_host_checks_reject_bad_shapes(gen):
         gemm(a, _rand((64, 128), torch.bfloat16, gen), M=128)
 
 
-@pytest.mark.parametrize("tile", ["p256", "p128"])
+@pytest.mark.parametrize("tile", ["p256", "p128", "pi256"])
 def test_persistent_many_tiles_grouped(gen, tile):
     """Persistent streaming kernel: more tiles than blocks, grouped C rows, repeat-identical."""
     from ddlb_amd.ops.gemm import gemm
@@ -181,3 +181,17 @@ def test_persistent_many_tiles_grouped(gen, tile):
         gemm(a, w, out, tile=tile, c_grp=1024, c_gstride=2048)
     torch.cuda.synchronize()
     assert torch.equal(out, first)
+
+
+@pytest.mark.parametrize("act", ["gelu", "relu", "silu"])
+@pytest.mark.parametrize("tile", ["auto", "128x128", "pi256"])
+def test_fused_activation_epilogue(gen, act, tile):
+    from ddlb_amd.ops.gemm import gemm
+    from ddlb_amd.parallel.sim import apply_act
+
+    M, N, K = 512, 512, 256
+    a, w = _rand((M, K), torch.bfloat16, gen), _rand((N, K), torch.bfloat16, gen)
+    out = gemm(a, w, tile=tile, act=act)
+    torch.cuda.synchronize()
+    code = {"gelu": 1, "relu": 2, "silu": 3}[act]
+    torch.testing.assert_close(out.float(), apply_act(_ref(a, w), code), rtol=0.02, atol=0.05)

@@ -129,3 +129,39 @@ def test_ipc_shared_gpu(world):
     bad = {k: v for k, v in res.items() if v != "ok"}
     assert not bad, json.dumps(bad, indent=1)
     assert all(c == 0 for c in codes), (codes, outs[1][-2000:])
+
+
+@pytest.mark.parametrize("prim", ["col", "row"])
+def test_graph_replay_world1(comm, prim):
+    from ddlb_amd.primitives.tp_columnwise.native import NativeTPColumnwise
+    from ddlb_amd.primitives.tp_rowwise.native import NativeTPRowwise
+
+    cls = NativeTPColumnwise if prim == "col" else NativeTPRowwise
+    impl = cls(m=2048, n=512, k=512, dtype="bfloat16", algorithm="coll_pipeline", s=4,
+               graph=True)
+    assert impl.graph
+    for _ in range(5):
+        out = impl.run()
+    torch.cuda.synchronize()
+    impl.validate(out)
+    first = out.clone()
+    out.zero_()
+    impl.run()
+    torch.cuda.synchronize()
+    assert torch.equal(out, first)  # the replay really recomputes into the same buffer
+    impl.close()
+
+
+def test_graph_refused_for_signal_plans():
+    from ddlb_amd.parallel.algorithms import AlgoConfig, build_tp_columnwise
+    from ddlb_amd.parallel.plan import DT_BF16
+    from ddlb_amd.ops import load
+
+    C = load()
+    plan, _ = build_tp_columnwise(0, 2, 256, 64, 64, DT_BF16, DT_BF16,
+                                  AlgoConfig(algorithm="p2p_pipeline", backend="ipc"))
+    ex = C.PlanExecutor(0, plan.nstreams, max(plan.nevents, 1), list(plan.stream_priority))
+    ex.load(plan.encode(lambda ref: 4096))
+    assert not ex.graph_capturable()
+    with pytest.raises(RuntimeError):
+        ex.enable_graph(True)
