@@ -21,7 +21,9 @@ enum Tile : int { TILE_AUTO = 0, TILE_256x256 = 1, TILE_256x128 = 2, TILE_128x25
                   TILE_128x128 = 4, TILE_PP256 = 5, TILE_256x256_W4 = 6, TILE_256x128_W4 = 7,
                   TILE_P256 = 8, TILE_P128 = 9,     // P*: persistent streaming variants
                   TILE_I256 = 10, TILE_I128 = 11,    // I*: DMA interleaved into the MFMAs
-                  TILE_I256W4 = 12, TILE_PI256 = 13 };
+                  TILE_I256W4 = 12, TILE_PI256 = 13,
+                  TILE_PI256W4 = 14,
+                  TILE_R256 = 15 };   // R: persistent LDS-ring (3 K-steps in flight)
 enum GemmMode : int { GEMM_MODE_AUTO = 0, GEMM_MODE_GENERIC = 1, GEMM_MODE_MX = 2 };
 
 // C[M,N] = A[M,K] * Bt[N,K]^T. Leading dimensions in ELEMENTS.
@@ -46,7 +48,7 @@ enum Act : int { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_SILU = 3 };
 
 hipError_t gemm_launch(const GemmArgs& p, int din, int dout, int tile, int mode, hipStream_t s);
 bool gemm_fast_path_ok(const GemmArgs& p, int din, int dout);
-int choose_tile(int64_t M, int64_t N, int din);
+int choose_tile(int64_t M, int64_t N, int64_t K, int din);
 int tile_rows(int tile);
 int tile_cols(int tile);
 

@@ -31,969 +31,9 @@
 #include <stdint.h>
 
 #include "gemm.h"
+#include "gemm_entry.h"
 
 namespace ddlb {
-namespace {
-
-typedef __attribute__((ext_vector_type(4))) float f32x4;
-typedef __attribute__((ext_vector_type(4))) int i32x4;
-typedef __attribute__((ext_vector_type(8))) int i32x8;
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
-typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
-
-#define LDS_AS __attribute__((address_space(3)))
-#define GLB_AS __attribute__((address_space(1)))
-
-__device__ __forceinline__ void glds16(const void* g, void* lds) {
-  __builtin_amdgcn_global_load_lds((const GLB_AS void*)g, (LDS_AS void*)lds, 16, 0, 0);
-}
-
-// Rows and group sizes fit in 32 bits: 32-bit unsigned division is ~10x cheaper than 64-bit.
-__device__ __forceinline__ int64_t map_row(int64_t i, int64_t grp, int64_t gstride) {
-  const unsigned ui = (unsigned)i, ug = (unsigned)grp;
-  const unsigned q = ui / ug;
-  return (int64_t)q * gstride + (int64_t)(ui - q * ug);
-}
-
-// Bijective XCD remap (guide §5, "XCD swizzle must be bijective").
-__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
-  const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, idx = bid >> 3;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-}
-
-// Block -> tile. Default: bijective XCD remap over the whole grid. With ``tile_order`` the grid
-// is dispatched shard-major (shard (first_shard + j) % nshards at dispatch position j, so the
-// tiles of the shard that arrives first run first) and XCD-remapped within each shard.
-__device__ __forceinline__ int tile_index(const GemmArgs& p, int nwg) {
-  if (!p.tile_order) return xcd_remap((int)blockIdx.x, nwg);
-  const int per = nwg / p.nshards;
-  const int j = (int)blockIdx.x / per, local = (int)blockIdx.x % per;
-  const int shard = (p.first_shard + j) % p.nshards;
-  return shard * per + xcd_remap(local, per);
-}
-
-__device__ __forceinline__ int tile_index_virtual(const GemmArgs& p, int vid, int nwg) {
-  if (!p.tile_order) return xcd_remap(vid, nwg);
-  const int per = nwg / p.nshards;
-  const int j = vid / per, local = vid % per;
-  const int shard = (p.first_shard + j) % p.nshards;
-  return shard * per + xcd_remap(local, per);
-}
-
-// ---------------------------------------------------------------- MFMA "consume 16 bytes" ops
-struct MmaBF16 {
-  static constexpr int kElem = 2;
-  static __device__ __forceinline__ void step(f32x4& acc, const i32x4& b, const i32x4& a) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, b),
-                                                  __builtin_bit_cast(bf16x8, a), acc, 0, 0, 0);
-  }
-};
-struct MmaF16 {
-  static constexpr int kElem = 2;
-  static __device__ __forceinline__ void step(f32x4& acc, const i32x4& b, const i32x4& a) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, b),
-                                                 __builtin_bit_cast(f16x8, a), acc, 0, 0, 0);
-  }
-};
-struct MmaFP8 {  // OCP e4m3 x e4m3, f32 accumulate; 2 instructions per 16 B
-  static constexpr int kElem = 1;
-  static __device__ __forceinline__ void step(f32x4& acc, const i32x4& b, const i32x4& a) {
-    const long b0 = ((long)(unsigned)b.y << 32) | (unsigned)b.x;
-    const long b1 = ((long)(unsigned)b.w << 32) | (unsigned)b.z;
-    const long a0 = ((long)(unsigned)a.y << 32) | (unsigned)a.x;
-    const long a1 = ((long)(unsigned)a.w << 32) | (unsigned)a.z;
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(b0, a0, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(b1, a1, acc, 0, 0, 0);
-  }
-};
-struct MmaF32 {  // exact f32 MFMA; 4 instructions per 16 B
-  static constexpr int kElem = 4;
-  static __device__ __forceinline__ void step(f32x4& acc, const i32x4& b, const i32x4& a) {
-    const f32x4 bf = __builtin_bit_cast(f32x4, b), af = __builtin_bit_cast(f32x4, a);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(bf.x, af.x, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(bf.y, af.y, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(bf.z, af.z, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(bf.w, af.w, acc, 0, 0, 0);
-  }
-};
-
-// Compile-time emission of the {PER x MFMA, 1 x VMEM, n_g x DS_READ} interleave pattern
-// (sched_group_barrier arguments must be literal constants).
-template <int G, int NG, int PER, int NRD, int NDMA>
-struct IlvPattern {
-  static __device__ __forceinline__ void emit() {
-    if constexpr (G < NG) {
-      __builtin_amdgcn_sched_group_barrier(0x008, PER, 0);
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      constexpr int nrd = ((G + 1) * NRD) / NDMA - (G * NRD) / NDMA;
-      if constexpr (nrd > 0) __builtin_amdgcn_sched_group_barrier(0x100, nrd, 0);
-      IlvPattern<G + 1, NG, PER, NRD, NDMA>::emit();
-    }
-  }
-};
-
-// ---------------------------------------------------------------- fused epilogue activation
-__device__ __forceinline__ float act1(float x, int act) {
-  switch (act) {
-    case ACT_GELU: {  // tanh approximation (what Megatron / TE use for GPT-style MLPs)
-      const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
-      return 0.5f * x * (1.f + tanhf(u));
-    }
-    case ACT_RELU: return x > 0.f ? x : 0.f;
-    case ACT_SILU: return x / (1.f + __expf(-x));
-    default: return x;
-  }
-}
-__device__ __forceinline__ f32x4 act4(f32x4 v, int act) {
-  if (act == ACT_NONE) return v;
-  return f32x4{act1(v.x, act), act1(v.y, act), act1(v.z, act), act1(v.w, act)};
-}
-
-// ---------------------------------------------------------------- output conversion
-template <int OUT> struct Store4;
-template <> struct Store4<DT_BF16> {
-  static __device__ __forceinline__ void st(void* p, const f32x4 v) {
-    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-    bf16x4 o = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
-    *(uint2*)p = __builtin_bit_cast(uint2, o);
-  }
-  static __device__ __forceinline__ void st1(void* p, float v) { *(__bf16*)p = (__bf16)v; }
-};
-template <> struct Store4<DT_F16> {
-  static __device__ __forceinline__ void st(void* p, const f32x4 v) {
-    typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
-    f16x4 o = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
-    *(uint2*)p = __builtin_bit_cast(uint2, o);
-  }
-  static __device__ __forceinline__ void st1(void* p, float v) { *(_Float16*)p = (_Float16)v; }
-};
-template <> struct Store4<DT_F32> {
-  static __device__ __forceinline__ void st(void* p, const f32x4 v) { *(f32x4*)p = v; }
-  static __device__ __forceinline__ void st1(void* p, float v) { *(float*)p = v; }
-};
-
-template <int OUT> constexpr int out_size() { return OUT == DT_F32 ? 4 : 2; }
-
-// ---------------------------------------------------------------- bounded arrival spin
-__device__ __forceinline__ void wait_flag(const GemmArgs& p, int64_t row) {
-  if (p.flags == nullptr) return;
-  const int shard = (int)(row / p.flag_rows);
-  unsigned* f = const_cast<unsigned*>(p.flags) + shard;
-  if (threadIdx.x == 0) {
-    unsigned spins = 0;
-    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) <
-           p.epoch) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1u << 26)) {  // ~seconds: give up, report, let the grid drain
-        if (p.timeout_word) atomicOr(p.timeout_word, 1u);
-        break;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  }
-  __syncthreads();
-}
-
-// ---------------------------------------------------------------- the tiled kernel
-template <class Mma, int OUT, int BM, int BN, int WM, int WN, bool ILV = false>
-__global__ __launch_bounds__(WM* WN * 64) void gemm_tn_kernel(const GemmArgs p) {
-  constexpr int NT = WM * WN * 64, NW = WM * WN;
-  constexpr int ROWB = 128;  // bytes per row per K-tile
-  constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, STAGE = A_BYTES + B_BYTES;
-  constexpr int TM = BM / WM, TN = BN / WN, MR = TM / 16, NR = TN / 16;
-  constexpr int LA = BM / 8 / NW, LB = BN / 8 / NW;  // LDS-DMA instructions per wave per tile
-  static_assert(LA * NW * 8 == BM && LB * NW * 8 == BN, "tile rows must split over waves");
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
-  const int nwg = tiles_m * tiles_n;
-  const int wg = tile_index(p, nwg);
-  const int tm = wg / tiles_n, tn = wg % tiles_n;
-  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
-
-  // Per-lane source pointers for the LDS-DMA rows this wave stages.
-  const int esz = Mma::kElem;
-  const char* aptr[LA];
-  const char* bptr[LB];
-#pragma unroll
-  for (int i = 0; i < LA; ++i) {
-    const int row = (wave * LA + i) * 8 + (lane >> 3);
-    int64_t gr = m0 + row;
-    gr = gr < p.M ? gr : p.M - 1;
-    const int64_t phys = map_row(gr, p.a_grp, p.a_gstride);
-    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
-    aptr[i] = (const char*)p.a + phys * p.lda * esz + chunk * 16;
-  }
-#pragma unroll
-  for (int i = 0; i < LB; ++i) {
-    const int row = (wave * LB + i) * 8 + (lane >> 3);
-    int64_t gr = n0 + row;
-    gr = gr < p.N ? gr : p.N - 1;
-    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
-    bptr[i] = (const char*)p.b + gr * p.ldb * esz + chunk * 16;
-  }
-
-  wait_flag(p, map_row(m0, p.a_grp, p.a_gstride));
-
-  auto stage = [&](int buf, int kt) {
-    char* base = smem + buf * STAGE;
-    const int64_t koff = (int64_t)kt * ROWB;
-#pragma unroll
-    for (int i = 0; i < LA; ++i) glds16(aptr[i] + koff, base + (wave * LA + i) * 1024);
-#pragma unroll
-    for (int i = 0; i < LB; ++i) glds16(bptr[i] + koff, base + A_BYTES + (wave * LB + i) * 1024);
-  };
-
-  const int wm = wave / WN, wn = wave % WN;
-  const int swz = (lane & 15) >> 1;
-  const int frow = lane & 15, fq = lane >> 4;
-  f32x4 acc[MR][NR];
-#pragma unroll
-  for (int i = 0; i < MR; ++i)
-#pragma unroll
-    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto compute = [&](int buf) {
-    const char* As = smem + buf * STAGE;
-    const char* Bs = As + A_BYTES;
-#pragma unroll
-    for (int c4 = 0; c4 < 8; c4 += 4) {
-      const int choff = ((c4 + fq) ^ swz) * 16;
-      i32x4 af[MR], bfr[NR];
-#pragma unroll
-      for (int i = 0; i < MR; ++i)
-        af[i] = *(const i32x4*)(As + (wm * TM + i * 16 + frow) * ROWB + choff);
-#pragma unroll
-      for (int j = 0; j < NR; ++j)
-        bfr[j] = *(const i32x4*)(Bs + (wn * TN + j * 16 + frow) * ROWB + choff);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < MR; ++i)
-#pragma unroll
-        for (int j = 0; j < NR; ++j) Mma::step(acc[i][j], bfr[j], af[i]);
-      __builtin_amdgcn_s_setprio(0);
-    }
-  };
-
-  // Interleaved variant: the next tile's LDS-DMA is issued INSIDE the first MFMA cluster (one
-  // DMA per MR*NR/(LA+LB) MFMAs), so its issue cost hides behind the matrix pipe instead of
-  // forming a burst at the top of every K-tile (cdna guide: "the per-phase interleave is the
-  // lever"). The DMA writes the other LDS buffer, so it may be placed after this tile's reads.
-  auto compute_ilv = [&](int buf, int next_kt) {
-    // First half: MFMAs on the c4=0 fragments, with the next tile's LDS-DMA (1 per PER MFMAs)
-    // and the c4=4 fragment reads (into a second register set) interleaved between them.
-    constexpr int NDMA = LA + LB, NRD = MR + NR, NQ = MR * NR;
-    constexpr int PER = NQ / NDMA > 0 ? NQ / NDMA : 1;
-    const char* As = smem + buf * STAGE;
-    const char* Bs = As + A_BYTES;
-    char* nbase = smem + (buf ^ 1) * STAGE;
-    const int64_t koff = (int64_t)next_kt * ROWB;
-    const int ch0 = ((0 + fq) ^ swz) * 16, ch1 = ((4 + fq) ^ swz) * 16;
-    i32x4 af0[MR], bf0[NR], af1[MR], bf1[NR];
-#pragma unroll
-    for (int i = 0; i < MR; ++i)
-      af0[i] = *(const i32x4*)(As + (wm * TM + i * 16 + frow) * ROWB + ch0);
-#pragma unroll
-    for (int j = 0; j < NR; ++j)
-      bf0[j] = *(const i32x4*)(Bs + (wn * TN + j * 16 + frow) * ROWB + ch0);
-    auto rd1 = [&](int r) {
-      if (r < MR) af1[r] = *(const i32x4*)(As + (wm * TM + r * 16 + frow) * ROWB + ch1);
-      else bf1[r - MR] = *(const i32x4*)(Bs + (wn * TN + (r - MR) * 16 + frow) * ROWB + ch1);
-    };
-    auto dma = [&](int d) {
-      if (d < LA) glds16(aptr[d] + koff, nbase + (wave * LA + d) * 1024);
-      else glds16(bptr[d - LA] + koff, nbase + A_BYTES + (wave * LB + d - LA) * 1024);
-    };
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      Mma::step(acc[q / NR][q % NR], bf0[q % NR], af0[q / NR]);
-      if ((q % PER) == PER - 1) {
-        const int g = q / PER;
-        if (g < NDMA) dma(g);
-        // spread the NRD second-half reads over the NDMA groups
-#pragma unroll
-        for (int r = (g * NRD) / NDMA; r < ((g + 1) * NRD) / NDMA; ++r) rd1(r);
-      }
-    }
-#pragma unroll
-    for (int d = NQ / PER; d < NDMA; ++d) dma(d);
-#pragma unroll
-    for (int r = ((NQ / PER) * NRD) / NDMA; r < NRD; ++r) rd1(r);
-    IlvPattern<0, (NDMA < NQ / PER ? NDMA : NQ / PER), PER, NRD, NDMA>::emit();
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) Mma::step(acc[q / NR][q % NR], bf1[q % NR], af1[q / NR]);
-    __builtin_amdgcn_s_setprio(0);
-  };
-
-  const int nk = p.K * esz / ROWB;
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  int cur = 0;
-  for (int kt = 0; kt < nk - 1; ++kt) {
-    if constexpr (ILV) {
-      compute_ilv(cur, kt + 1);
-    } else {
-      stage(cur ^ 1, kt + 1);
-      compute(cur);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    cur ^= 1;
-  }
-  compute(cur);
-
-  // Epilogue: lane holds C[row = .. + frow][col = .. + 4*fq + r], r = 0..3.
-  constexpr int OSZ = out_size<OUT>();
-#pragma unroll
-  for (int i = 0; i < MR; ++i) {
-    const int64_t row = m0 + wm * TM + i * 16 + frow;
-    if (row >= p.M) continue;
-    char* crow = (char*)p.c + map_row(row, p.c_grp, p.c_gstride) * p.ldc * OSZ;
-#pragma unroll
-    for (int j = 0; j < NR; ++j) {
-      const int64_t col = n0 + wn * TN + j * 16 + fq * 4;
-      if (col + 3 < p.N) {
-        Store4<OUT>::st(crow + col * OSZ, act4(acc[i][j], p.act));
-      } else {
-        const f32x4 a4 = act4(acc[i][j], p.act);
-        const float v[4] = {a4.x, a4.y, a4.z, a4.w};
-        for (int r = 0; r < 4; ++r)
-          if (col + r < p.N) Store4<OUT>::st1(crow + (col + r) * OSZ, v[r]);
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------- persistent streaming kernel
-// Same tile / staging / MFMA body as gemm_tn_kernel, but a fixed grid (one block per CU) walks
-// the tiles, and the (tile, k-step) pairs form ONE continuous stream: the last k-step of tile i
-// already stages k-step 0 of tile i+1, the epilogue of tile i issues its C stores, and the wait
-// before the next compute is a COUNTED vmcnt(NSTORE) — LDS-DMA and stores share the in-order
-// vmcnt queue, so waiting for "at most NSTORE outstanding" retires the (older) DMA while the C
-// stores keep draining under tile i+1's MFMAs. Exactly NSTORE stores must be issued per tile, so
-// this kernel is used only for full tiles (M % BM == 0, N % BN == 0): no store is predicated.
-template <class Mma, int OUT, int BM, int BN, int WM, int WN, bool ILV = false>
-__global__ __launch_bounds__(WM* WN * 64) void gemm_tn_persist_kernel(const GemmArgs p) {
-  constexpr int NW = WM * WN, ROWB = 128;
-  constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, STAGE = A_BYTES + B_BYTES;
-  constexpr int TM = BM / WM, TN = BN / WN, MR = TM / 16, NR = TN / 16;
-  constexpr int LA = BM / 8 / NW, LB = BN / 8 / NW;
-  constexpr int NSTORE = MR * NR;
-  static_assert(NSTORE <= 63, "vmcnt is a 6-bit counter");
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int tiles_n = p.N / BN, tiles_m = p.M / BM, ntiles = tiles_m * tiles_n;
-  const int esz = Mma::kElem;
-  const int nk = p.K * esz / ROWB;
-  const int my_tiles = ((int)blockIdx.x < ntiles) ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
-  const int total = my_tiles * nk;
-  if (total == 0) return;
-
-  const char* aptr[LA];
-  const char* bptr[LB];
-  int cur_tile = -1;
-  auto set_tile = [&](int i) {  // i-th tile of this block -> source pointers
-    const int wg = tile_index_virtual(p, (int)blockIdx.x + i * (int)gridDim.x, ntiles);
-    const int64_t m0 = (int64_t)(wg / tiles_n) * BM, n0 = (int64_t)(wg % tiles_n) * BN;
-#pragma unroll
-    for (int r = 0; r < LA; ++r) {
-      const int row = (wave * LA + r) * 8 + (lane >> 3);
-      const int chunk = (lane & 7) ^ ((row >> 1) & 7);
-      aptr[r] = (const char*)p.a + map_row(m0 + row, p.a_grp, p.a_gstride) * p.lda * esz +
-                chunk * 16;
-    }
-#pragma unroll
-    for (int r = 0; r < LB; ++r) {
-      const int row = (wave * LB + r) * 8 + (lane >> 3);
-      const int chunk = (lane & 7) ^ ((row >> 1) & 7);
-      bptr[r] = (const char*)p.b + (n0 + row) * p.ldb * esz + chunk * 16;
-    }
-  };
-  auto stage = [&](int buf, int g) {
-    const int ti = g / nk, kt = g - ti * nk;
-    if (ti != cur_tile) {
-      set_tile(ti);
-      cur_tile = ti;
-    }
-    char* base = smem + buf * STAGE;
-    const int64_t koff = (int64_t)kt * ROWB;
-#pragma unroll
-    for (int i = 0; i < LA; ++i) glds16(aptr[i] + koff, base + (wave * LA + i) * 1024);
-#pragma unroll
-    for (int i = 0; i < LB; ++i) glds16(bptr[i] + koff, base + A_BYTES + (wave * LB + i) * 1024);
-  };
-
-  const int wm = wave / WN, wn = wave % WN;
-  const int swz = (lane & 15) >> 1, frow = lane & 15, fq = lane >> 4;
-  f32x4 acc[MR][NR];
-#pragma unroll
-  for (int i = 0; i < MR; ++i)
-#pragma unroll
-    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto compute = [&](int buf) {
-    const char* As = smem + buf * STAGE;
-    const char* Bs = As + A_BYTES;
-#pragma unroll
-    for (int c4 = 0; c4 < 8; c4 += 4) {
-      const int choff = ((c4 + fq) ^ swz) * 16;
-      i32x4 af[MR], bfr[NR];
-#pragma unroll
-      for (int i = 0; i < MR; ++i)
-        af[i] = *(const i32x4*)(As + (wm * TM + i * 16 + frow) * ROWB + choff);
-#pragma unroll
-      for (int j = 0; j < NR; ++j)
-        bfr[j] = *(const i32x4*)(Bs + (wn * TN + j * 16 + frow) * ROWB + choff);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < MR; ++i)
-#pragma unroll
-        for (int j = 0; j < NR; ++j) Mma::step(acc[i][j], bfr[j], af[i]);
-      __builtin_amdgcn_s_setprio(0);
-    }
-  };
-  constexpr int OSZ = out_size<OUT>();
-  auto epilogue = [&](int ti) {
-    const int wg = tile_index_virtual(p, (int)blockIdx.x + ti * (int)gridDim.x, ntiles);
-    const int64_t m0 = (int64_t)(wg / tiles_n) * BM, n0 = (int64_t)(wg % tiles_n) * BN;
-#pragma unroll
-    for (int i = 0; i < MR; ++i) {
-      const int64_t row = m0 + wm * TM + i * 16 + frow;
-      char* crow = (char*)p.c + map_row(row, p.c_grp, p.c_gstride) * p.ldc * OSZ;
-#pragma unroll
-      for (int j = 0; j < NR; ++j) {
-        const int64_t col = n0 + wn * TN + j * 16 + fq * 4;
-        Store4<OUT>::st(crow + col * OSZ, act4(acc[i][j], p.act));
-        acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
-  };
-
-  // interleaved compute (see gemm_tn_kernel::compute_ilv): next step's DMA + second-half
-  // fragment reads issued between the first-half MFMAs
-  auto compute_ilv = [&](int buf, int64_t koff) {
-    constexpr int NDMA = LA + LB, NRD = MR + NR, NQ = MR * NR;
-    constexpr int PER = NQ / NDMA > 0 ? NQ / NDMA : 1;
-    const char* As = smem + buf * STAGE;
-    const char* Bs = As + A_BYTES;
-    char* nbase = smem + (buf ^ 1) * STAGE;
-    const int ch0 = ((0 + fq) ^ swz) * 16, ch1 = ((4 + fq) ^ swz) * 16;
-    i32x4 af0[MR], bf0[NR], af1[MR], bf1[NR];
-#pragma unroll
-    for (int i = 0; i < MR; ++i)
-      af0[i] = *(const i32x4*)(As + (wm * TM + i * 16 + frow) * ROWB + ch0);
-#pragma unroll
-    for (int j = 0; j < NR; ++j)
-      bf0[j] = *(const i32x4*)(Bs + (wn * TN + j * 16 + frow) * ROWB + ch0);
-    auto rd1 = [&](int r) {
-      if (r < MR) af1[r] = *(const i32x4*)(As + (wm * TM + r * 16 + frow) * ROWB + ch1);
-      else bf1[r - MR] = *(const i32x4*)(Bs + (wn * TN + (r - MR) * 16 + frow) * ROWB + ch1);
-    };
-    auto dma = [&](int d) {
-      if (d < LA) glds16(aptr[d] + koff, nbase + (wave * LA + d) * 1024);
-      else glds16(bptr[d - LA] + koff, nbase + A_BYTES + (wave * LB + d - LA) * 1024);
-    };
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      Mma::step(acc[q / NR][q % NR], bf0[q % NR], af0[q / NR]);
-      if ((q % PER) == PER - 1) {
-        const int gg = q / PER;
-        if (gg < NDMA) dma(gg);
-#pragma unroll
-        for (int r = (gg * NRD) / NDMA; r < ((gg + 1) * NRD) / NDMA; ++r) rd1(r);
-      }
-    }
-#pragma unroll
-    for (int d = NQ / PER; d < NDMA; ++d) dma(d);
-#pragma unroll
-    for (int r = ((NQ / PER) * NRD) / NDMA; r < NRD; ++r) rd1(r);
-    IlvPattern<0, (NDMA < NQ / PER ? NDMA : NQ / PER), PER, NRD, NDMA>::emit();
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) Mma::step(acc[q / NR][q % NR], bf1[q % NR], af1[q / NR]);
-    __builtin_amdgcn_s_setprio(0);
-  };
-
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  int cur = 0;
-  for (int g = 0; g < total; ++g) {
-    const bool more = g + 1 < total;
-    if constexpr (ILV) {
-      // last step of the stream: re-stage the current k-step into the idle buffer (never read)
-      const int gn = more ? g + 1 : g;
-      const int ti = gn / nk;
-      if (ti != cur_tile) {
-        set_tile(ti);
-        cur_tile = ti;
-      }
-      compute_ilv(cur, (int64_t)(gn - ti * nk) * ROWB);
-    } else {
-      if (more) stage(cur ^ 1, g + 1);
-      compute(cur);
-    }
-    const bool last_k = (g % nk) == nk - 1;
-    if (last_k) {
-      __builtin_amdgcn_sched_barrier(0);
-      epilogue(g / nk);
-      __builtin_amdgcn_sched_barrier(0);
-      if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSTORE) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    cur ^= 1;
-  }
-  // never leave an LDS-DMA in flight past the end of the workgroup (its LDS is reassigned)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// ---------------------------------------------------------------- 256x256 ping-pong kernel
-// 8 waves = 2 groups (wr = 0: waves 0-3, wr = 1: waves 4-7; every SIMD hosts one wave of each)
-// x 4 column waves. Each wave owns a 128x64 output tile = 2x2 quadrants of 64x32 and runs, per
-// 64-deep K-tile, 4 phases of {LOAD section: ds_read the quadrant's fragments (+ LDS-DMA of the
-// next K-tile) | barrier | COMP section: 16 MFMAs | barrier}. Group 1 starts one barrier later,
-// so in every interval between two barriers one group computes while the other loads
-// (cdna guide §5 "256^2 8-phase template", T3/T4/T5).
-//
-// Sections of group 0 are numbered s = 8t + {0 L1, 1 C1, 2 L2, 3 C2, 4 L3, 5 C3, 6 L4, 7 C4} and
-// run between barriers B[s+1] and B[s+2]; group 1's section s runs between B[s+2] and B[s+3].
-//  * tile t+1 -> buffer (t+1)&1: group 1 issues its DMA in L1, L2 of tile t, group 0 in L2, L3.
-//    WAR: the last reads of tile t-1 (both groups' L4) retire in their C4, i.e. by B[8t+2],
-//    and group 1's L1 of tile t starts at B[8t+2].
-//  * RAW: group 0 waits vmcnt(0) at the end of C4 (before B[8t+9]), group 1 at the end of its
-//    L4 (before B[8t+9]); the first read of tile t+1 (group 0's L1) starts after B[8t+9].
-//  * Barrier balance: group 1 executes one extra barrier before the loop, group 0 one after it.
-template <class Mma, int OUT>
-__global__ __launch_bounds__(512) void gemm_tn_pp256_kernel(const GemmArgs p) {
-  constexpr int BM = 256, BN = 256, ROWB = 128;
-  constexpr int A_BYTES = BM * ROWB, STAGE = A_BYTES + BN * ROWB;
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 2, wc = wave & 3;
-  const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
-  const int wg = tile_index(p, tiles_m * tiles_n);
-  const int tm = wg / tiles_n, tn = wg % tiles_n;
-  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
-  const int esz = Mma::kElem;
-
-  // LDS-DMA sources: this wave stages rows [32*wave, 32*wave+32) of A and of B (4 x 8 rows each)
-  const char* aptr[4];
-  const char* bptr[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = (wave * 4 + i) * 8 + (lane >> 3);
-    int64_t gr = m0 + row;
-    gr = gr < p.M ? gr : p.M - 1;
-    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
-    aptr[i] = (const char*)p.a + map_row(gr, p.a_grp, p.a_gstride) * p.lda * esz + chunk * 16;
-    int64_t gc = n0 + row;
-    gc = gc < p.N ? gc : p.N - 1;
-    bptr[i] = (const char*)p.b + gc * p.ldb * esz + chunk * 16;
-  }
-  wait_flag(p, map_row(m0, p.a_grp, p.a_gstride));
-
-  // part 0: A rows 0-15 + B rows 0-15 of this wave's 32; part 1: the other 16 of each
-  auto stage_part = [&](int buf, int kt, int part) {
-    char* base = smem + buf * STAGE;
-    const int64_t koff = (int64_t)kt * ROWB;
-#pragma unroll
-    for (int i = 2 * part; i < 2 * part + 2; ++i) {
-      glds16(aptr[i] + koff, base + (wave * 4 + i) * 1024);
-      glds16(bptr[i] + koff, base + A_BYTES + (wave * 4 + i) * 1024);
-    }
-  };
-
-  const int swz = (lane & 15) >> 1, frow = lane & 15, fq = lane >> 4;
-  const int c0 = ((0 + fq) ^ swz) * 16, c1 = ((4 + fq) ^ swz) * 16;
-  const int arow0 = (wr * 128 + frow) * ROWB, brow0 = (wc * 64 + frow) * ROWB;
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  i32x4 aR[4][2], bR[2][2];
-
-  auto loadA = [&](const char* As, int mq) {
-#pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      const char* r = As + arow0 + (mq * 64 + f * 16) * ROWB;
-      aR[f][0] = *(const i32x4*)(r + c0);
-      aR[f][1] = *(const i32x4*)(r + c1);
-    }
-  };
-  auto loadB = [&](const char* Bs, int nq) {
-#pragma unroll
-    for (int f = 0; f < 2; ++f) {
-      const char* r = Bs + brow0 + (nq * 32 + f * 16) * ROWB;
-      bR[f][0] = *(const i32x4*)(r + c0);
-      bR[f][1] = *(const i32x4*)(r + c1);
-    }
-  };
-  auto comp = [&](int mq, int nq) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int f = 0; f < 4; ++f)
-#pragma unroll
-        for (int g = 0; g < 2; ++g) Mma::step(acc[mq * 4 + f][nq * 2 + g], bR[g][kk], aR[f][kk]);
-    __builtin_amdgcn_s_setprio(0);
-  };
-#define PP_BAR()                            \
-  do {                                      \
-    __builtin_amdgcn_sched_barrier(0);      \
-    __builtin_amdgcn_s_barrier();           \
-    __builtin_amdgcn_sched_barrier(0);      \
-  } while (0)
-#define PP_VM0() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
-
-  const int nk = p.K * esz / ROWB;
-  stage_part(0, 0, 0);
-  stage_part(0, 0, 1);
-  PP_VM0();
-  PP_BAR();
-  const bool g1 = wr == 1;  // wave-uniform (wave came through readfirstlane)
-  if (g1) PP_BAR();
-  for (int t = 0; t < nk; ++t) {
-    const char* As = smem + (t & 1) * STAGE;
-    const char* Bs = As + A_BYTES;
-    const int nb = (t + 1) & 1;
-    const bool nxt = t + 1 < nk;
-    // L1
-    loadA(As, 0);
-    loadB(Bs, 0);
-    if (g1 && nxt) stage_part(nb, t + 1, 0);
-    PP_BAR();
-    comp(0, 0);
-    PP_BAR();
-    // L2
-    loadB(Bs, 1);
-    if (nxt) stage_part(nb, t + 1, g1 ? 1 : 0);
-    PP_BAR();
-    comp(0, 1);
-    PP_BAR();
-    // L3
-    loadA(As, 1);
-    if (!g1 && nxt) stage_part(nb, t + 1, 1);
-    PP_BAR();
-    comp(1, 1);
-    PP_BAR();
-    // L4
-    loadB(Bs, 0);
-    if (g1) PP_VM0();
-    PP_BAR();
-    comp(1, 0);
-    if (!g1) PP_VM0();
-    PP_BAR();
-  }
-  if (!g1) PP_BAR();
-#undef PP_BAR
-#undef PP_VM0
-
-  constexpr int OSZ = out_size<OUT>();
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int64_t row = m0 + wr * 128 + (i >> 2) * 64 + (i & 3) * 16 + frow;
-    if (row >= p.M) continue;
-    char* crow = (char*)p.c + map_row(row, p.c_grp, p.c_gstride) * p.ldc * OSZ;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t col = n0 + wc * 64 + (j >> 1) * 32 + (j & 1) * 16 + fq * 4;
-      if (col + 3 < p.N) {
-        Store4<OUT>::st(crow + col * OSZ, act4(acc[i][j], p.act));
-      } else {
-        const f32x4 a4 = act4(acc[i][j], p.act);
-        const float v[4] = {a4.x, a4.y, a4.z, a4.w};
-        for (int r = 0; r < 4; ++r)
-          if (col + r < p.N) Store4<OUT>::st1(crow + (col + r) * OSZ, v[r]);
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------- MX-fp8 (block-scaled) kernel
-// One v_mfma_scale_f32_16x16x128_f8f6f4 per 128-byte K-row (unit E8M0 scales = 127): 2x the bf16
-// MFMA rate (MI355X_MICROARCH.md "Matrix cores"). Same staging as above.
-template <int OUT, int BM, int BN, int WM, int WN>
-__global__ __launch_bounds__(WM* WN * 64) void gemm_tn_mxfp8_kernel(const GemmArgs p) {
-  constexpr int NW = WM * WN, ROWB = 128;
-  constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, STAGE = A_BYTES + B_BYTES;
-  constexpr int TM = BM / WM, TN = BN / WN, MR = TM / 16, NR = TN / 16;
-  constexpr int LA = BM / 8 / NW, LB = BN / 8 / NW;
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
-  const int nwg = tiles_m * tiles_n;
-  const int wg = tile_index(p, nwg);
-  const int tm = wg / tiles_n, tn = wg % tiles_n;
-  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
-  const char* aptr[LA];
-  const char* bptr[LB];
-#pragma unroll
-  for (int i = 0; i < LA; ++i) {
-    const int row = (wave * LA + i) * 8 + (lane >> 3);
-    int64_t gr = m0 + row;
-    gr = gr < p.M ? gr : p.M - 1;
-    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
-    aptr[i] = (const char*)p.a + map_row(gr, p.a_grp, p.a_gstride) * p.lda + chunk * 16;
-  }
-#pragma unroll
-  for (int i = 0; i < LB; ++i) {
-    const int row = (wave * LB + i) * 8 + (lane >> 3);
-    int64_t gr = n0 + row;
-    gr = gr < p.N ? gr : p.N - 1;
-    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
-    bptr[i] = (const char*)p.b + gr * p.ldb + chunk * 16;
-  }
-  wait_flag(p, map_row(m0, p.a_grp, p.a_gstride));
-  auto stage = [&](int buf, int kt) {
-    char* base = smem + buf * STAGE;
-    const int64_t koff = (int64_t)kt * ROWB;
-#pragma unroll
-    for (int i = 0; i < LA; ++i) glds16(aptr[i] + koff, base + (wave * LA + i) * 1024);
-#pragma unroll
-    for (int i = 0; i < LB; ++i) glds16(bptr[i] + koff, base + A_BYTES + (wave * LB + i) * 1024);
-  };
-  const int wm = wave / WN, wn = wave % WN;
-  const int swz = (lane & 15) >> 1, frow = lane & 15, fq = lane >> 4;
-  f32x4 acc[MR][NR];
-#pragma unroll
-  for (int i = 0; i < MR; ++i)
-#pragma unroll
-    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto compute = [&](int buf) {
-    const char* As = smem + buf * STAGE;
-    const char* Bs = As + A_BYTES;
-    const int c0 = ((fq) ^ swz) * 16, c1 = ((4 + fq) ^ swz) * 16;
-    i32x8 af[MR], bfr[NR];
-#pragma unroll
-    for (int i = 0; i < MR; ++i) {
-      const char* r = As + (wm * TM + i * 16 + frow) * ROWB;
-      const i32x4 lo = *(const i32x4*)(r + c0), hi = *(const i32x4*)(r + c1);
-      af[i] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-    }
-#pragma unroll
-    for (int j = 0; j < NR; ++j) {
-      const char* r = Bs + (wn * TN + j * 16 + frow) * ROWB;
-      const i32x4 lo = *(const i32x4*)(r + c0), hi = *(const i32x4*)(r + c1);
-      bfr[j] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-    }
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < MR; ++i)
-#pragma unroll
-      for (int j = 0; j < NR; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfr[j], af[i], acc[i][j], 0,
-                                                                       0, 0, 127, 0, 127);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  const int nk = p.K / ROWB;
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  int cur = 0;
-  for (int kt = 0; kt < nk - 1; ++kt) {
-    stage(cur ^ 1, kt + 1);
-    compute(cur);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    cur ^= 1;
-  }
-  compute(cur);
-  constexpr int OSZ = out_size<OUT>();
-#pragma unroll
-  for (int i = 0; i < MR; ++i) {
-    const int64_t row = m0 + wm * TM + i * 16 + frow;
-    if (row >= p.M) continue;
-    char* crow = (char*)p.c + map_row(row, p.c_grp, p.c_gstride) * p.ldc * OSZ;
-#pragma unroll
-    for (int j = 0; j < NR; ++j) {
-      const int64_t col = n0 + wn * TN + j * 16 + fq * 4;
-      if (col + 3 < p.N) {
-        Store4<OUT>::st(crow + col * OSZ, act4(acc[i][j], p.act));
-      } else {
-        const f32x4 a4 = act4(acc[i][j], p.act);
-        const float v[4] = {a4.x, a4.y, a4.z, a4.w};
-        for (int r = 0; r < 4; ++r)
-          if (col + r < p.N) Store4<OUT>::st1(crow + (col + r) * OSZ, v[r]);
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------- generic fallback kernel
-// Any shape / alignment / dtype (incl. f64): 64x64 tile, 4x4 per thread, f32 (f64) FMA.
-template <typename T> __device__ __forceinline__ double ld_as_double(const void* p, int64_t i);
-template <int DT> __device__ __forceinline__ double load_elem(const char* base, int64_t idx) {
-  if constexpr (DT == DT_BF16) return (double)(float)((const __bf16*)base)[idx];
-  else if constexpr (DT == DT_F16) return (double)(float)((const _Float16*)base)[idx];
-  else if constexpr (DT == DT_F32) return (double)((const float*)base)[idx];
-  else if constexpr (DT == DT_F64) return ((const double*)base)[idx];
-  else {  // OCP e4m3fn
-    const uint8_t v = ((const uint8_t*)base)[idx];
-    const int s = v >> 7, e = (v >> 3) & 0xF, m = v & 7;
-    double r;
-    if (e == 0xF && m == 7) r = __builtin_nan("");
-    else if (e == 0) r = ldexp((double)m / 8.0, -6);
-    else r = ldexp(1.0 + (double)m / 8.0, e - 7);
-    return s ? -r : r;
-  }
-}
-template <int DT> __device__ __forceinline__ void store_elem(char* base, int64_t idx, double v) {
-  if constexpr (DT == DT_BF16) ((__bf16*)base)[idx] = (__bf16)(float)v;
-  else if constexpr (DT == DT_F16) ((_Float16*)base)[idx] = (_Float16)(float)v;
-  else if constexpr (DT == DT_F32) ((float*)base)[idx] = (float)v;
-  else ((double*)base)[idx] = v;
-}
-
-template <int DIN, int DOUT, typename Acc>
-__global__ __launch_bounds__(256) void gemm_generic_kernel(const GemmArgs p) {
-  const int tn = blockIdx.x, tm = blockIdx.y;
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  Acc acc[4][4] = {};
-  const char* A = (const char*)p.a;
-  const char* B = (const char*)p.b;
-  for (int k = 0; k < p.K; ++k) {
-    Acc av[4], bv[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t r = (int64_t)tm * 64 + ty * 4 + i;
-      av[i] = r < p.M ? (Acc)load_elem<DIN>(A, map_row(r, p.a_grp, p.a_gstride) * p.lda + k) : 0;
-      const int64_t c = (int64_t)tn * 64 + tx * 4 + i;
-      bv[i] = c < p.N ? (Acc)load_elem<DIN>(B, c * p.ldb + k) : 0;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] += av[i] * bv[j];
-  }
-  char* C = (char*)p.c;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int64_t r = (int64_t)tm * 64 + ty * 4 + i;
-    if (r >= p.M) continue;
-    const int64_t rp = map_row(r, p.c_grp, p.c_gstride) * p.ldc;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t c = (int64_t)tn * 64 + tx * 4 + j;
-      if (c < p.N) store_elem<DOUT>(C, rp + c, (double)act1((float)acc[i][j], p.act));
-    }
-  }
-}
-
-// ---------------------------------------------------------------- dispatch
-template <class Mma, int OUT, int BM, int BN, int WM, int WN, bool ILV = false>
-hipError_t launch_tiled(const GemmArgs& p, hipStream_t s) {
-  const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_tn_kernel<Mma, OUT, BM, BN, WM, WN, ILV>), dim3(tiles),
-                     dim3(WM * WN * 64), 0, s, p);
-  return hipGetLastError();
-}
-template <int OUT, int BM, int BN, int WM, int WN>
-hipError_t launch_mx(const GemmArgs& p, hipStream_t s) {
-  const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_tn_mxfp8_kernel<OUT, BM, BN, WM, WN>), dim3(tiles),
-                     dim3(WM * WN * 64), 0, s, p);
-  return hipGetLastError();
-}
-
-int num_cus() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-  }
-  return n;
-}
-
-template <class Mma, int OUT, int BM, int BN, int WM, int WN, bool ILV = false>
-hipError_t launch_persist(const GemmArgs& p, int blocks_per_cu, hipStream_t s) {
-  const int tiles = (p.M / BM) * (p.N / BN);
-  int grid = num_cus() * blocks_per_cu;
-  grid = (grid / 8) * 8;  // keep blockIdx % 8 == XCD group for every virtual tile id
-  if (grid > tiles) grid = tiles;
-  if (grid < 1) grid = 1;
-  hipLaunchKernelGGL((gemm_tn_persist_kernel<Mma, OUT, BM, BN, WM, WN, ILV>), dim3(grid),
-                     dim3(WM * WN * 64), 0, s, p);
-  return hipGetLastError();
-}
-
-template <class Mma, int OUT>
-hipError_t launch_pp256(const GemmArgs& p, hipStream_t s) {
-  const int tiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
-  hipLaunchKernelGGL((gemm_tn_pp256_kernel<Mma, OUT>), dim3(tiles), dim3(512), 0, s, p);
-  return hipGetLastError();
-}
-
-template <class Mma, int OUT>
-hipError_t launch_cfg(const GemmArgs& p, int tile, hipStream_t s) {
-  switch (tile) {
-    case TILE_PP256: return launch_pp256<Mma, OUT>(p, s);
-    case TILE_256x256: return launch_tiled<Mma, OUT, 256, 256, 2, 4>(p, s);
-    case TILE_256x128: return launch_tiled<Mma, OUT, 256, 128, 4, 2>(p, s);
-    case TILE_128x256: return launch_tiled<Mma, OUT, 128, 256, 2, 4>(p, s);
-    case TILE_128x128: return launch_tiled<Mma, OUT, 128, 128, 2, 2>(p, s);
-    case TILE_256x256_W4: return launch_tiled<Mma, OUT, 256, 256, 2, 2>(p, s);
-    case TILE_256x128_W4: return launch_tiled<Mma, OUT, 256, 128, 2, 2>(p, s);
-    case TILE_I256: return launch_tiled<Mma, OUT, 256, 256, 2, 4, true>(p, s);
-    case TILE_I128: return launch_tiled<Mma, OUT, 128, 128, 2, 2, true>(p, s);
-    case TILE_I256W4: return launch_tiled<Mma, OUT, 256, 256, 2, 2, true>(p, s);
-    case TILE_PI256:
-      if (p.M % 256 == 0 && p.N % 256 == 0 && p.flags == nullptr)
-        return launch_persist<Mma, OUT, 256, 256, 2, 4, true>(p, 1, s);
-      return launch_tiled<Mma, OUT, 256, 256, 2, 4, true>(p, s);
-    case TILE_P256:
-      if (p.M % 256 == 0 && p.N % 256 == 0 && p.flags == nullptr)
-        return launch_persist<Mma, OUT, 256, 256, 2, 4>(p, 1, s);
-      return launch_tiled<Mma, OUT, 256, 256, 2, 4>(p, s);
-    case TILE_P128:
-      if (p.M % 128 == 0 && p.N % 128 == 0 && p.flags == nullptr)
-        return launch_persist<Mma, OUT, 128, 128, 2, 2>(p, 2, s);
-      return launch_tiled<Mma, OUT, 128, 128, 2, 2>(p, s);
-    default: return hipErrorInvalidValue;
-  }
-}
-template <int OUT>
-hipError_t launch_mx_cfg(const GemmArgs& p, int tile, hipStream_t s) {
-  switch (tile) {
-    case TILE_PP256:
-    case TILE_256x256: return launch_mx<OUT, 256, 256, 2, 4>(p, s);
-    case TILE_256x128: return launch_mx<OUT, 256, 128, 4, 2>(p, s);
-    case TILE_128x256: return launch_mx<OUT, 128, 256, 2, 4>(p, s);
-    case TILE_128x128: return launch_mx<OUT, 128, 128, 2, 2>(p, s);
-    case TILE_256x256_W4: return launch_mx<OUT, 256, 256, 2, 2>(p, s);
-    case TILE_P256: case TILE_I256: return launch_mx<OUT, 256, 256, 2, 4>(p, s);
-    case TILE_I128: return launch_mx<OUT, 128, 128, 2, 2>(p, s);
-    case TILE_I256W4: return launch_mx<OUT, 256, 256, 2, 2>(p, s);
-    case TILE_PI256: return launch_mx<OUT, 256, 256, 2, 4>(p, s);
-    case TILE_P128: return launch_mx<OUT, 128, 128, 2, 2>(p, s);
-    case TILE_256x128_W4: return launch_mx<OUT, 256, 128, 2, 2>(p, s);
-    default: return hipErrorInvalidValue;
-  }
-}
-
-template <int DIN, int DOUT>
-hipError_t launch_generic_t(const GemmArgs& p, hipStream_t s) {
-  dim3 grid((p.N + 63) / 64, (p.M + 63) / 64);
-  if constexpr (DIN == DT_F64)
-    hipLaunchKernelGGL((gemm_generic_kernel<DIN, DOUT, double>), grid, dim3(256), 0, s, p);
-  else
-    hipLaunchKernelGGL((gemm_generic_kernel<DIN, DOUT, float>), grid, dim3(256), 0, s, p);
-  return hipGetLastError();
-}
-
-}  // namespace
 
 int tile_rows(int tile) {
   return (tile == TILE_128x128 || tile == TILE_128x256 || tile == TILE_P128 || tile == TILE_I128)
@@ -1016,9 +56,14 @@ bool gemm_fast_path_ok(const GemmArgs& p, int din, int dout) {
   return true;
 }
 
-int choose_tile(int64_t M, int64_t N, int din) {
-  // Fill the 256 CUs: prefer the big tile while it yields >= ~1.5 waves of blocks.
+int choose_tile(int64_t M, int64_t N, int64_t K, int din) {
+  // Measured on MI355X (profiles/r01/gemm_*): the LDS-ring kernel wins whenever it gets at least
+  // one 256x256 tile per CU and the K extent is short (<= 2 KiB per row, e.g. K <= 1024 bf16:
+  // the flagship 65536x1024x1024 and the row-parallel 16384x8192x1024 partial); long K prefers
+  // the 128-byte-row interleaved kernel; fewer tiles than CUs want 128x128 blocks.
   auto tiles = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
+  const int64_t kbytes = K * dtype_size(din);
+  if (M % 256 == 0 && N % 256 == 0 && tiles(256, 256) >= 256 && kbytes <= 2048) return TILE_R256;
   if (tiles(256, 256) >= 384) return TILE_I256;
   if (tiles(256, 128) >= 384) return TILE_256x128;
   if (tiles(128, 256) >= 384) return TILE_128x256;
@@ -1034,37 +79,20 @@ hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mo
   const bool fast = mode != GEMM_MODE_GENERIC && gemm_fast_path_ok(p, din, dout);
   if (p.tile_order && !fast) p.tile_order = 0;
   if (fast) {
-    if (tile == TILE_AUTO) tile = choose_tile(p.M, p.N, din);
+    if (tile == TILE_AUTO) tile = choose_tile(p.M, p.N, p.K, din);
     if (p.tile_order && (p.nshards <= 0 || p.M % p.nshards != 0 ||
                          (p.M / p.nshards) % tile_rows(tile) != 0))
       p.tile_order = 0;
-    if (din == DT_FP8 && mode == GEMM_MODE_MX) {
-      if (dout == DT_BF16) return launch_mx_cfg<DT_BF16>(p, tile, s);
-      if (dout == DT_F16) return launch_mx_cfg<DT_F16>(p, tile, s);
-      if (dout == DT_F32) return launch_mx_cfg<DT_F32>(p, tile, s);
-    }
-    if (din == DT_BF16) {
-      if (dout == DT_BF16) return launch_cfg<MmaBF16, DT_BF16>(p, tile, s);
-      if (dout == DT_F32) return launch_cfg<MmaBF16, DT_F32>(p, tile, s);
-    } else if (din == DT_F16) {
-      if (dout == DT_F16) return launch_cfg<MmaF16, DT_F16>(p, tile, s);
-      if (dout == DT_F32) return launch_cfg<MmaF16, DT_F32>(p, tile, s);
-    } else if (din == DT_FP8) {
-      if (dout == DT_BF16) return launch_cfg<MmaFP8, DT_BF16>(p, tile, s);
-      if (dout == DT_F16) return launch_cfg<MmaFP8, DT_F16>(p, tile, s);
-      if (dout == DT_F32) return launch_cfg<MmaFP8, DT_F32>(p, tile, s);
-    } else if (din == DT_F32) {
-      if (dout == DT_F32) return launch_cfg<MmaF32, DT_F32>(p, tile, s);
-    }
+    hipError_t e = hipErrorInvalidValue;
+    if (din == DT_FP8 && mode == GEMM_MODE_MX) e = launch_fast_mx(p, dout, tile, s);
+    else if (din == DT_BF16) e = launch_fast_bf16(p, dout, tile, s);
+    else if (din == DT_F16) e = launch_fast_f16(p, dout, tile, s);
+    else if (din == DT_FP8) e = launch_fast_fp8(p, dout, tile, s);
+    else if (din == DT_F32) e = launch_fast_f32(p, dout, tile, s);
+    if (e != hipErrorInvalidValue) return e;
   }
   if (p.flags != nullptr) return hipErrorNotSupported;  // arrival flags need the tiled kernel
-  // generic path
-#define GEN(DI, DO) if (din == DI && dout == DO) return launch_generic_t<DI, DO>(p, s)
-  GEN(DT_BF16, DT_BF16); GEN(DT_BF16, DT_F32); GEN(DT_F16, DT_F16); GEN(DT_F16, DT_F32);
-  GEN(DT_F32, DT_F32); GEN(DT_F64, DT_F64); GEN(DT_FP8, DT_BF16); GEN(DT_FP8, DT_F16);
-  GEN(DT_FP8, DT_F32);
-#undef GEN
-  return hipErrorInvalidValue;
+  return launch_generic(p, din, dout, s);
 }
 
 }  // namespace ddlb

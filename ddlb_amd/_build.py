@@ -29,13 +29,19 @@ ARCH = os.environ.get("DDLB_OFFLOAD_ARCH", os.environ.get("PYTORCH_ROCM_ARCH", "
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
 SOURCES = [
+    "gemm/gemm_bf16.hip",
+    "gemm/gemm_f16.hip",
+    "gemm/gemm_fp8.hip",
+    "gemm/gemm_f32.hip",
+    "gemm/gemm_mx.hip",
+    "gemm/gemm_generic.hip",
     "gemm/gemm_mfma.hip",
     "runtime/kernels.hip",
     "comm/comm.cpp",
     "runtime/plan.cpp",
     "bindings.cpp",
 ]
-HEADERS = ["gemm/gemm.h", "runtime/kernels.h", "comm/comm.h", "runtime/plan.h"]
+HEADERS = ["gemm/gemm.h", "gemm/gemm_kernels.h", "gemm/gemm_entry.h", "runtime/kernels.h", "comm/comm.h", "runtime/plan.h"]
 
 
 def ext_path() -> str:
@@ -101,7 +107,7 @@ def _compile(src_rel: str, force: bool, verbose: bool) -> str:
 
 def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
     os.makedirs(BUILD, exist_ok=True)
-    jobs = jobs or min(len(SOURCES), max(1, (os.cpu_count() or 4) // 2), 8)
+    jobs = jobs or min(len(SOURCES), max(1, os.cpu_count() or 4), 8)
     with ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, force, verbose), SOURCES))
     out = ext_path()

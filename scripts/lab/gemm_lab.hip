@@ -1,0 +1,607 @@
+// Standalone GEMM lab (not part of the extension): iterate on new CDNA4 GEMM schedules with a
+// plain executable, validate against an fp32 reference kernel, time with hipEvents.
+//
+//   hipcc -O3 --offload-arch=gfx950 -std=c++17 scripts/lab/gemm_lab.hip -o build/gemm_lab
+//   build/gemm_lab 65536 1024 1024
+//
+// Kernel under test: "ring" — persistent 256x256 tiles, 8 waves (2x4, 128x64 per wave),
+// K sliced in 32-deep steps (64-byte LDS rows), NS-slot LDS ring filled by LDS-DMA with
+// NS-1 steps in flight ACROSS barriers (counted vmcnt, never 0 inside the stream), one raw
+// barrier per step, C stores of tile i draining under tile i+1.
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <algorithm>
+#include <vector>
+
+#define CHECK(x)                                                                      \
+  do {                                                                                \
+    hipError_t e_ = (x);                                                              \
+    if (e_ != hipSuccess) {                                                           \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      exit(1);                                                                        \
+    }                                                                                 \
+  } while (0)
+
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+#define LDS_AS __attribute__((address_space(3)))
+#define GLB_AS __attribute__((address_space(1)))
+
+struct Args {
+  const void* a;
+  const void* b;
+  void* c;
+  int64_t lda, ldb, ldc;
+  int M, N, K;
+  unsigned long long* stamps;  // optional per-wave cycle breakdown
+};
+
+__device__ __forceinline__ void glds16(const void* g, void* lds) {
+  __builtin_amdgcn_global_load_lds((const GLB_AS void*)g, (LDS_AS void*)lds, 16, 0, 0);
+}
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, idx = bid >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// swizzle of 16-byte chunk positions inside a 64-byte row: conflict-free ds_read_b128 for
+// 16-row fragments (brute-forced against the gfx950 lane groups)
+__device__ __forceinline__ int swz64(int row) { return (row >> 1) & 2; }
+
+template <int NS, int DPOS, bool STAMP, int EPI = 0>
+__global__ __launch_bounds__(512) void ring_kernel(const Args p) {
+  constexpr int BM = 256, BN = 256, WN = 4;
+  constexpr int ROWB = 64;  // bytes per row per K-step (32 bf16)
+  constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, SLOT = A_BYTES + B_BYTES;
+  constexpr int TM = 128, TN = 64, MR = TM / 16, NR = TN / 16;
+  constexpr int LA = BM / 16 / 8, LB = BN / 16 / 8;  // DMA instructions per wave per step
+  constexpr int NDMA = LA + LB;
+  constexpr int NSTORE = EPI == 1 ? MR * NR / 2 : (EPI == 2 ? 0 : MR * NR);
+  constexpr int NQ = MR * NR;
+  __shared__ __attribute__((aligned(1024))) char smem[NS * SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles_n = p.N / BN, tiles_m = p.M / BM, ntiles = tiles_m * tiles_n;
+  const int nk = p.K * 2 / ROWB;
+  const int my_tiles =
+      ((int)blockIdx.x < ntiles) ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int total = my_tiles * nk;
+  if (total == 0) return;
+
+  // DMA lane mapping: 16 rows x 64 B per instruction; lane -> (row l>>2, physical chunk l&3)
+  const int drow = lane >> 2, dchunk = lane & 3;
+  const char* abase[LA];
+  const char* bbase[LB];
+  int dma_tile = -1;
+  auto set_dma_tile = [&](int ti) {
+    const int wg = xcd_remap((int)blockIdx.x + ti * (int)gridDim.x, ntiles);
+    const int64_t m0 = (int64_t)(wg / tiles_n) * BM, n0 = (int64_t)(wg % tiles_n) * BN;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int row = (wave * LA + i) * 16 + drow;
+      abase[i] = (const char*)p.a + (m0 + row) * p.lda * 2 + ((dchunk ^ swz64(row)) * 16);
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int row = (wave * LB + i) * 16 + drow;
+      // EPI 1: LDS row t of each 32-row block holds column 8*((t&15)>>2) + 4*(t>>4) + (t&3), so a
+      // lane's two adjacent fragments hold 8 consecutive columns (one 16-byte store)
+      const int t32 = row & 31;
+      const int gcol = EPI == 1 ? (row & ~31) + 8 * ((t32 & 15) >> 2) + 4 * (t32 >> 4) + (t32 & 3) : row;
+      bbase[i] = (const char*)p.b + (n0 + gcol) * p.ldb * 2 + ((dchunk ^ swz64(row)) * 16);
+    }
+  };
+  // DMA of stream step g (clamped to the last step: past the end a harmless duplicate lands in a
+  // slot nobody reads again, which keeps the per-step vmcnt arithmetic uniform) into slot gs
+  auto prep = [&](int g) -> int64_t {
+    g = g < total ? g : total - 1;
+    const int ti = g / nk;
+    if (ti != dma_tile) {
+      set_dma_tile(ti);
+      dma_tile = ti;
+    }
+    return (int64_t)(g - ti * nk) * ROWB;
+  };
+  auto dma = [&](int d, int64_t koff, char* base) {
+    if (d < LA) glds16(abase[d] + koff, base + (wave * LA + d) * 1024);
+    else glds16(bbase[d - LA] + koff, base + A_BYTES + (wave * LB + d - LA) * 1024);
+  };
+
+  const int wm = wave / WN, wn = wave % WN;
+  const int frow = lane & 15, fq = lane >> 4;
+  const int rdoff = frow * ROWB + ((fq ^ swz64(frow)) * 16);
+  f32x4 acc[MR][NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  unsigned long long t_wait = 0, t_bar = 0, t_comp = 0, t_epi = 0, t0 = 0, t1 = 0;
+
+  // prologue: NS-1 steps in flight
+  for (int g = 0; g < NS - 1; ++g) {
+    const int64_t koff = prep(g);
+#pragma unroll
+    for (int d = 0; d < NDMA; ++d) dma(d, koff, smem + (g % NS) * SLOT);
+  }
+
+  int stores_window = 0;  // bit j: step (g-1-j) issued C stores (after DMA(g) in issue order)
+  for (int g = 0; g < total; ++g) {
+    if constexpr (STAMP) t0 = __builtin_readcyclecounter();
+    // wait until step g's DMA landed: ops issued after it = DMA of steps g+1..g+NS-2 + the
+    // stores of any tile that ended in steps g-NS+1..g-1
+    const int nst = __builtin_popcount(stores_window);
+    if (nst == 0) wait_vm<NDMA*(NS - 2)>();
+    else if (nst == 1) wait_vm<(NDMA*(NS - 2) + NSTORE < 63 ? NDMA*(NS - 2) + NSTORE : 63)>();
+    else wait_vm<(NDMA*(NS - 2) + 2 * NSTORE < 63 ? NDMA*(NS - 2) + 2 * NSTORE : 63)>();
+    if constexpr (STAMP) { t1 = __builtin_readcyclecounter(); t_wait += t1 - t0; t0 = t1; }
+    const int64_t koff = prep(g + NS - 1);
+    char* nbase = smem + ((g + NS - 1) % NS) * SLOT;
+    __builtin_amdgcn_s_barrier();
+    if constexpr (STAMP) { t1 = __builtin_readcyclecounter(); t_bar += t1 - t0; t0 = t1; }
+
+    const char* As = smem + (g % NS) * SLOT;
+    const char* Bs = As + A_BYTES;
+    if constexpr (DPOS == 0) {
+#pragma unroll
+      for (int d = 0; d < NDMA; ++d) dma(d, koff, nbase);
+    }
+    i32x4 af[MR], bfr[NR];
+#pragma unroll
+    for (int j = 0; j < NR; ++j) bfr[j] = *(const i32x4*)(Bs + (wn * TN + j * 16) * ROWB + rdoff);
+#pragma unroll
+    for (int i = 0; i < MR; ++i) af[i] = *(const i32x4*)(As + (wm * TM + i * 16) * ROWB + rdoff);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int i = q / NR, j = q % NR;
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bfr[j]),
+                                                          __builtin_bit_cast(bf16x8, af[i]),
+                                                          acc[i][j], 0, 0, 0);
+      if constexpr (DPOS == 1) {
+        if (q == NQ / 2 - 1) {
+#pragma unroll
+          for (int d = 0; d < NDMA; ++d) dma(d, koff, nbase);
+        }
+      }
+      if constexpr (DPOS == 2) {
+        if (q % (NQ / NDMA) == 0) dma(q / (NQ / NDMA), koff, nbase);
+      }
+    }
+    if constexpr (DPOS == 2) {
+      __builtin_amdgcn_sched_group_barrier(0x100, MR + NR, 0);  // fragment reads first
+#pragma unroll
+      for (int d = 0; d < NDMA; ++d) {
+        __builtin_amdgcn_sched_group_barrier(0x008, NQ / NDMA, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+    if constexpr (STAMP) { t1 = __builtin_readcyclecounter(); t_comp += t1 - t0; t0 = t1; }
+
+    const int ti = g / nk;
+    const bool last_k = (g - ti * nk) == nk - 1;
+    stores_window = (stores_window << 1) & ((1 << (NS - 1)) - 1);
+    if (last_k) {
+      const int wg = xcd_remap((int)blockIdx.x + ti * (int)gridDim.x, ntiles);
+      const int64_t m0 = (int64_t)(wg / tiles_n) * BM, n0 = (int64_t)(wg % tiles_n) * BN;
+      __builtin_amdgcn_sched_barrier(0);
+      typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+      if constexpr (EPI == 0 || EPI == 2) {
+        if (EPI == 0 || p.M < 0) {
+#pragma unroll
+          for (int i = 0; i < MR; ++i) {
+            char* crow = (char*)p.c + (m0 + wm * TM + i * 16 + frow) * p.ldc * 2;
+#pragma unroll
+            for (int j = 0; j < NR; ++j) {
+              const int64_t col = n0 + wn * TN + j * 16 + fq * 4;
+              const f32x4 v = acc[i][j];
+              bf16x4 o = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+              *(uint2*)(crow + col * 2) = __builtin_bit_cast(uint2, o);
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < MR; ++i) {
+          char* crow = (char*)p.c + (m0 + wm * TM + i * 16 + frow) * p.ldc * 2;
+#pragma unroll
+          for (int jp = 0; jp < NR / 2; ++jp) {
+            const int64_t col = n0 + wn * TN + jp * 32 + fq * 8;
+            const f32x4 v0 = acc[i][2 * jp], v1 = acc[i][2 * jp + 1];
+            typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8o;
+            bf16x8o o = {(__bf16)v0.x, (__bf16)v0.y, (__bf16)v0.z, (__bf16)v0.w,
+                         (__bf16)v1.x, (__bf16)v1.y, (__bf16)v1.z, (__bf16)v1.w};
+            *(uint4*)(crow + col * 2) = __builtin_bit_cast(uint4, o);
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      __builtin_amdgcn_sched_barrier(0);
+      stores_window |= 1;
+      if constexpr (STAMP) { t1 = __builtin_readcyclecounter(); t_epi += t1 - t0; t0 = t1; }
+    }
+  }
+  wait_vm<0>();
+  if constexpr (STAMP) {
+    if (lane == 0) {
+      unsigned long long* s = p.stamps + ((size_t)blockIdx.x * 8 + wave) * 4;
+      s[0] = t_wait; s[1] = t_bar; s[2] = t_comp; s[3] = t_epi;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// ring2: same ring, but the barrier sits in the MIDDLE of a step's MFMAs so the matrix pipe never
+// waits for fragment reads:
+//   part A: MFMAs rows 0-3 (A0 x Bc) + DMA of step g+NS-1 + reads of A1 (rows 4-7, step g)
+//   wait DMA(g+1); lgkmcnt(0); barrier
+//   part C: MFMAs rows 4-7 (A1 x Bc) + reads of A0 and Bn for step g+1
+template <int NS, bool STAMP, int DMAP = 0, int PRIO = 0, int EPI = 1>
+__global__ __launch_bounds__(512) void ring2_kernel(const Args p) {
+  constexpr int BM = 256, BN = 256, WN = 4;
+  constexpr int ROWB = 64;
+  constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, SLOT = A_BYTES + B_BYTES;
+  constexpr int TM = 128, TN = 64, MR = TM / 16, NR = TN / 16, MH = MR / 2;
+  constexpr int LA = BM / 16 / 8, LB = BN / 16 / 8;
+  constexpr int NDMA = LA + LB;
+  constexpr int NSTORE = MR * NR / 2;  // 16-byte stores
+  static_assert(NS >= 3, "need at least one step in flight beyond the next");
+  __shared__ __attribute__((aligned(1024))) char smem[NS * SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles_n = p.N / BN, tiles_m = p.M / BM, ntiles = tiles_m * tiles_n;
+  const int nk = p.K * 2 / ROWB;
+  const int my_tiles =
+      ((int)blockIdx.x < ntiles) ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int total = my_tiles * nk;
+  if (total == 0) return;
+
+  const int drow = lane >> 2, dchunk = lane & 3;
+  const char* abase[LA];
+  const char* bbase[LB];
+  int dma_tile = -1;
+  auto set_dma_tile = [&](int ti) {
+    const int wg = xcd_remap((int)blockIdx.x + ti * (int)gridDim.x, ntiles);
+    const int64_t m0 = (int64_t)(wg / tiles_n) * BM, n0 = (int64_t)(wg % tiles_n) * BN;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int row = (wave * LA + i) * 16 + drow;
+      abase[i] = (const char*)p.a + (m0 + row) * p.lda * 2 + ((dchunk ^ swz64(row)) * 16);
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int row = (wave * LB + i) * 16 + drow;
+      const int t32 = row & 31;
+      const int gcol = (row & ~31) + 8 * ((t32 & 15) >> 2) + 4 * (t32 >> 4) + (t32 & 3);
+      bbase[i] = (const char*)p.b + (n0 + gcol) * p.ldb * 2 + ((dchunk ^ swz64(row)) * 16);
+    }
+  };
+  auto prep = [&](int g) -> int64_t {
+    g = g < total ? g : total - 1;
+    const int ti = g / nk;
+    if (ti != dma_tile) {
+      set_dma_tile(ti);
+      dma_tile = ti;
+    }
+    return (int64_t)(g - ti * nk) * ROWB;
+  };
+  auto dma = [&](int d, int64_t koff, char* base) {
+    if (d < LA) glds16(abase[d] + koff, base + (wave * LA + d) * 1024);
+    else glds16(bbase[d - LA] + koff, base + A_BYTES + (wave * LB + d - LA) * 1024);
+  };
+
+  const int wm = wave / WN, wn = wave % WN;
+  const int frow = lane & 15, fq = lane >> 4;
+  const int rdoff = frow * ROWB + ((fq ^ swz64(frow)) * 16);
+  const int aoff = wm * TM * ROWB + rdoff, boff = A_BYTES + wn * TN * ROWB + rdoff;
+  f32x4 acc[MR][NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](int i, int j, const i32x4& a, const i32x4& b) {
+    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, b),
+                                                        __builtin_bit_cast(bf16x8, a), acc[i][j],
+                                                        0, 0, 0);
+  };
+
+  unsigned long long t_wait = 0, t_a = 0, t_c = 0, t_epi = 0, t_vm = 0, t0 = 0, t1 = 0;
+  unsigned long long c_start = 0, r_start = 0;
+  if constexpr (STAMP) {
+    c_start = __builtin_readcyclecounter();
+    r_start = __builtin_amdgcn_s_memrealtime();
+  }
+
+  for (int g = 0; g < NS - 1; ++g) {
+    const int64_t koff = prep(g);
+#pragma unroll
+    for (int d = 0; d < NDMA; ++d) dma(d, koff, smem + (g % NS) * SLOT);
+  }
+  wait_vm<NDMA*(NS - 2)>();
+  __builtin_amdgcn_s_barrier();
+  i32x4 A0[MH], A1[MH], Bc[NR], Bn[NR];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) Bc[j] = *(const i32x4*)(smem + boff + j * 16 * ROWB);
+#pragma unroll
+  for (int i = 0; i < MH; ++i) A0[i] = *(const i32x4*)(smem + aoff + i * 16 * ROWB);
+
+  if constexpr (PRIO == 1) {
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+  }
+  int stores_window = 0;  // bit j: step g-1-j issued C stores
+  for (int g = 0; g < total; ++g) {
+    if constexpr (STAMP) t0 = __builtin_readcyclecounter();
+    const char* cur = smem + (g % NS) * SLOT;
+    const char* nxt = smem + ((g + 1) % NS) * SLOT;
+    const int64_t koff = prep(g + NS - 1);
+    char* nbase = smem + ((g + NS - 1) % NS) * SLOT;
+    // ---- part A
+    constexpr int DA = DMAP == 0 ? NDMA : (DMAP == 1 ? 0 : NDMA / 2);  // DMAs in part A
+    if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int q = 0; q < MH * NR; ++q) {
+      const int i = q / NR, j = q % NR;
+      mma(i, j, A0[i], Bc[j]);
+      if (DA > 0 && q % (16 / (DA > 0 ? DA : 1)) == 1) dma(q / (16 / (DA > 0 ? DA : 1)), koff, nbase);
+      if (q % 4 == 3) A1[q / 4] = *(const i32x4*)(cur + aoff + (MH + q / 4) * 16 * ROWB);
+    }
+    if constexpr (DA == 4) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+    } else if constexpr (DA == 2) {
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+    }
+    if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(0);
+    if constexpr (STAMP) { t1 = __builtin_readcyclecounter(); t_a += t1 - t0; t0 = t1; }
+    // ---- wait for step g+1's DMA (ops issued after it: DMA of g+2..g+NS-1, stores of steps
+    //      g-NS+2..g-1), all fragment reads of this slot done, barrier
+    // DMA halves issued in part C of step g-NS+2 are the newest part of DMA(g+1)
+    constexpr int VMB = NDMA * (NS - 2) - (NDMA - DA);
+    const int nst = __builtin_popcount(stores_window);
+    if (nst == 0) wait_vm<VMB>();
+    else if (nst == 1) wait_vm<(VMB + NSTORE < 63 ? VMB + NSTORE : 63)>();
+    else wait_vm<(VMB + 2 * NSTORE < 63 ? VMB + 2 * NSTORE : 63)>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (STAMP) { t1 = __builtin_readcyclecounter(); t_vm += t1 - t0; t0 = t1; }
+    __builtin_amdgcn_s_barrier();
+    if constexpr (STAMP) { t1 = __builtin_readcyclecounter(); t_wait += t1 - t0; t0 = t1; }
+    // ---- part C
+    constexpr int DC = NDMA - DA;
+    if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int q = 0; q < MH * NR; ++q) {
+      const int j = q / MH, i = MH + q % MH;  // j-major: Bc[j] free after its 4 MFMAs
+      mma(i, j, A1[i - MH], Bc[j]);
+      if (q % 2 == 1) {
+        const int r = q / 2;  // 8 reads: Bn[0..3], A0[0..3] of step g+1
+        if (r < NR) Bn[r] = *(const i32x4*)(nxt + boff + r * 16 * ROWB);
+        else A0[r - NR] = *(const i32x4*)(nxt + aoff + (r - NR) * 16 * ROWB);
+      }
+      if (DC > 0 && q % (16 / (DC > 0 ? DC : 1)) == 0) dma(DA + q / (16 / (DC > 0 ? DC : 1)), koff, nbase);
+    }
+    if constexpr (DC == 0) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        if ((r * 2) % (16 / (DC > 0 ? DC : 1)) == 0) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+    }
+    if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(0);
+    if constexpr (STAMP) { t1 = __builtin_readcyclecounter(); t_c += t1 - t0; t0 = t1; }
+#pragma unroll
+    for (int j = 0; j < NR; ++j) Bc[j] = Bn[j];
+
+    const int ti = g / nk;
+    const bool last_k = (g - ti * nk) == nk - 1;
+    stores_window = (stores_window << 1) & ((1 << (NS - 2)) - 1);
+    if (last_k) {
+      const int wg = xcd_remap((int)blockIdx.x + ti * (int)gridDim.x, ntiles);
+      const int64_t m0 = (int64_t)(wg / tiles_n) * BM, n0 = (int64_t)(wg % tiles_n) * BN;
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < MR; ++i) {
+        char* crow = (char*)p.c + (m0 + wm * TM + i * 16 + frow) * p.ldc * 2;
+#pragma unroll
+        for (int jp = 0; jp < NR / 2; ++jp) {
+          const int64_t col = n0 + wn * TN + jp * 32 + fq * 8;
+          const f32x4 v0 = acc[i][2 * jp], v1 = acc[i][2 * jp + 1];
+          typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8o;
+          bf16x8o o = {(__bf16)v0.x, (__bf16)v0.y, (__bf16)v0.z, (__bf16)v0.w,
+                       (__bf16)v1.x, (__bf16)v1.y, (__bf16)v1.z, (__bf16)v1.w};
+          if (EPI == 3) __builtin_nontemporal_store(__builtin_bit_cast(i32x4, o), (i32x4*)(crow + col * 2));
+          else if (EPI == 1 || p.M < 0) *(uint4*)(crow + col * 2) = __builtin_bit_cast(uint4, o);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      __builtin_amdgcn_sched_barrier(0);
+      stores_window |= 1;
+      if constexpr (STAMP) { t1 = __builtin_readcyclecounter(); t_epi += t1 - t0; t0 = t1; }
+    }
+  }
+  wait_vm<0>();
+  if constexpr (STAMP) {
+    if (lane == 0 && blockIdx.x == 0 && wave == 0) {
+      p.stamps[(size_t)gridDim.x * 8 * 5 + 1] = __builtin_readcyclecounter() - c_start;
+      p.stamps[(size_t)gridDim.x * 8 * 5 + 3] = __builtin_amdgcn_s_memrealtime() - r_start;
+    }
+    if (lane == 0) {
+      unsigned long long* s = p.stamps + ((size_t)blockIdx.x * 8 + wave) * 5;
+      s[0] = t_wait; s[1] = t_a; s[2] = t_c; s[3] = t_epi; s[4] = t_vm;
+    }
+  }
+}
+
+// fp32 reference: C[m][n] = sum_k A[m][k] * B[n][k]
+__global__ void ref_kernel(const __hip_bfloat16* A, const __hip_bfloat16* B, float* C, int M, int N,
+                           int K) {
+  __shared__ float as[16][65], bs[16][65];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int m = blockIdx.y * 16 + ty, n = blockIdx.x * 16 + tx;
+  float acc = 0.f;
+  for (int k0 = 0; k0 < K; k0 += 64) {
+    for (int kk = tx; kk < 64; kk += 16) {
+      as[ty][kk] = (float)A[(size_t)(blockIdx.y * 16 + ty) * K + k0 + kk];
+      bs[ty][kk] = (float)B[(size_t)(blockIdx.x * 16 + ty) * K + k0 + kk];
+    }
+    __syncthreads();
+    for (int kk = 0; kk < 64; ++kk) acc += as[ty][kk] * bs[tx][kk];
+    __syncthreads();
+  }
+  C[(size_t)m * N + n] = acc;
+}
+
+__global__ void fill_kernel(__hip_bfloat16* x, size_t n, uint32_t seed) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  for (; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 13; h *= 0x5bd1e995u; h ^= h >> 15;
+    x[i] = (__hip_bfloat16)(((h & 0xffffff) / 16777216.0f) * 2.f - 1.f);
+  }
+}
+
+__global__ void cmp_kernel(const __hip_bfloat16* C, const float* R, size_t n, float* maxerr) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  float e = 0.f;
+  for (; i < n; i += (size_t)gridDim.x * blockDim.x) e = fmaxf(e, fabsf((float)C[i] - R[i]));
+  atomicMax((int*)maxerr, __float_as_int(e));
+}
+
+typedef void (*KFn)(const Args);
+
+struct Variant {
+  const char* name;
+  KFn fn;
+  int ns;
+};
+
+int main(int argc, char** argv) {
+  const int M = argc > 1 ? atoi(argv[1]) : 65536;
+  const int N = argc > 2 ? atoi(argv[2]) : 1024;
+  const int K = argc > 3 ? atoi(argv[3]) : 1024;
+  const int rounds = 5, iters = 20;
+  if (M % 256 || N % 256 || K % 32) { fprintf(stderr, "shape must be multiple of 256/256/32\n"); return 2; }
+  int dev = 0, ncu = 0;
+  CHECK(hipGetDevice(&dev));
+  CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  __hip_bfloat16 *A, *B, *C;
+  float *R, *err;
+  CHECK(hipMalloc(&A, (size_t)M * K * 2));
+  CHECK(hipMalloc(&B, (size_t)N * K * 2));
+  CHECK(hipMalloc(&C, (size_t)M * N * 2));
+  CHECK(hipMalloc(&R, (size_t)M * N * 4));
+  CHECK(hipMalloc(&err, 4));
+  fill_kernel<<<1024, 256>>>(A, (size_t)M * K, 1u);
+  fill_kernel<<<1024, 256>>>(B, (size_t)N * K, 2u);
+  ref_kernel<<<dim3(N / 16, M / 16), 256>>>(A, B, R, M, N, K);
+  CHECK(hipDeviceSynchronize());
+  unsigned long long* stamps;
+  const int grid = std::min(ncu, (M / 256) * (N / 256));
+  CHECK(hipMalloc(&stamps, ((size_t)grid * 8 * 5 + 8) * 8));
+
+  Variant vs[] = {
+      {"ring2 ns4", ring2_kernel<4, false>, 4},
+      {"ring2 dmaAC", ring2_kernel<4, false, 2>, 4},
+      {"ring2 ns3 dmaAC", ring2_kernel<3, false, 2>, 3},
+      {"ring2 ns5 dmaAC", ring2_kernel<5, false, 2>, 5},
+      {"ring2 dmaAC noprio", ring2_kernel<4, false, 2, 2>, 4},
+      {"ring2 dmaAC nt", ring2_kernel<4, false, 2, 0, 3>, 4},
+      {"ring2 dmaAC nost", ring2_kernel<4, false, 2, 0, 2>, 4},
+  };
+  Args a{A, B, C, K, K, N, M, N, K, nullptr};
+  const double flop = 2.0 * M * N * K;
+  std::vector<std::vector<float>> times(sizeof(vs) / sizeof(vs[0]));
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  for (size_t v = 0; v < sizeof(vs) / sizeof(vs[0]); ++v) {
+    CHECK(hipMemset(C, 0, (size_t)M * N * 2));
+    CHECK(hipMemset(err, 0, 4));
+    hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(512), 0, 0, a);
+    CHECK(hipGetLastError());
+    cmp_kernel<<<1024, 256>>>(C, R, (size_t)M * N, err);
+    float e = 0;
+    CHECK(hipMemcpy(&e, err, 4, hipMemcpyDeviceToHost));
+    printf("%-20s max|err| = %.4g %s\n", vs[v].name, e, e < 2e-3 * K ? "ok" : "FAIL");
+  }
+  for (int r = 0; r < rounds; ++r)
+    for (size_t v = 0; v < sizeof(vs) / sizeof(vs[0]); ++v) {
+      for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(512), 0, 0, a);
+      CHECK(hipEventRecord(e0));
+      for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(512), 0, 0, a);
+      CHECK(hipEventRecord(e1));
+      CHECK(hipEventSynchronize(e1));
+      float ms;
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      times[v].push_back(ms / iters);
+    }
+  printf("\n%dx%dx%d bf16, grid %d\n", M, N, K, grid);
+  for (size_t v = 0; v < sizeof(vs) / sizeof(vs[0]); ++v) {
+    auto t = times[v];
+    std::sort(t.begin(), t.end());
+    const float med = t[t.size() / 2];
+    printf("  %-20s %8.4f ms  %7.1f TFLOP/s\n", vs[v].name, med, flop / (med * 1e-3) / 1e12);
+  }
+  // stamps for NS=4
+  Args s = a;
+  s.stamps = stamps;
+  CHECK(hipMemset(stamps, 0, ((size_t)grid * 8 * 5 + 8) * 8));
+  hipLaunchKernelGGL((ring2_kernel<4, true, 2>), dim3(grid), dim3(512), 0, 0, s);
+  CHECK(hipDeviceSynchronize());
+  std::vector<unsigned long long> h((size_t)grid * 8 * 5 + 8);
+  CHECK(hipMemcpy(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost));
+  double sum[5] = {0, 0, 0, 0, 0};
+  for (size_t i = 0; i < (size_t)grid * 8 * 5; ++i) sum[i % 5] += (double)h[i];
+  const double nw = grid * 8.0, steps = (double)(M / 256) * (N / 256) * (K / 32) / grid;
+  printf("\nstamps (ring2 NS=4, cycles per step per wave): vmwait %.0f barrier %.0f  partA %.0f  partC %.0f  epilogue(amortized) %.0f\n",
+         sum[4] / nw / steps, sum[0] / nw / steps, sum[1] / nw / steps, sum[2] / nw / steps, sum[3] / nw / steps);
+  {
+    const double cyc = (double)h[(size_t)grid * 8 * 5 + 1], ns = (double)h[(size_t)grid * 8 * 5 + 3] * 10.0;
+    printf("block 0 wave 0: %.0f cycles in %.1f us -> %.2f GHz\n", cyc, ns / 1e3, cyc / ns);
+  }
+  printf("ideal MFMA cycles per step per wave: %d (x2 waves per SIMD)\n", 32 * 16);
+  return 0;
+}

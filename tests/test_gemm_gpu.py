@@ -35,7 +35,7 @@ def gen():
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
-@pytest.mark.parametrize("tile", ["256x256", "256x128", "128x256", "128x128", "pp256", "256x256w4", "256x128w4", "p256", "p128", "i256", "i128", "i256w4", "pi256"])
+@pytest.mark.parametrize("tile", ["256x256", "256x128", "128x256", "128x128", "pp256", "256x256w4", "256x128w4", "p256", "p128", "i256", "i128", "i256w4", "pi256", "pi256w4", "r256"])
 def test_gemm_tiles(dtype, tile, gen):
     from ddlb_amd.ops.gemm import gemm
 
@@ -96,7 +96,7 @@ def test_gemm_fp8(mode, odt, gen):
     torch.testing.assert_close(out.float(), _ref(a, w), rtol=0, atol=_tol(torch.float8_e4m3fn, K))
 
 
-@pytest.mark.parametrize("tile", ["auto", "pp256", "128x128", "256x256w4", "256x128w4", "p256", "p128", "i256", "i128", "i256w4", "pi256"])
+@pytest.mark.parametrize("tile", ["auto", "pp256", "128x128", "256x256w4", "256x128w4", "p256", "p128", "i256", "i128", "i256w4", "pi256", "r256"])
 def test_fp8_integer_exact(gen, tile):
     """Small integers are exact in e4m3: both fp8 paths must match bit for bit."""
     from ddlb_amd.ops.gemm import gemm
@@ -133,7 +133,7 @@ def test_grouped_rows(gen):
     assert torch.count_nonzero(C[untouched].float()) == 0
 
 
-@pytest.mark.parametrize("tile", ["auto", "pp256", "128x128", "256x256w4", "256x128w4", "p256", "p128", "i256", "i128", "i256w4", "pi256"])
+@pytest.mark.parametrize("tile", ["auto", "pp256", "128x128", "256x256w4", "256x128w4", "p256", "p128", "i256", "i128", "i256w4", "pi256", "r256"])
 @pytest.mark.parametrize("shape", [(2048, 1024, 1024), (4096, 2048, 2048), (768, 512, 192)])
 def test_repeat_race_screen(gen, tile, shape):
     """Same inputs, 20 launches: identical bits every time (LDS-DMA/barrier race screen)."""
@@ -161,7 +161,7 @@ def test_host_checks_reject_bad_shapes(gen):
         gemm(a, _rand((64, 128), torch.bfloat16, gen), M=128)
 
 
-@pytest.mark.parametrize("tile", ["p256", "p128", "pi256"])
+@pytest.mark.parametrize("tile", ["p256", "p128", "pi256", "r256"])
 def test_persistent_many_tiles_grouped(gen, tile):
     """Persistent streaming kernel: more tiles than blocks, grouped C rows, repeat-identical."""
     from ddlb_amd.ops.gemm import gemm
@@ -184,7 +184,7 @@ def test_persistent_many_tiles_grouped(gen, tile):
 
 
 @pytest.mark.parametrize("act", ["gelu", "relu", "silu"])
-@pytest.mark.parametrize("tile", ["auto", "128x128", "pi256"])
+@pytest.mark.parametrize("tile", ["auto", "128x128", "pi256", "r256"])
 def test_fused_activation_epilogue(gen, act, tile):
     from ddlb_amd.ops.gemm import gemm
     from ddlb_amd.parallel.sim import apply_act
@@ -195,3 +195,50 @@ def test_fused_activation_epilogue(gen, act, tile):
     torch.cuda.synchronize()
     code = {"gelu": 1, "relu": 2, "silu": 3}[act]
     torch.testing.assert_close(out.float(), apply_act(_ref(a, w), code), rtol=0.02, atol=0.05)
+
+
+_RING_DT = [(torch.bfloat16, torch.bfloat16), (torch.bfloat16, torch.float32),
+            (torch.float16, torch.float16), (torch.float16, torch.float32),
+            (torch.float32, torch.float32), (torch.float8_e4m3fn, torch.bfloat16),
+            (torch.float8_e4m3fn, torch.float32)]
+
+
+@pytest.mark.parametrize("dt", _RING_DT, ids=lambda d: f"{str(d[0])[6:]}-{str(d[1])[6:]}")
+@pytest.mark.parametrize("shape", [(256, 256, 128), (8192, 1024, 512), (32768, 1024, 256),
+                                   (4096, 768, 1024)])
+def test_ring_kernel(dt, shape, gen):
+    """LDS-ring kernel: one tile, fewer tiles than CUs, several tiles per block (C stores of one
+    tile draining under the next), N not a power of two; every input/output dtype."""
+    from ddlb_amd.ops.gemm import gemm
+
+    din, dout = dt
+    M, N, K = shape
+    a, w = _rand((M, K), din, gen), _rand((N, K), din, gen)
+    out = gemm(a, w, tile="r256", out_dtype=dout)
+    torch.cuda.synchronize()
+    assert out.dtype == dout
+    torch.testing.assert_close(out.float(), _ref(a, w), rtol=0, atol=_tol(din, K))
+    again = gemm(a, w, tile="r256", out_dtype=dout)
+    torch.cuda.synchronize()
+    assert torch.equal(out, again)
+
+
+def test_ring_grouped_rows(gen):
+    """Ring kernel with the pipelines' strided A and C row blocks."""
+    from ddlb_amd.ops.gemm import gemm
+
+    d, blk, K, N = 4, 512, 256, 1024
+    A = _rand((d * 2048, K), torch.bfloat16, gen)
+    w = _rand((N, K), torch.bfloat16, gen)
+    C = torch.zeros((d * 2048, N), dtype=torch.bfloat16, device=DEV)
+    j = 1
+    gemm(A[j * blk:], w, C[j * blk:], M=d * blk, a_grp=blk, a_gstride=2048, c_grp=blk,
+         c_gstride=2048, tile="r256")
+    torch.cuda.synchronize()
+    ref = _ref(A, w)
+    mask = torch.zeros(d * 2048, dtype=torch.bool, device=DEV)
+    for r in range(d):
+        rows = slice(r * 2048 + j * blk, r * 2048 + (j + 1) * blk)
+        mask[rows] = True
+        torch.testing.assert_close(C[rows].float(), ref[rows], rtol=0, atol=_tol(torch.bfloat16, K))
+    assert torch.count_nonzero(C[~mask].float()) == 0
