@@ -37,21 +37,35 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 # (label, impl, options), tried in this order; RCCL paths first (most mature transport).
+# "/blas" = the plan's plain GEMM ops on hipBLASLt (gemm_mode=blas), everything else identical.
+def _blas(opts):
+    return dict(opts, gemm_mode="blas")
+
+
+_COLL4 = dict(algorithm="coll_pipeline", backend="rccl", s=4)
+_DEF = dict(algorithm="default", backend="rccl")
+_P2P = dict(algorithm="p2p_pipeline", backend="ipc", multicast_protocol="memcpy")
+_COLL_IPC = dict(algorithm="coll_pipeline", backend="ipc", multicast_protocol="memcpy", s=4)
+_DEF_K = dict(algorithm="default", backend="ipc", multicast_protocol="kernel", copy_blocks=128)
 CANDIDATES = [
-    ("coll_pipeline/rccl/s4", "native", dict(algorithm="coll_pipeline", backend="rccl", s=4)),
-    ("default/rccl", "native", dict(algorithm="default", backend="rccl")),
-    ("p2p_pipeline/ipc/memcpy", "native", dict(algorithm="p2p_pipeline", backend="ipc",
-                                                multicast_protocol="memcpy")),
-    ("p2p_pipeline/ipc/memcpy/fused", "native", dict(algorithm="p2p_pipeline", backend="ipc",
-                                                      multicast_protocol="memcpy", fused=True)),
-    ("coll_pipeline/ipc/memcpy/s4", "native", dict(algorithm="coll_pipeline", backend="ipc",
-                                                    multicast_protocol="memcpy", s=4)),
-    ("default/ipc/kernel", "native", dict(algorithm="default", backend="ipc",
-                                           multicast_protocol="kernel", copy_blocks=128)),
-    ("coll_pipeline/rccl/s8", "native", dict(algorithm="coll_pipeline", backend="rccl", s=8)),
-    ("coll_pipeline/rccl/s4/graph", "native", dict(algorithm="coll_pipeline", backend="rccl", s=4,
-                                                    graph=True)),
+    ("coll_pipeline/rccl/s4", "native", _COLL4),
+    ("coll_pipeline/rccl/s4/blas", "native", _blas(_COLL4)),
+    ("default/rccl", "native", _DEF),
+    ("default/rccl/blas", "native", _blas(_DEF)),
+    ("p2p_pipeline/ipc/memcpy", "native", _P2P),
+    ("p2p_pipeline/ipc/memcpy/blas", "native", _blas(_P2P)),
+    ("p2p_pipeline/ipc/memcpy/fused", "native", dict(_P2P, fused=True)),
+    ("coll_pipeline/ipc/memcpy/s4", "native", _COLL_IPC),
+    ("coll_pipeline/ipc/memcpy/s4/blas", "native", _blas(_COLL_IPC)),
+    ("default/ipc/kernel", "native", _DEF_K),
+    ("default/ipc/kernel/blas", "native", _blas(_DEF_K)),
+    ("coll_pipeline/rccl/s8", "native", dict(_COLL4, s=8)),
     ("pytorch(rccl+hipblaslt)", "pytorch", dict(backend="nccl", empty_cache=False)),
+]
+# world 1: the all-gather is the identity; the plan is one GEMM on either kernel family
+WORLD1 = [
+    ("gemm (world=1)/hip", "native", _DEF),
+    ("gemm (world=1)/blas", "native", _blas(_DEF)),
 ]
 
 
@@ -79,6 +93,14 @@ def child_main(a) -> int:
             except AssertionError as e:
                 valid = False
                 res["validation"] = str(e).splitlines()[0][:200]
+        # untimed pre-warm: keep the GPU busy for prewarm_ms so the timed window does not
+        # include the clock ramp out of idle (measured: 10 warmups of this step leave the
+        # first 50 timed steps ~14 % slow). Then the W warmup steps of the contract.
+        t_end = time.perf_counter() + a.prewarm_ms / 1e3
+        while time.perf_counter() < t_end:
+            for _ in range(8):
+                impl.run()
+            comm.synchronize()
         for _ in range(a.warmup):
             impl.run()
         comm.barrier()
@@ -142,7 +164,7 @@ class Job:
         return out
 
     def measure(self, impl: str, opts: dict, steps: int, warmup: int, validate: bool,
-                timeout: float) -> dict:
+                timeout: float, prewarm_ms: float = 0.0) -> dict:
         """Run one measurement in a child per rank; every rank returns the same dict."""
         self.counter += 1
         port = self.bcast(_free_port() if self.rank == 0 else None)
@@ -152,7 +174,8 @@ class Job:
         cmd = [sys.executable, os.path.abspath(__file__), "--child", "--child-out", out,
                "--child-impl", impl, "--child-opts", json.dumps(opts), "--steps", str(steps),
                "--warmup", str(warmup), "-m", str(self.a.m), "-n", str(self.a.n), "-k",
-               str(self.a.k), "--dtype", self.a.dtype, "--child-timeout", str(timeout)]
+               str(self.a.k), "--dtype", self.a.dtype, "--child-timeout", str(timeout),
+               "--prewarm-ms", str(prewarm_ms)]
         if validate:
             cmd.append("--validate")
         proc = subprocess.Popen(cmd, env=env)
@@ -190,6 +213,8 @@ def main(argv=None) -> int:
     p.add_argument("--tune-steps", type=int, default=10)
     p.add_argument("--candidate-timeout", type=float, default=180.0)
     p.add_argument("--no-validate", dest="validate", action="store_false", default=True)
+    p.add_argument("--prewarm-ms", type=float, default=300.0,
+                   help="untimed GPU pre-warm before the warmup steps (clock ramp)")
     # child-mode arguments (internal)
     p.add_argument("--child", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--child-out", help=argparse.SUPPRESS)
@@ -207,18 +232,18 @@ def main(argv=None) -> int:
         return 2
     job = Job(a)
     tune = {}
+    pool = WORLD1 if world == 1 else CANDIDATES
     if a.algorithm != "auto":
-        match = [c for c in CANDIDATES if c[0] == a.algorithm]
+        match = [c for c in WORLD1 + CANDIDATES if c[0] == a.algorithm]
         if not match:
             raise SystemExit(f"unknown --algorithm {a.algorithm}; choose from "
-                             f"{[c[0] for c in CANDIDATES]}")
+                             f"{[c[0] for c in WORLD1 + CANDIDATES]}")
         chosen = match[0]
-    elif world == 1:
-        chosen = ("gemm (world=1)", "native", dict(algorithm="default", backend="rccl"))
     else:
         best = None
-        for label, impl, opts in CANDIDATES:
-            r = job.measure(impl, opts, a.tune_steps, 3, False, a.candidate_timeout)
+        for label, impl, opts in pool:
+            r = job.measure(impl, opts, a.tune_steps, 3, False, a.candidate_timeout,
+                            prewarm_ms=min(a.prewarm_ms, 100.0))
             tune[label] = round(r["ms"], 4) if r["ok"] else r["error"][:160]
             if r["ok"] and impl == "native" and (best is None or r["ms"] < best[0]):
                 best = (r["ms"], (label, impl, opts))
@@ -227,7 +252,7 @@ def main(argv=None) -> int:
             return 1
         chosen = best[1]
     final = job.measure(chosen[1], chosen[2], a.steps, a.warmup, a.validate,
-                        a.candidate_timeout + a.steps * 0.05)
+                        a.candidate_timeout + a.steps * 0.05, prewarm_ms=a.prewarm_ms)
     if not final["ok"]:
         sys.stderr.write(f"final measurement failed: {final['error']}\n")
         return 1
@@ -245,6 +270,9 @@ def main(argv=None) -> int:
                        "global_batch": 1, "seq_len": a.m, "parallelism": f"tp{world}-sp",
                        "implementation": chosen[1], "algorithm": chosen[0]},
             "per_gpu_tflops": round(per_gpu, 6), "valid": final.get("valid"),
+            "gemm": ("hipblaslt" if chosen[1] == "pytorch" or chosen[2].get("gemm_mode") == "blas"
+                     else "ddlb_amd MFMA"),
+            "prewarm_ms": a.prewarm_ms,
             "autotune_ms": tune,
         }
         print(json.dumps(line), flush=True)

@@ -1,0 +1,173 @@
+// hipBLASLt backend for PLAIN GEMMs inside native plans (gemm_mode = blas).
+//
+// The hand-written kernels (gemm_kernels.h) stay the path for everything fused — arrival-flag
+// gated tiles, epilogue activations, fp8/MX — and for ragged groupings; a plain or
+// strided-batched bf16/f16/f32 GEMM may instead run on the vendor library, which is what the
+// reference's torch.matmul reaches (ddlb/primitives/TPColumnwise/pytorch.py:97). The autotuner
+// (bench.py) times both and reports which one ran.
+//
+// Mapping to hipBLASLt's column-major problem: C[M,N] = A[M,K] * Bt[N,K]^T (all row-major) is
+// C^T (N x M, ld = ldc) = op(Bt)^T-view (N x K) * A^T-view (K x M): "A" = Bt with TRANSA = T,
+// "B" = A with TRANSB = N. Grouped-row addressing with equal A and C groups becomes a strided
+// batch: batch = M / grp, A stride = a_gstride * lda, C stride = c_gstride * ldc, Bt stride 0.
+#include <hip/hip_runtime.h>
+#include <hipblaslt/hipblaslt.h>
+
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+#include <unordered_map>
+
+#include "gemm.h"
+
+namespace ddlb {
+namespace {
+
+struct LtKey {
+  int dev, din, dout;
+  int64_t m, n, k, lda, ldb, ldc, batch, sa, sc;
+  bool operator==(const LtKey& o) const { return std::memcmp(this, &o, sizeof(LtKey)) == 0; }
+};
+struct LtKeyHash {
+  size_t operator()(const LtKey& k) const {
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(&k);
+    uint64_t h = 1469598103934665603ull;
+    for (size_t i = 0; i < sizeof(LtKey) / 8; ++i) h = (h ^ w[i]) * 1099511628211ull;
+    return (size_t)h;
+  }
+};
+struct LtPlan {
+  hipblasLtMatmulDesc_t op = nullptr;
+  hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr;
+  hipblasLtMatmulAlgo_t algo;
+  size_t ws = 0;
+  bool ok = false;
+};
+struct LtDevice {
+  hipblasLtHandle_t handle = nullptr;
+  void* workspace = nullptr;
+  size_t ws_bytes = 0;
+};
+
+constexpr size_t kWorkspace = 64ull << 20;
+std::mutex g_mu;
+std::unordered_map<int, LtDevice> g_dev;
+std::unordered_map<LtKey, LtPlan, LtKeyHash> g_plans;
+
+bool lt_type(int dt, hipDataType* t) {
+  switch (dt) {
+    case DT_BF16: *t = HIP_R_16BF; return true;
+    case DT_F16: *t = HIP_R_16F; return true;
+    case DT_F32: *t = HIP_R_32F; return true;
+    default: return false;
+  }
+}
+
+LtDevice* device_state(int dev) {
+  LtDevice& d = g_dev[dev];
+  if (d.handle == nullptr) {
+    if (hipblasLtCreate(&d.handle) != HIPBLAS_STATUS_SUCCESS) {
+      d.handle = nullptr;
+      return nullptr;
+    }
+    if (hipMalloc(&d.workspace, kWorkspace) != hipSuccess) {
+      (void)hipGetLastError();
+      d.workspace = nullptr;
+      d.ws_bytes = 0;
+    } else {
+      d.ws_bytes = kWorkspace;
+    }
+  }
+  return &d;
+}
+
+bool build_plan(LtDevice* d, const LtKey& key, LtPlan* pl) {
+  hipDataType tin, tout;
+  if (!lt_type(key.din, &tin) || !lt_type(key.dout, &tout)) return false;
+  if (hipblasLtMatmulDescCreate(&pl->op, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS)
+    return false;
+  const int32_t ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
+  hipblasLtMatmulDescSetAttribute(pl->op, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta));
+  hipblasLtMatmulDescSetAttribute(pl->op, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb));
+  // column-major: "A" = Bt viewed K x N (ld = ldb), "B" = A viewed K x M (ld = lda), C: N x M
+  if (hipblasLtMatrixLayoutCreate(&pl->la, tin, key.k, key.n, key.ldb) != HIPBLAS_STATUS_SUCCESS ||
+      hipblasLtMatrixLayoutCreate(&pl->lb, tin, key.k, key.m, key.lda) != HIPBLAS_STATUS_SUCCESS ||
+      hipblasLtMatrixLayoutCreate(&pl->lc, tout, key.n, key.m, key.ldc) != HIPBLAS_STATUS_SUCCESS)
+    return false;
+  if (key.batch > 1) {
+    const int32_t b = (int32_t)key.batch;
+    const int64_t s0 = 0, sa = key.sa, sc = key.sc;
+    hipblasLtMatrixLayoutSetAttribute(pl->la, HIPBLASLT_MATRIX_LAYOUT_BATCH_COUNT, &b, sizeof(b));
+    hipblasLtMatrixLayoutSetAttribute(pl->la, HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, &s0,
+                                      sizeof(s0));
+    hipblasLtMatrixLayoutSetAttribute(pl->lb, HIPBLASLT_MATRIX_LAYOUT_BATCH_COUNT, &b, sizeof(b));
+    hipblasLtMatrixLayoutSetAttribute(pl->lb, HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, &sa,
+                                      sizeof(sa));
+    hipblasLtMatrixLayoutSetAttribute(pl->lc, HIPBLASLT_MATRIX_LAYOUT_BATCH_COUNT, &b, sizeof(b));
+    hipblasLtMatrixLayoutSetAttribute(pl->lc, HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, &sc,
+                                      sizeof(sc));
+  }
+  hipblasLtMatmulPreference_t pref = nullptr;
+  if (hipblasLtMatmulPreferenceCreate(&pref) != HIPBLAS_STATUS_SUCCESS) return false;
+  const uint64_t wsb = d->ws_bytes;
+  hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb,
+                                        sizeof(wsb));
+  hipblasLtMatmulHeuristicResult_t res[1];
+  int n = 0;
+  const hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(d->handle, pl->op, pl->la, pl->lb,
+                                                             pl->lc, pl->lc, pref, 1, res, &n);
+  hipblasLtMatmulPreferenceDestroy(pref);
+  if (st != HIPBLAS_STATUS_SUCCESS || n < 1 || res[0].state != HIPBLAS_STATUS_SUCCESS) return false;
+  pl->algo = res[0].algo;
+  pl->ws = res[0].workspaceSize;
+  return pl->ws <= d->ws_bytes;
+}
+
+}  // namespace
+
+bool blaslt_supports(const GemmArgs& p, int din, int dout) {
+  hipDataType t;
+  if (!lt_type(din, &t) || !lt_type(dout, &t)) return false;
+  if (p.flags != nullptr || p.act != ACT_NONE || p.tile_order != 0) return false;
+  if (p.M <= 0 || p.N <= 0 || p.K <= 0) return false;
+  const int64_t ag = p.a_grp > 0 ? p.a_grp : p.M, cg = p.c_grp > 0 ? p.c_grp : p.M;
+  if (ag != cg || p.M % ag != 0) return false;  // one strided batch for A and C
+  return true;
+}
+
+hipError_t blaslt_gemm(const GemmArgs& p, int din, int dout, hipStream_t s) {
+  if (!blaslt_supports(p, din, dout)) return hipErrorNotSupported;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return hipErrorNotSupported;
+  const int64_t grp = p.a_grp > 0 ? p.a_grp : p.M;
+  LtKey key;
+  std::memset(&key, 0, sizeof(key));
+  key.dev = dev; key.din = din; key.dout = dout;
+  key.m = grp; key.n = p.N; key.k = p.K;
+  key.lda = p.lda; key.ldb = p.ldb; key.ldc = p.ldc;
+  key.batch = p.M / grp;
+  key.sa = (p.a_gstride > 0 ? p.a_gstride : grp) * p.lda;
+  key.sc = (p.c_gstride > 0 ? p.c_gstride : grp) * p.ldc;
+  LtDevice* d;
+  LtPlan* pl;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    d = device_state(dev);
+    if (d == nullptr) return hipErrorNotSupported;
+    auto it = g_plans.find(key);
+    if (it == g_plans.end()) {
+      LtPlan fresh;
+      fresh.ok = build_plan(d, key, &fresh);
+      it = g_plans.emplace(key, fresh).first;
+    }
+    pl = &it->second;
+  }
+  if (!pl->ok) return hipErrorNotSupported;
+  const float alpha = 1.f, beta = 0.f;
+  const hipblasStatus_t st =
+      hipblasLtMatmul(d->handle, pl->op, &alpha, p.b, pl->la, p.a, pl->lb, &beta, p.c, pl->lc,
+                      p.c, pl->lc, &pl->algo, d->workspace, pl->ws, s);
+  return st == HIPBLAS_STATUS_SUCCESS ? hipSuccess : hipErrorLaunchFailure;
+}
+
+}  // namespace ddlb

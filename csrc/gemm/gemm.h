@@ -24,7 +24,8 @@ enum Tile : int { TILE_AUTO = 0, TILE_256x256 = 1, TILE_256x128 = 2, TILE_128x25
                   TILE_I256W4 = 12, TILE_PI256 = 13,
                   TILE_PI256W4 = 14,
                   TILE_R256 = 15 };   // R: persistent LDS-ring (3 K-steps in flight)
-enum GemmMode : int { GEMM_MODE_AUTO = 0, GEMM_MODE_GENERIC = 1, GEMM_MODE_MX = 2 };
+enum GemmMode : int { GEMM_MODE_AUTO = 0, GEMM_MODE_GENERIC = 1, GEMM_MODE_MX = 2,
+                      GEMM_MODE_BLAS = 3 };  // BLAS: hipBLASLt for plain GEMMs (blaslt.cpp)
 
 // C[M,N] = A[M,K] * Bt[N,K]^T. Leading dimensions in ELEMENTS.
 // Logical row i of A (and of C) lives at physical row (i / grp) * gstride + (i % grp).
@@ -51,5 +52,8 @@ bool gemm_fast_path_ok(const GemmArgs& p, int din, int dout);
 int choose_tile(int64_t M, int64_t N, int64_t K, int din);
 int tile_rows(int tile);
 int tile_cols(int tile);
+// hipBLASLt backend (csrc/gemm/blaslt.cpp): plain / strided-batched bf16, f16, f32 GEMMs.
+bool blaslt_supports(const GemmArgs& p, int din, int dout);
+hipError_t blaslt_gemm(const GemmArgs& p, int din, int dout, hipStream_t s);
 
 }  // namespace ddlb

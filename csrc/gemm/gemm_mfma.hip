@@ -76,6 +76,11 @@ hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mo
   if (p.a_grp <= 0) { p.a_grp = p.M > 0 ? p.M : 1; p.a_gstride = p.a_grp; }
   if (p.c_grp <= 0) { p.c_grp = p.M > 0 ? p.M : 1; p.c_gstride = p.c_grp; }
   if (p.M == 0 || p.N == 0) return hipSuccess;
+  if (mode == GEMM_MODE_BLAS) {
+    const hipError_t e = blaslt_gemm(p, din, dout, s);
+    if (e != hipErrorNotSupported) return e;
+    mode = GEMM_MODE_AUTO;  // fused / fp8 / ragged-group GEMMs stay on the MFMA kernels
+  }
   const bool fast = mode != GEMM_MODE_GENERIC && gemm_fast_path_ok(p, din, dout);
   if (p.tile_order && !fast) p.tile_order = 0;
   if (fast) {

@@ -36,6 +36,7 @@ SOURCES = [
     "gemm/gemm_mx.hip",
     "gemm/gemm_generic.hip",
     "gemm/gemm_mfma.hip",
+    "gemm/blaslt.cpp",
     "runtime/kernels.hip",
     "comm/comm.cpp",
     "runtime/plan.cpp",
@@ -116,7 +117,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
         return out
     tl = _torch_lib_dir()
     cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", out + ".tmp",
-           f"-L{ROCM}/lib", "-lrccl", "-lamdhip64", f"-Wl,-rpath,{tl}" if tl else "",
+           f"-L{ROCM}/lib", "-lrccl", "-lhipblaslt", "-lamdhip64", f"-Wl,-rpath,{tl}" if tl else "",
            "-Wl,--no-undefined" if False else ""]
     cmd = [c for c in cmd if c]
     if verbose:

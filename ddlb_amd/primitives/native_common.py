@@ -20,7 +20,8 @@ inter_stream_synchronization       serialise the per-peer transfers
 =================================  ===============================================================
 
 Native-only: ``signal`` (``stream`` = hipStreamWrite/WaitValue32 memops, ``kernel`` = tiny spin
-kernels), ``tile`` (GEMM tile or ``auto``), ``gemm_mode`` (``auto`` | ``mx`` for block-scaled fp8),
+kernels), ``tile`` (GEMM tile or ``auto``), ``gemm_mode`` (``auto`` | ``mx`` for block-scaled fp8 |
+``blas`` = hipBLASLt for the plain GEMM ops of the plan, fused ones stay on the MFMA kernels),
 ``copy_blocks`` (CU budget of the kernel protocol), ``fused`` (p2p: one arrival-flag-gated GEMM),
 ``graph`` (capture the plan once and replay it as one hipGraph launch; ``auto`` = whenever the
 plan has no cross-process signals).
@@ -56,7 +57,7 @@ COMMON_ALLOWED = {
     "signal": ["stream", "kernel"],
     "tile": ["auto", "pp256", "256x256", "256x128", "128x256", "128x128", "256x256w4",
              "256x128w4", "p256", "p128", "i256", "i128", "i256w4", "pi256", "pi256w4", "r256"],
-    "gemm_mode": ["auto", "mx", "generic"],
+    "gemm_mode": ["auto", "mx", "generic", "blas"],
     "copy_blocks": (1, 4096),
     "fused": [True, False],
     "graph": [True, False, "auto"],
@@ -69,7 +70,7 @@ COMMON_ALIASES = {
 TILE_CODE = {"auto": 0, "256x256": 1, "256x128": 2, "128x256": 3, "128x128": 4, "pp256": 5,
              "256x256w4": 6, "256x128w4": 7, "p256": 8, "p128": 9, "i256": 10,
              "i128": 11, "i256w4": 12, "pi256": 13, "pi256w4": 14, "r256": 15}
-MODE_CODE = {"auto": 0, "generic": 1, "mx": 2}
+MODE_CODE = {"auto": 0, "generic": 1, "mx": 2, "blas": 3}
 
 
 def algo_config(options, order: str = "AG_before") -> AlgoConfig:

@@ -475,6 +475,206 @@ __global__ __launch_bounds__(512) void ring2_kernel(const Args p) {
   }
 }
 
+// 4-wave variant: 2x2 waves of 128x128 (one wave per SIMD, 256 accumulator registers)
+template <int NS, bool STAMP, int DMAP = 2, int PRIO = 0, int EPI = 1>
+__global__ __launch_bounds__(256) void ring4w_kernel(const Args p) {
+  constexpr int BM = 256, BN = 256, WN = 2, NWAVE = 4;
+  constexpr int ROWB = 64;
+  constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, SLOT = A_BYTES + B_BYTES;
+  constexpr int TM = 128, TN = 128, MR = TM / 16, NR = TN / 16, MH = MR / 2;
+  constexpr int LA = BM / 16 / NWAVE, LB = BN / 16 / NWAVE;
+  constexpr int NDMA = LA + LB;
+  constexpr int NSTORE = MR * NR / 2;  // 16-byte stores
+  static_assert(NS >= 3, "need at least one step in flight beyond the next");
+  __shared__ __attribute__((aligned(1024))) char smem[NS * SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles_n = p.N / BN, tiles_m = p.M / BM, ntiles = tiles_m * tiles_n;
+  const int nk = p.K * 2 / ROWB;
+  const int my_tiles =
+      ((int)blockIdx.x < ntiles) ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int total = my_tiles * nk;
+  if (total == 0) return;
+
+  const int drow = lane >> 2, dchunk = lane & 3;
+  const char* abase[LA];
+  const char* bbase[LB];
+  int dma_tile = -1;
+  auto set_dma_tile = [&](int ti) {
+    const int wg = xcd_remap((int)blockIdx.x + ti * (int)gridDim.x, ntiles);
+    const int64_t m0 = (int64_t)(wg / tiles_n) * BM, n0 = (int64_t)(wg % tiles_n) * BN;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int row = (wave * LA + i) * 16 + drow;
+      abase[i] = (const char*)p.a + (m0 + row) * p.lda * 2 + ((dchunk ^ swz64(row)) * 16);
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int row = (wave * LB + i) * 16 + drow;
+      const int t32 = row & 31;
+      const int gcol = (row & ~31) + 8 * ((t32 & 15) >> 2) + 4 * (t32 >> 4) + (t32 & 3);
+      bbase[i] = (const char*)p.b + (n0 + gcol) * p.ldb * 2 + ((dchunk ^ swz64(row)) * 16);
+    }
+  };
+  auto prep = [&](int g) -> int64_t {
+    g = g < total ? g : total - 1;
+    const int ti = g / nk;
+    if (ti != dma_tile) {
+      set_dma_tile(ti);
+      dma_tile = ti;
+    }
+    return (int64_t)(g - ti * nk) * ROWB;
+  };
+  auto dma = [&](int d, int64_t koff, char* base) {
+    if (d < LA) glds16(abase[d] + koff, base + (wave * LA + d) * 1024);
+    else glds16(bbase[d - LA] + koff, base + A_BYTES + (wave * LB + d - LA) * 1024);
+  };
+
+  const int wm = wave / WN, wn = wave % WN;
+  const int frow = lane & 15, fq = lane >> 4;
+  const int rdoff = frow * ROWB + ((fq ^ swz64(frow)) * 16);
+  const int aoff = wm * TM * ROWB + rdoff, boff = A_BYTES + wn * TN * ROWB + rdoff;
+  f32x4 acc[MR][NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](int i, int j, const i32x4& a, const i32x4& b) {
+    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, b),
+                                                        __builtin_bit_cast(bf16x8, a), acc[i][j],
+                                                        0, 0, 0);
+  };
+
+  unsigned long long t_wait = 0, t_a = 0, t_c = 0, t_epi = 0, t_vm = 0, t0 = 0, t1 = 0;
+  unsigned long long c_start = 0, r_start = 0;
+  if constexpr (STAMP) {
+    c_start = __builtin_readcyclecounter();
+    r_start = __builtin_amdgcn_s_memrealtime();
+  }
+
+  for (int g = 0; g < NS - 1; ++g) {
+    const int64_t koff = prep(g);
+#pragma unroll
+    for (int d = 0; d < NDMA; ++d) dma(d, koff, smem + (g % NS) * SLOT);
+  }
+  wait_vm<NDMA*(NS - 2)>();
+  __builtin_amdgcn_s_barrier();
+  i32x4 A0[MH], A1[MH], Bc[NR], Bn[NR];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) Bc[j] = *(const i32x4*)(smem + boff + j * 16 * ROWB);
+#pragma unroll
+  for (int i = 0; i < MH; ++i) A0[i] = *(const i32x4*)(smem + aoff + i * 16 * ROWB);
+
+  if constexpr (PRIO == 1) {
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 128) __builtin_amdgcn_s_setprio(1);
+  }
+  int stores_window = 0;  // bit j: step g-1-j issued C stores
+  for (int g = 0; g < total; ++g) {
+    if constexpr (STAMP) t0 = __builtin_readcyclecounter();
+    const char* cur = smem + (g % NS) * SLOT;
+    const char* nxt = smem + ((g + 1) % NS) * SLOT;
+    const int64_t koff = prep(g + NS - 1);
+    char* nbase = smem + ((g + NS - 1) % NS) * SLOT;
+    // ---- part A
+    constexpr int DA = NDMA / 2;  // DMAs in part A
+    if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int q = 0; q < MH * NR; ++q) {
+      const int i = q / NR, j = q % NR;
+      mma(i, j, A0[i], Bc[j]);
+      if (q % 8 == 1) dma(q / 8, koff, nbase);
+      if (q % 8 == 5) A1[q / 8] = *(const i32x4*)(cur + aoff + (MH + q / 8) * 16 * ROWB);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    }
+    if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(0);
+    if constexpr (STAMP) { t1 = __builtin_readcyclecounter(); t_a += t1 - t0; t0 = t1; }
+    // ---- wait for step g+1's DMA (ops issued after it: DMA of g+2..g+NS-1, stores of steps
+    //      g-NS+2..g-1), all fragment reads of this slot done, barrier
+    // DMA halves issued in part C of step g-NS+2 are the newest part of DMA(g+1)
+    constexpr int VMB = NDMA * (NS - 2) - (NDMA - DA);
+    const int nst = __builtin_popcount(stores_window);
+    if (nst == 0) wait_vm<VMB>();
+    else if (nst == 1) wait_vm<(VMB + NSTORE < 63 ? VMB + NSTORE : 63)>();
+    else wait_vm<(VMB + 2 * NSTORE < 63 ? VMB + 2 * NSTORE : 63)>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (STAMP) { t1 = __builtin_readcyclecounter(); t_vm += t1 - t0; t0 = t1; }
+    __builtin_amdgcn_s_barrier();
+    if constexpr (STAMP) { t1 = __builtin_readcyclecounter(); t_wait += t1 - t0; t0 = t1; }
+    // ---- part C
+    if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int q = 0; q < MH * NR; ++q) {
+      const int j = q / MH, i = MH + q % MH;  // j-major: Bc[j] is free after its 4 MFMAs
+      mma(i, j, A1[i - MH], Bc[j]);
+      if (q % 4 == 3 && q / 4 < NR) Bn[q / 4] = *(const i32x4*)(nxt + boff + (q / 4) * 16 * ROWB);
+      if (q % 8 == 1) A0[q / 8] = *(const i32x4*)(nxt + aoff + (q / 8) * 16 * ROWB);
+      if (q % 8 == 5) dma(DA + q / 8, koff, nbase);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+    for (int j = 0; j < NR; ++j) Bc[j] = Bn[j];
+
+    const int ti = g / nk;
+    const bool last_k = (g - ti * nk) == nk - 1;
+    stores_window = (stores_window << 1) & ((1 << (NS - 2)) - 1);
+    if (last_k) {
+      const int wg = xcd_remap((int)blockIdx.x + ti * (int)gridDim.x, ntiles);
+      const int64_t m0 = (int64_t)(wg / tiles_n) * BM, n0 = (int64_t)(wg % tiles_n) * BN;
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < MR; ++i) {
+        char* crow = (char*)p.c + (m0 + wm * TM + i * 16 + frow) * p.ldc * 2;
+#pragma unroll
+        for (int jp = 0; jp < NR / 2; ++jp) {
+          const int64_t col = n0 + wn * TN + jp * 32 + fq * 8;
+          const f32x4 v0 = acc[i][2 * jp], v1 = acc[i][2 * jp + 1];
+          typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8o;
+          bf16x8o o = {(__bf16)v0.x, (__bf16)v0.y, (__bf16)v0.z, (__bf16)v0.w,
+                       (__bf16)v1.x, (__bf16)v1.y, (__bf16)v1.z, (__bf16)v1.w};
+          if (EPI == 3) __builtin_nontemporal_store(__builtin_bit_cast(i32x4, o), (i32x4*)(crow + col * 2));
+          else if (EPI == 1 || p.M < 0) *(uint4*)(crow + col * 2) = __builtin_bit_cast(uint4, o);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      __builtin_amdgcn_sched_barrier(0);
+      stores_window |= 1;
+      if constexpr (STAMP) { t1 = __builtin_readcyclecounter(); t_epi += t1 - t0; t0 = t1; }
+    }
+  }
+  wait_vm<0>();
+  if constexpr (STAMP) {
+    if (lane == 0 && blockIdx.x == 0 && wave == 0) {
+      p.stamps[(size_t)gridDim.x * 8 * 5 + 1] = __builtin_readcyclecounter() - c_start;
+      p.stamps[(size_t)gridDim.x * 8 * 5 + 3] = __builtin_amdgcn_s_memrealtime() - r_start;
+    }
+    if (lane == 0) {
+      unsigned long long* s = p.stamps + ((size_t)blockIdx.x * 8 + wave) * 5;
+      s[0] = t_wait; s[1] = t_a; s[2] = t_c; s[3] = t_epi; s[4] = t_vm;
+    }
+  }
+}
+
 // fp32 reference: C[m][n] = sum_k A[m][k] * B[n][k]
 __global__ void ref_kernel(const __hip_bfloat16* A, const __hip_bfloat16* B, float* C, int M, int N,
                            int K) {
@@ -516,6 +716,7 @@ struct Variant {
   const char* name;
   KFn fn;
   int ns;
+  int threads;
 };
 
 int main(int argc, char** argv) {
@@ -543,13 +744,10 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&stamps, ((size_t)grid * 8 * 5 + 8) * 8));
 
   Variant vs[] = {
-      {"ring2 ns4", ring2_kernel<4, false>, 4},
-      {"ring2 dmaAC", ring2_kernel<4, false, 2>, 4},
-      {"ring2 ns3 dmaAC", ring2_kernel<3, false, 2>, 3},
-      {"ring2 ns5 dmaAC", ring2_kernel<5, false, 2>, 5},
-      {"ring2 dmaAC noprio", ring2_kernel<4, false, 2, 2>, 4},
-      {"ring2 dmaAC nt", ring2_kernel<4, false, 2, 0, 3>, 4},
-      {"ring2 dmaAC nost", ring2_kernel<4, false, 2, 0, 2>, 4},
+      {"ring2 dmaAC", ring2_kernel<4, false, 2>, 4, 512},
+      {"ring4w", ring4w_kernel<4, false>, 4, 256},
+      {"ring4w ns3", ring4w_kernel<3, false>, 3, 256},
+      {"ring4w nost", ring4w_kernel<4, false, 2, 0, 2>, 4, 256},
   };
   Args a{A, B, C, K, K, N, M, N, K, nullptr};
   const double flop = 2.0 * M * N * K;
@@ -560,7 +758,7 @@ int main(int argc, char** argv) {
   for (size_t v = 0; v < sizeof(vs) / sizeof(vs[0]); ++v) {
     CHECK(hipMemset(C, 0, (size_t)M * N * 2));
     CHECK(hipMemset(err, 0, 4));
-    hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(512), 0, 0, a);
+    hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(vs[v].threads), 0, 0, a);
     CHECK(hipGetLastError());
     cmp_kernel<<<1024, 256>>>(C, R, (size_t)M * N, err);
     float e = 0;
@@ -569,9 +767,9 @@ int main(int argc, char** argv) {
   }
   for (int r = 0; r < rounds; ++r)
     for (size_t v = 0; v < sizeof(vs) / sizeof(vs[0]); ++v) {
-      for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(512), 0, 0, a);
+      for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(vs[v].threads), 0, 0, a);
       CHECK(hipEventRecord(e0));
-      for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(512), 0, 0, a);
+      for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(vs[v].threads), 0, 0, a);
       CHECK(hipEventRecord(e1));
       CHECK(hipEventSynchronize(e1));
       float ms;

@@ -49,6 +49,19 @@ def test_native_world1(comm, alg, backend, dtype):
         impl.close()
 
 
+@pytest.mark.parametrize("alg", ["default", "coll_pipeline", "p2p_pipeline"])
+def test_native_blas_world1(comm, alg):
+    from ddlb_amd.primitives.tp_columnwise.native import NativeTPColumnwise
+    from ddlb_amd.primitives.tp_rowwise.native import NativeTPRowwise
+
+    for cls in (NativeTPColumnwise, NativeTPRowwise):
+        impl = cls(m=2048, n=512, k=512, dtype="bfloat16", algorithm=alg, s=2, gemm_mode="blas")
+        out = impl.run()
+        torch.cuda.synchronize()
+        impl.validate(out)
+        impl.close()
+
+
 def test_native_fp8_mx_world1(comm):
     from ddlb_amd.primitives.tp_columnwise.native import NativeTPColumnwise
 
