@@ -50,6 +50,7 @@ _DEF_K = dict(algorithm="default", backend="ipc", multicast_protocol="kernel", c
 CANDIDATES = [
     ("coll_pipeline/rccl/s4", "native", _COLL4),
     ("coll_pipeline/rccl/s4/blas", "native", _blas(_COLL4)),
+    ("direct/ipc", "native", dict(algorithm="direct", backend="ipc")),
     ("default/rccl", "native", _DEF),
     ("default/rccl/blas", "native", _blas(_DEF)),
     ("p2p_pipeline/ipc/memcpy", "native", _P2P),

@@ -128,7 +128,7 @@ bool build_plan(LtDevice* d, const LtKey& key, LtPlan* pl) {
 bool blaslt_supports(const GemmArgs& p, int din, int dout) {
   hipDataType t;
   if (!lt_type(din, &t) || !lt_type(dout, &t)) return false;
-  if (p.flags != nullptr || p.act != ACT_NONE || p.tile_order != 0) return false;
+  if (p.flags != nullptr || p.act != ACT_NONE || p.tile_order != 0 || p.a_table) return false;
   if (p.M <= 0 || p.N <= 0 || p.K <= 0) return false;
   const int64_t ag = p.a_grp > 0 ? p.a_grp : p.M, cg = p.c_grp > 0 ? p.c_grp : p.M;
   if (ag != cg || p.M % ag != 0) return false;  // one strided batch for A and C

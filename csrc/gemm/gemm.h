@@ -44,6 +44,10 @@ struct GemmArgs {
   unsigned* timeout_word = nullptr; // set to 1 if a spin gave up
   int tile_order = 0, nshards = 1, first_shard = 0;
   int act = 0;                      // fused epilogue activation: ACT_* below
+  // Direct-access A (optional): row block s of shard_rows rows starts at a_table[s] (device
+  // array of addresses, e.g. the peers' IPC-mapped shards read straight over xGMI).
+  const uint64_t* a_table = nullptr;
+  int64_t shard_rows = 0;
 };
 enum Act : int { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_SILU = 3 };
 

@@ -32,6 +32,16 @@ __device__ __forceinline__ int64_t map_row(int64_t i, int64_t grp, int64_t gstri
   return (int64_t)q * gstride + (int64_t)(ui - q * ug);
 }
 
+// Address of logical A row ``row``: grouped rows, or a per-shard pointer table (direct access).
+__device__ __forceinline__ const char* a_row(const GemmArgs& p, int64_t row, int esz) {
+  if (p.a_table != nullptr) {
+    const unsigned ur = (unsigned)row, us = (unsigned)p.shard_rows;
+    const unsigned sh = ur / us;
+    return (const char*)p.a_table[sh] + (int64_t)(ur - sh * us) * p.lda * esz;
+  }
+  return (const char*)p.a + map_row(row, p.a_grp, p.a_gstride) * p.lda * esz;
+}
+
 // Bijective XCD remap (guide §5, "XCD swizzle must be bijective").
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, idx = bid >> 3;
@@ -198,9 +208,8 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_kernel(const GemmArgs p) 
     const int row = (wave * LA + i) * 8 + (lane >> 3);
     int64_t gr = m0 + row;
     gr = gr < p.M ? gr : p.M - 1;
-    const int64_t phys = map_row(gr, p.a_grp, p.a_gstride);
     const int chunk = (lane & 7) ^ ((row >> 1) & 7);
-    aptr[i] = (const char*)p.a + phys * p.lda * esz + chunk * 16;
+    aptr[i] = a_row(p, gr, esz) + chunk * 16;
   }
 #pragma unroll
   for (int i = 0; i < LB; ++i) {
@@ -611,8 +620,7 @@ __global__ __launch_bounds__(512) void gemm_tn_ring_kernel(const GemmArgs p) {
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const int row = (wave * LA + i) * 16 + drow;
-      abase[i] = (const char*)p.a + map_row(m0 + row, p.a_grp, p.a_gstride) * p.lda * esz +
-                 ((dchunk ^ swz64(row)) * 16);
+      abase[i] = a_row(p, m0 + row, esz) + ((dchunk ^ swz64(row)) * 16);
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {

@@ -76,6 +76,18 @@ hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mo
   if (p.a_grp <= 0) { p.a_grp = p.M > 0 ? p.M : 1; p.a_gstride = p.a_grp; }
   if (p.c_grp <= 0) { p.c_grp = p.M > 0 ? p.M : 1; p.c_gstride = p.c_grp; }
   if (p.M == 0 || p.N == 0) return hipSuccess;
+  if (p.a_table != nullptr) {
+    // direct-access A: only the tiled and ring kernels read A through the shard table
+    if (p.shard_rows <= 0 || p.flags != nullptr) return hipErrorInvalidValue;
+    if (mode == GEMM_MODE_BLAS || mode == GEMM_MODE_MX) mode = GEMM_MODE_AUTO;
+    if (tile == TILE_PP256 || tile == TILE_P256 || tile == TILE_PI256 || tile == TILE_PI256W4)
+      tile = TILE_I256;
+    if (tile == TILE_P128) tile = TILE_I128;
+    if (tile == TILE_AUTO || tile == TILE_R256)
+      tile = (p.M % 256 == 0 && p.N % 256 == 0 && p.shard_rows % 256 == 0) ? TILE_R256
+                                                                              : TILE_128x128;
+    if (mode == GEMM_MODE_GENERIC || !gemm_fast_path_ok(p, din, dout)) return hipErrorNotSupported;
+  }
   if (mode == GEMM_MODE_BLAS) {
     const hipError_t e = blaslt_gemm(p, din, dout, s);
     if (e != hipErrorNotSupported) return e;

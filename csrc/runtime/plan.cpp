@@ -157,6 +157,8 @@ void PlanExecutor::exec(const int64_t* o, hipStream_t main) {
       g.first_shard = (int)o[22];
       g.tile_order = (int)o[23];
       g.act = (int)o[24];
+      g.a_table = (const uint64_t*)o[25];
+      g.shard_rows = o[26];
       g.timeout_word = d_timeout_;
       DDLB_HIP(gemm_launch(g, (int)o[15], (int)o[16], (int)o[17], (int)o[18], s));
       return;

@@ -138,10 +138,12 @@ def check_columnwise(d: int, m: int, n: int, k: int, cfg: AlgoConfig) -> None:
     if cfg.algorithm == "coll_pipeline" and m % (d * cfg.s):
         raise ValueError(f"m ({m}) must be divisible by s*world_size ({cfg.s}*{d}) for "
                          "coll_pipeline")
-    if cfg.algorithm not in ("default", "coll_pipeline", "p2p_pipeline"):
+    if cfg.algorithm not in ("default", "coll_pipeline", "p2p_pipeline", "direct"):
         raise ValueError(f"unknown algorithm {cfg.algorithm}")
     if cfg.backend not in ("rccl", "ipc"):
         raise ValueError(f"unknown backend {cfg.backend}")
+    if cfg.algorithm == "direct" and (cfg.backend != "ipc" or cfg.order != "AG_before"):
+        raise ValueError("algorithm=direct reads peer shards over xGMI: backend=ipc, AG_before")
     if cfg.protocol not in ("memcpy", "batch_memcpy", "kernel"):
         raise ValueError(f"unknown protocol {cfg.protocol}")
     if d > 17:
@@ -156,14 +158,21 @@ def build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, dou
     plan = Plan(rank, d, nstreams=_nstreams(d), stream_priority=[0, 1] + [1] * max(d - 1, 1))
     plan.meta.update(primitive="tp_columnwise", algorithm=cfg.algorithm, backend=cfg.backend,
                      order=cfg.order)
-    A = plan.buffer("A_full", m * k * ein, symmetric=(cfg.backend == "ipc"))
     Bt = plan.buffer("Bt", n * k * ein)
-    flags = _Flags(plan, d, max(cfg.s, 1)) if cfg.backend == "ipc" and d > 1 else None
+    A = (plan.buffer("A_full", m * k * ein, symmetric=(cfg.backend == "ipc"))
+         if cfg.algorithm != "direct" else None)
+    flags = (_Flags(plan, d, max(cfg.s, 1))
+             if cfg.backend == "ipc" and d > 1 and cfg.algorithm != "direct" else None)
     gdt = dict(din=din, dout=dout, tile=cfg.tile, mode=cfg.mode, act=cfg.act)
     comm_dt = DT_U8 if ein == 1 else din   # fp8 moves as bytes
 
     def arow(r0: int) -> Ref:
         return A + r0 * k * ein
+
+    if cfg.algorithm == "direct":
+        return _col_direct(plan, rank, d, m, n, k, din, dout, ein, eout, cfg, gdt), \
+            PlanIO(TensorLoc("A_own", 0, ml, k, din), TensorLoc("Bt", 0, n, k, din),
+                   TensorLoc("C", 0, m, n, dout))
 
     if cfg.order == "AG_after":
         C = plan.buffer("C_full", m * n * eout, symmetric=(cfg.backend == "ipc"))
@@ -254,6 +263,32 @@ def build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, dou
     else:  # pragma: no cover
         raise ValueError(f"unsupported combination {alg}/{be}")
     return plan, io
+
+
+def _col_direct(plan, rank, d, m, n, k, din, dout, ein, eout, cfg, gdt) -> Plan:
+    """Direct-access AG+GEMM: no all-gather at all. Every rank keeps only its own shard in a
+    symmetric buffer; ONE GEMM launch reads row block p straight from rank p's HBM over xGMI
+    (IPC-mapped pointers in a per-shard address table, LDS-DMA from peer memory), so the
+    transfer is spread over all d-1 links at once and fully overlapped with the MFMA work, and
+    no [m, k] gather buffer is written or read locally. READY: my shard is in place for this
+    epoch; ACK: I finished reading yours (the owner may overwrite it afterwards)."""
+    ml = m // d
+    A_own = plan.buffer("A_own", ml * k * ein, symmetric=True)
+    C = plan.buffer("C", m * n * eout)
+    Bt = Ref("Bt")
+    if d == 1:
+        plan.gemm(S_MAIN, A_own, Bt, C, M=m, N=n, K=k, lda=k, ldb=k, ldc=n, **gdt)
+        return plan
+    flags = _Flags(plan, d, 1)
+    peers = [p for p in range(d) if p != rank]
+    _signal(plan, S_MAIN, [flags.ref("READY", rank, owner=p) for p in peers], cfg)
+    _wait(plan, S_MAIN, [flags.ref("READY", p) for p in peers], cfg)
+    shards = [A_own.at(None if p == rank else p) for p in range(d)]
+    plan.gemm(S_MAIN, A_own, Bt, C, M=m, N=n, K=k, lda=k, ldb=k, ldc=n, a_shards=shards,
+              shard_rows=ml, **gdt)
+    _signal(plan, S_MAIN, [flags.ref("ACK", rank, owner=p) for p in peers], cfg)
+    _wait(plan, S_MAIN, [flags.ref("ACK", p) for p in peers], cfg)
+    return plan
 
 
 def _ipc_pull_shards(plan: Plan, rank: int, d: int, cfg: AlgoConfig, flags: _Flags,
@@ -372,7 +407,7 @@ def check_rowwise(d: int, m: int, n: int, k: int, cfg: AlgoConfig) -> None:
     if cfg.algorithm == "coll_pipeline" and m % (d * cfg.s):
         raise ValueError(f"m ({m}) must be divisible by s*world_size ({cfg.s}*{d})")
     if cfg.algorithm not in ("default", "coll_pipeline", "p2p_pipeline"):
-        raise ValueError(f"unknown algorithm {cfg.algorithm}")
+        raise ValueError(f"unknown algorithm {cfg.algorithm} for tp_rowwise")
     if cfg.backend not in ("rccl", "ipc"):
         raise ValueError(f"unknown backend {cfg.backend}")
     if d > 16:

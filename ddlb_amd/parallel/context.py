@@ -152,6 +152,10 @@ class BoundPlan:
                                                device=dev)
         if externals:
             raise ValueError(f"externals {sorted(externals)} are not buffers of this plan")
+        for name, spec in plan.buffers.items():
+            if spec.table is not None:
+                addrs = torch.tensor([self.resolve(r) for r in spec.table], dtype=torch.int64)
+                self.local[name][:8 * len(spec.table)].copy_(addrs.view(torch.uint8))
         words = plan.encode(self.resolve)
         C = ctx.C
         self.ex = C.PlanExecutor(ctx.device_index, plan.nstreams, max(plan.nevents, 1),

@@ -64,6 +64,7 @@ class BufferSpec:
     nbytes: int
     symmetric: bool = False
     zero: bool = False          # must start zeroed (flags)
+    table: Optional[List[Ref]] = None  # pointer table: filled with the refs' addresses at bind
 
 
 @dataclass
@@ -117,12 +118,27 @@ class Plan:
              ldb: int, ldc: int, din: int, dout: int, a_grp: int = 0, a_gstride: int = 0,
              c_grp: int = 0, c_gstride: int = 0, tile: int = 0, mode: int = 0,
              flags: Optional[Ref] = None, flag_rows: int = 0, nshards: int = 1,
-             first_shard: int = 0, tile_order: int = 0, act: int = 0) -> Op:
+             first_shard: int = 0, tile_order: int = 0, act: int = 0,
+             a_shards: Optional[Sequence[Ref]] = None, shard_rows: int = 0) -> Op:
+        """``a_shards``: A row block s (``shard_rows`` rows each) is read from ``a_shards[s]``
+        (a peer's copy for a direct-access GEMM that pulls its operand over xGMI)."""
+        a_table = None
+        if a_shards is not None:
+            if shard_rows <= 0 or len(a_shards) * shard_rows < M:
+                raise ValueError("a_shards must cover the M rows")
+            a_table = self.table(f"__atab{len(self.buffers)}", a_shards)
         return self._add(OP_GEMM, stream, a=a, b=b, c=c, M=M, N=N, K=K, lda=lda, ldb=ldb, ldc=ldc,
                          din=din, dout=dout, a_grp=a_grp, a_gstride=a_gstride, c_grp=c_grp,
                          c_gstride=c_gstride, tile=tile, mode=mode, flags=flags,
                          flag_rows=flag_rows, nshards=nshards, first_shard=first_shard,
-                         tile_order=tile_order, act=act)
+                         tile_order=tile_order, act=act,
+                         a_shards=list(a_shards) if a_shards is not None else None,
+                         shard_rows=shard_rows, a_table=a_table)
+
+    def table(self, name: str, refs: Sequence[Ref]) -> Ref:
+        """Device array of 64-bit addresses of ``refs`` (written once when the plan is bound)."""
+        self.buffers[name] = BufferSpec(name, max(16, 8 * len(refs)), table=list(refs))
+        return Ref(name, 0, None)
 
     def record(self, stream: int, event: int) -> Op:
         return self._add(OP_RECORD, stream, event=event)
@@ -203,6 +219,8 @@ class Plan:
                 w[19] = resolve(a["flags"]) if a["flags"] is not None else 0
                 w[20:25] = [a["flag_rows"], a["nshards"], a["first_shard"], a["tile_order"],
                             a.get("act", 0)]
+                if a.get("a_table") is not None:
+                    w[25], w[26] = resolve(a["a_table"]), a["shard_rows"]
             elif k in (OP_RECORD, OP_WAIT):
                 w[2] = a["event"]
             elif k in (OP_ALLGATHER, OP_REDUCE_SCATTER):

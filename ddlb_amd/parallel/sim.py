@@ -157,15 +157,30 @@ class Simulator:
         what = f"r{r}.s{op.stream}.{OP_NAMES[k]}"
         if k == OP_GEMM:
             ein, eout = DT_SIZE[a["din"]], DT_SIZE[a["dout"]]
-            for ref, nb in self._rows(a["a"], a["M"], a["a_grp"], a["a_gstride"], a["lda"],
-                                      a["K"], ein):
-                self._touch(r, ref, nb, False, vc, what + ".A")
+            shards = a.get("a_shards")
+            if shards is not None:  # direct-access GEMM: row block s read from a_shards[s]
+                R, parts = a["shard_rows"], []
+                for sidx, ref in enumerate(shards):
+                    rows = min(R, a["M"] - sidx * R)
+                    if rows <= 0:
+                        break
+                    span = (rows - 1) * a["lda"] + a["K"]
+                    self._touch(r, ref, span * ein, False, vc, what + f".A{sidx}")
+                    parts.append(_view(self._buf(r, ref), ref.off, span, a["din"]).as_strided(
+                        (rows, a["K"]), (a["lda"], 1)).float())
+                A_shards = torch.cat(parts)
+            else:
+                A_shards = None
+                for ref, nb in self._rows(a["a"], a["M"], a["a_grp"], a["a_gstride"], a["lda"],
+                                          a["K"], ein):
+                    self._touch(r, ref, nb, False, vc, what + ".A")
             self._touch(r, a["b"], ((a["N"] - 1) * a["ldb"] + a["K"]) * ein, False, vc, what + ".B")
             for ref, nb in self._rows(a["c"], a["M"], a["c_grp"], a["c_gstride"], a["ldc"],
                                       a["N"], eout):
                 self._touch(r, ref, nb, True, vc, what + ".C")
-            A = self._gather_rows(self._buf(r, a["a"]), a["a"].off, a["M"], a["a_grp"],
-                                  a["a_gstride"], a["lda"], a["K"], a["din"]).float()
+            A = A_shards if A_shards is not None else self._gather_rows(
+                self._buf(r, a["a"]), a["a"].off, a["M"], a["a_grp"], a["a_gstride"], a["lda"],
+                a["K"], a["din"]).float()
             Bt = _view(self._buf(r, a["b"]), a["b"].off, (a["N"] - 1) * a["ldb"] + a["K"],
                        a["din"]).as_strided((a["N"], a["K"]), (a["ldb"], 1)).float()
             Cv = apply_act(A @ Bt.t(), a.get("act", 0))

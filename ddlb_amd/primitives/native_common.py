@@ -49,7 +49,7 @@ COMMON_DEFAULTS = {
 }
 COMMON_ALLOWED = {
     "backend": ["rccl", "ipc", *UCC_BACKENDS],
-    "algorithm": ["default", "coll_pipeline", "p2p_pipeline"],
+    "algorithm": ["default", "coll_pipeline", "p2p_pipeline", "direct"],
     "s": (1, 1 << 20),
     "offset_stream_indexing_by_rank": [True, False],
     "multicast_protocol": ["memcpy", "batch_memcpy", "kernel"],

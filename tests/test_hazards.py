@@ -129,3 +129,37 @@ def test_explain_cli_simulates(capsys):
           "--algorithm", "p2p_pipeline", "--backend", "ipc", "--dtype", "float32", "--simulate"])
     out = capsys.readouterr().out
     assert "no race, no deadlock, max|err| = 0.0" in out
+
+
+def _direct_with_producer(drop_ack: bool):
+    """Direct-access plans preceded by a producer that rewrites the own shard every run."""
+    from ddlb_amd.parallel.algorithms import AlgoConfig, build_tp_columnwise
+    from ddlb_amd.parallel.plan import OP_COPY, OP_WAIT_SIGNAL, Op, Ref
+
+    d, m, n, k = 2, 16, 8, 8
+    plans = []
+    for r in range(d):
+        plan, io = build_tp_columnwise(r, d, m, n, k, DT_F32, DT_F32,
+                                       AlgoConfig(algorithm="direct", backend="ipc"))
+        nb = (m // d) * k * 4
+        plan.buffer("A_in", nb)
+        plan.ops.insert(0, Op(OP_COPY, 0, dict(dst=Ref("A_own"), src=Ref("A_in"), nbytes=nb,
+                                               method=0, max_blocks=0)))
+        if drop_ack:
+            last = max(i for i, op in enumerate(plan.ops) if op.kind == OP_WAIT_SIGNAL)
+            del plan.ops[last]
+        plans.append(plan)
+    return Simulator(plans, make_buffers(plans))
+
+
+def test_direct_access_ack_protects_next_write():
+    sim = _direct_with_producer(drop_ack=False)
+    for _ in range(3):
+        sim.run_epoch()
+
+
+def test_direct_access_without_ack_is_a_race():
+    sim = _direct_with_producer(drop_ack=True)
+    with pytest.raises((RaceDetected, Deadlock)):
+        for _ in range(3):
+            sim.run_epoch()

@@ -62,6 +62,19 @@ def test_native_blas_world1(comm, alg):
         impl.close()
 
 
+@pytest.mark.parametrize("dtype", ["bfloat16", "float8_e4m3fn", "float32"])
+def test_native_direct_world1(comm, dtype):
+    from ddlb_amd.primitives.tp_columnwise.native import NativeTPColumnwise
+
+    impl = NativeTPColumnwise(m=2048, n=512, k=512, dtype=dtype, algorithm="direct",
+                              backend="ipc")
+    for _ in range(2):
+        out = impl.run()
+    torch.cuda.synchronize()
+    impl.validate(out)
+    impl.close()
+
+
 def test_native_fp8_mx_world1(comm):
     from ddlb_amd.primitives.tp_columnwise.native import NativeTPColumnwise
 
@@ -106,6 +119,11 @@ def _ipc_cfgs():
                                                offset_stream_indexing_by_rank=False)))
     cfgs.append(("col/p2p/fp8", "col", dict(algorithm="p2p_pipeline", backend="ipc",
                                             dtype="float8_e4m3fn")))
+    for sig in ("stream", "kernel"):
+        cfgs.append((f"col/direct/{sig}", "col", dict(algorithm="direct", backend="ipc",
+                                                      signal=sig)))
+    cfgs.append(("col/direct/128", "col", dict(algorithm="direct", backend="ipc",
+                                               tile="128x128")))
     return cfgs
 
 

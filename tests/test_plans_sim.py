@@ -92,6 +92,22 @@ def test_p2p_fused_plan(fused):
     _run_col(4, m=32, n=8, k=8, cfg=cfg)
 
 
+@pytest.mark.parametrize("d", [1, 2, 3, 4])
+@pytest.mark.parametrize("sig", [SIG_STREAM, SIG_KERNEL])
+def test_direct_access_plans(d, sig):
+    """algorithm=direct: one GEMM reading every peer's shard in place (no gather buffer)."""
+    cfg = AlgoConfig(algorithm="direct", backend="ipc", signal=sig)
+    _run_col(d, m=12 * d, n=8, k=8, cfg=cfg)
+
+
+def test_direct_access_rejects_bad_configs():
+    with pytest.raises(ValueError):
+        build_tp_columnwise(0, 2, 16, 8, 8, DT_F32, DT_F32, AlgoConfig(algorithm="direct"))
+    with pytest.raises(ValueError):
+        build_tp_rowwise(0, 2, 16, 8, 8, DT_F32, DT_F32,
+                         AlgoConfig(algorithm="direct", backend="ipc"))
+
+
 def test_bf16_plans_round_like_hardware():
     cfg = AlgoConfig(algorithm="coll_pipeline", backend="rccl", s=2)
     _run_col(2, m=16, n=8, k=8, cfg=cfg, dt=DT_BF16)
