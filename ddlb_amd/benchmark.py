@@ -29,8 +29,8 @@ import traceback
 from typing import Any, Dict, List, Optional
 
 from ddlb_amd.envs import get_master_addr, get_master_port, get_rank, get_world_size
-from ddlb_amd.utils.stats import CSV_COLUMNS, EXTRA_COLUMNS, impl_label, option_string, \
-    order_row, summarize
+from ddlb_amd.utils.stats import CSV_COLUMNS, EXTRA_COLUMNS, derived_metrics, impl_label, \
+    option_string, order_row, summarize
 
 
 def _spec_key(impl_opts: Dict[str, Any]) -> str:
@@ -149,6 +149,8 @@ def run_single(primitive: str, impl_id: str, m: int, n: int, k: int, dtype: str,
         comm.all_reduce_max(t)
         times = t.cpu().tolist()
         row.update(summarize(times, m, n, k))
+        row.update(derived_metrics(primitive, base, str(opts_used.get("size", "")), m, n, k, dtype,
+                                   get_world_size(), row["mean_time (ms)"]))
         if validate and last is not None:
             try:
                 impl.validate(last)

@@ -21,7 +21,7 @@ CSV_COLUMNS: List[str] = [
     "dtype", "Throughput (TFLOPS)", "Throughput std (TFLOPS)", "world_size", "hostname",
     "time_measurement_backend", "barrier_at_each_iteration", "option", "valid",
 ]
-EXTRA_COLUMNS: List[str] = ["gpu_arch", "error"]
+EXTRA_COLUMNS: List[str] = ["per_gpu_tflops", "algbw_GBps", "gpu_arch", "error"]
 
 SUMMARY_COLUMNS = ["m", "n", "k", "config", "Throughput (TFLOPS)", "Throughput std (TFLOPS)",
                    "mean_time (ms)", "std_time", "min_time", "max_time"]
@@ -39,6 +39,38 @@ def summarize(times_ms: Sequence[float], m: int, n: int, k: int) -> Dict[str, fl
         "Throughput (TFLOPS)": float(thr.mean()) if thr.size else 0.0,
         "Throughput std (TFLOPS)": float(thr.std()) if thr.size else 0.0,
     }
+
+
+_ESZ = {"float32": 4, "float16": 2, "bfloat16": 2, "float8_e4m3fn": 1, "float64": 8,
+        "int32": 4, "int64": 8}
+
+
+def derived_metrics(primitive: str, base_impl: str, size: str, m: int, n: int, k: int,
+                    dtype: str, world: int, mean_ms: float) -> Dict[str, float]:
+    """Append-only extras that undo the harness formula's per-primitive meaning:
+
+    * ``per_gpu_tflops``: tp_columnwise's harness number already is per GPU (every rank does
+      2mnk); tp_rowwise's and sharded compute_only's are aggregates, so they are divided by d.
+    * ``algbw_GBps``: collective payload / time, NCCL's "algorithm bandwidth" convention — the
+      gathered [m, k] input for tp_columnwise, the reduce-scattered [m, n] output for
+      tp_rowwise; 0 for compute_only.
+    """
+    if mean_ms <= 0:
+        return {"per_gpu_tflops": 0.0, "algbw_GBps": 0.0}
+    d = max(int(world), 1)
+    tflops = 2.0 * m * n * k / (mean_ms * 1e9)
+    esz = _ESZ.get(dtype, 2)
+    if base_impl == "compute_only":
+        per_gpu = tflops / d if size == "sharded" else tflops
+        payload = 0
+    elif primitive == "tp_rowwise":
+        per_gpu = tflops / d
+        payload = m * n * (2 if esz == 1 else esz)  # fp8 GEMMs emit bf16
+    else:
+        per_gpu = tflops
+        payload = m * k * esz
+    return {"per_gpu_tflops": per_gpu,
+            "algbw_GBps": (payload / (mean_ms * 1e-3) / 1e9) if d > 1 else 0.0}
 
 
 def impl_label(base_impl: str, options: Dict, default_keys: Sequence[str]) -> str:

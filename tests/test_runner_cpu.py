@@ -133,3 +133,20 @@ def test_json_script_entry(tmp_path):
                        cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "Benchmark Results" in r.stdout
+
+
+def test_derived_metrics_undo_the_harness_formula():
+    from ddlb_amd.utils.stats import derived_metrics
+
+    m, n, k, d, ms = 4096, 1024, 2048, 4, 2.0
+    harness = 2.0 * m * n * k / (ms * 1e9)
+    col = derived_metrics("tp_columnwise", "native", "", m, n, k, "bfloat16", d, ms)
+    assert col["per_gpu_tflops"] == pytest.approx(harness)
+    assert col["algbw_GBps"] == pytest.approx(m * k * 2 / (ms * 1e-3) / 1e9)
+    row = derived_metrics("tp_rowwise", "native", "", m, n, k, "bfloat16", d, ms)
+    assert row["per_gpu_tflops"] == pytest.approx(harness / d)
+    assert row["algbw_GBps"] == pytest.approx(m * n * 2 / (ms * 1e-3) / 1e9)
+    sh = derived_metrics("tp_columnwise", "compute_only", "sharded", m, n, k, "float32", d, ms)
+    assert sh["per_gpu_tflops"] == pytest.approx(harness / d) and sh["algbw_GBps"] == 0
+    assert derived_metrics("tp_columnwise", "native", "", m, n, k, "bfloat16", 1, ms)[
+        "algbw_GBps"] == 0
