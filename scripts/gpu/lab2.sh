@@ -1,5 +1,5 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-timeout -k 10 120 scripts/lab/bin/gemm_lab 65536 1024 1024 > gpurun_out/lab5_a.log 2>&1; rc=$?; cat gpurun_out/lab5_a.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python scripts/bench_gemm.py --tiles pi256 --shapes 0 > gpurun_out/lab5_ref.log 2>&1; grep -v amdgpu.ids gpurun_out/lab5_ref.log
+timeout -k 10 120 scripts/lab/bin/gemm_lab 65536 1024 1024 > gpurun_out/lab7_a.log 2>&1; rc=$?; cat gpurun_out/lab7_a.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python scripts/bench_gemm.py --tiles pi256 --shapes 0 > gpurun_out/lab7_ref.log 2>&1; grep -v amdgpu.ids gpurun_out/lab7_ref.log

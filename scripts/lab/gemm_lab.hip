@@ -251,7 +251,7 @@ __global__ __launch_bounds__(512) void ring_kernel(const Args p) {
 //   part A: MFMAs rows 0-3 (A0 x Bc) + DMA of step g+NS-1 + reads of A1 (rows 4-7, step g)
 //   wait DMA(g+1); lgkmcnt(0); barrier
 //   part C: MFMAs rows 4-7 (A1 x Bc) + reads of A0 and Bn for step g+1
-template <int NS, bool STAMP, int DMAP = 0, int PRIO = 0, int EPI = 1>
+template <int NS, bool STAMP, int DMAP = 0, int PRIO = 0, int EPI = 1, int SKIP = 0>
 __global__ __launch_bounds__(512) void ring2_kernel(const Args p) {
   constexpr int BM = 256, BN = 256, WN = 4;
   constexpr int ROWB = 64;
@@ -272,6 +272,7 @@ __global__ __launch_bounds__(512) void ring2_kernel(const Args p) {
   if (total == 0) return;
 
   const int drow = lane >> 2, dchunk = lane & 3;
+  bool g_loop_started = false;
   const char* abase[LA];
   const char* bbase[LB];
   int dma_tile = -1;
@@ -301,6 +302,9 @@ __global__ __launch_bounds__(512) void ring2_kernel(const Args p) {
     return (int64_t)(g - ti * nk) * ROWB;
   };
   auto dma = [&](int d, int64_t koff, char* base) {
+    if ((SKIP & 1) && koff >= 0 && p.M > 0 && dma_tile >= 0 && base != smem - 1) {
+      if (g_loop_started) return;
+    }
     if (d < LA) glds16(abase[d] + koff, base + (wave * LA + d) * 1024);
     else glds16(bbase[d - LA] + koff, base + A_BYTES + (wave * LB + d - LA) * 1024);
   };
@@ -335,6 +339,12 @@ __global__ __launch_bounds__(512) void ring2_kernel(const Args p) {
   wait_vm<NDMA*(NS - 2)>();
   __builtin_amdgcn_s_barrier();
   i32x4 A0[MH], A1[MH], Bc[NR], Bn[NR];
+  if constexpr ((SKIP & 4) != 0) {
+#pragma unroll
+    for (int i = 0; i < MH; ++i) A1[i] = *(const i32x4*)(smem + aoff + (MH + i) * 16 * ROWB);
+#pragma unroll
+    for (int j = 0; j < NR; ++j) Bn[j] = *(const i32x4*)(smem + boff + j * 16 * ROWB);
+  }
 #pragma unroll
   for (int j = 0; j < NR; ++j) Bc[j] = *(const i32x4*)(smem + boff + j * 16 * ROWB);
 #pragma unroll
@@ -344,6 +354,7 @@ __global__ __launch_bounds__(512) void ring2_kernel(const Args p) {
     if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
   }
   int stores_window = 0;  // bit j: step g-1-j issued C stores
+  g_loop_started = true;
   for (int g = 0; g < total; ++g) {
     if constexpr (STAMP) t0 = __builtin_readcyclecounter();
     const char* cur = smem + (g % NS) * SLOT;
@@ -358,7 +369,7 @@ __global__ __launch_bounds__(512) void ring2_kernel(const Args p) {
       const int i = q / NR, j = q % NR;
       mma(i, j, A0[i], Bc[j]);
       if (DA > 0 && q % (16 / (DA > 0 ? DA : 1)) == 1) dma(q / (16 / (DA > 0 ? DA : 1)), koff, nbase);
-      if (q % 4 == 3) A1[q / 4] = *(const i32x4*)(cur + aoff + (MH + q / 4) * 16 * ROWB);
+      if (!(SKIP & 4) && q % 4 == 3) A1[q / 4] = *(const i32x4*)(cur + aoff + (MH + q / 4) * 16 * ROWB);
     }
     if constexpr (DA == 4) {
 #pragma unroll
@@ -397,7 +408,7 @@ __global__ __launch_bounds__(512) void ring2_kernel(const Args p) {
     else wait_vm<(VMB + 2 * NSTORE < 63 ? VMB + 2 * NSTORE : 63)>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if constexpr (STAMP) { t1 = __builtin_readcyclecounter(); t_vm += t1 - t0; t0 = t1; }
-    __builtin_amdgcn_s_barrier();
+    if constexpr (!(SKIP & 2)) __builtin_amdgcn_s_barrier();
     if constexpr (STAMP) { t1 = __builtin_readcyclecounter(); t_wait += t1 - t0; t0 = t1; }
     // ---- part C
     constexpr int DC = NDMA - DA;
@@ -408,8 +419,10 @@ __global__ __launch_bounds__(512) void ring2_kernel(const Args p) {
       mma(i, j, A1[i - MH], Bc[j]);
       if (q % 2 == 1) {
         const int r = q / 2;  // 8 reads: Bn[0..3], A0[0..3] of step g+1
-        if (r < NR) Bn[r] = *(const i32x4*)(nxt + boff + r * 16 * ROWB);
-        else A0[r - NR] = *(const i32x4*)(nxt + aoff + (r - NR) * 16 * ROWB);
+        if (!(SKIP & 4)) {
+          if (r < NR) Bn[r] = *(const i32x4*)(nxt + boff + r * 16 * ROWB);
+          else A0[r - NR] = *(const i32x4*)(nxt + aoff + (r - NR) * 16 * ROWB);
+        }
       }
       if (DC > 0 && q % (16 / (DC > 0 ? DC : 1)) == 0) dma(DA + q / (16 / (DC > 0 ? DC : 1)), koff, nbase);
     }
@@ -477,7 +490,7 @@ __global__ __launch_bounds__(512) void ring2_kernel(const Args p) {
 
 // 4-wave variant: 2x2 waves of 128x128 (one wave per SIMD, 256 accumulator registers)
 template <int NS, bool STAMP, int DMAP = 2, int PRIO = 0, int EPI = 1>
-__global__ __launch_bounds__(256) void ring4w_kernel(const Args p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void ring4w_kernel(const Args p) {
   constexpr int BM = 256, BN = 256, WN = 2, NWAVE = 4;
   constexpr int ROWB = 64;
   constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, SLOT = A_BYTES + B_BYTES;
@@ -745,9 +758,12 @@ int main(int argc, char** argv) {
 
   Variant vs[] = {
       {"ring2 dmaAC", ring2_kernel<4, false, 2>, 4, 512},
-      {"ring4w", ring4w_kernel<4, false>, 4, 256},
-      {"ring4w ns3", ring4w_kernel<3, false>, 3, 256},
-      {"ring4w nost", ring4w_kernel<4, false, 2, 0, 2>, 4, 256},
+      {"ring2 nost", ring2_kernel<4, false, 2, 0, 2>, 4, 512},
+      {"nost nodma", ring2_kernel<4, false, 2, 0, 2, 1>, 4, 512},
+      {"nost nodma nobar", ring2_kernel<4, false, 2, 0, 2, 3>, 4, 512},
+      {"nost nodma nords", ring2_kernel<4, false, 2, 0, 2, 5>, 4, 512},
+      {"nost nodma nobar nords", ring2_kernel<4, false, 2, 0, 2, 7>, 4, 512},
+      {"nost nobar", ring2_kernel<4, false, 2, 0, 2, 2>, 4, 512},
   };
   Args a{A, B, C, K, K, N, M, N, K, nullptr};
   const double flop = 2.0 * M * N * K;
