@@ -71,6 +71,25 @@ WORLD1 = [
 
 
 # ------------------------------------------------------------------------------- child
+def prewarm_runs(impl, comm, prewarm_ms: float, calib: int = 4) -> int:
+    """Number of extra pre-warm run() calls after a ``calib``-call calibration batch, agreed by
+    all ranks (MAX over ranks) so every rank issues the same sequence of collectives."""
+    import torch
+
+    if prewarm_ms <= 0:
+        return 0
+    comm.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(calib):
+        impl.run()
+    comm.synchronize()
+    per_ms = max((time.perf_counter() - t0) * 1e3 / calib, 1e-3)
+    want = torch.tensor([min(int(prewarm_ms / per_ms), 20000)], dtype=torch.float64,
+                        device=comm.device)
+    comm.all_reduce_max(want)
+    return int(want.item())
+
+
 def child_main(a) -> int:
     """One measurement on this rank's GPU; writes a JSON result file (rank 0 aggregates)."""
     import torch
@@ -94,14 +113,15 @@ def child_main(a) -> int:
             except AssertionError as e:
                 valid = False
                 res["validation"] = str(e).splitlines()[0][:200]
-        # untimed pre-warm: keep the GPU busy for prewarm_ms so the timed window does not
+        # untimed pre-warm: keep the GPU busy for ~prewarm_ms so the timed window does not
         # include the clock ramp out of idle (measured: 10 warmups of this step leave the
         # first 50 timed steps ~14 % slow). Then the W warmup steps of the contract.
-        t_end = time.perf_counter() + a.prewarm_ms / 1e3
-        while time.perf_counter() < t_end:
-            for _ in range(8):
-                impl.run()
-            comm.synchronize()
+        # Every rank must issue the SAME number of run() calls (each one holds collectives /
+        # epoch-matched cross-rank signals), so the count is derived from a calibration batch
+        # and MAX-reduced over ranks — never from each rank's own wall clock.
+        for _ in range(prewarm_runs(impl, comm, a.prewarm_ms)):
+            impl.run()
+        comm.synchronize()
         for _ in range(a.warmup):
             impl.run()
         comm.barrier()
@@ -149,6 +169,12 @@ class Job:
             self.pg = dist
         self.tmp = os.environ.get("TMPDIR", "/tmp")
         self.counter = 0
+
+    def log(self, msg: str) -> None:
+        """Progress line on rank 0's stderr (the JSON result stays the only stdout line)."""
+        if self.rank == 0:
+            sys.stderr.write(f"[bench] {msg}\n")
+            sys.stderr.flush()
 
     def bcast(self, obj):
         if self.pg is None:
@@ -234,6 +260,7 @@ def main(argv=None) -> int:
     job = Job(a)
     tune = {}
     pool = WORLD1 if world == 1 else CANDIDATES
+    fallbacks = []
     if a.algorithm != "auto":
         match = [c for c in WORLD1 + CANDIDATES if c[0] == a.algorithm]
         if not match:
@@ -241,21 +268,38 @@ def main(argv=None) -> int:
                              f"{[c[0] for c in WORLD1 + CANDIDATES]}")
         chosen = match[0]
     else:
-        best = None
+        ranked = []
         for label, impl, opts in pool:
+            t0 = time.time()
             r = job.measure(impl, opts, a.tune_steps, 3, False, a.candidate_timeout,
                             prewarm_ms=min(a.prewarm_ms, 100.0))
             tune[label] = round(r["ms"], 4) if r["ok"] else r["error"][:160]
-            if r["ok"] and impl == "native" and (best is None or r["ms"] < best[0]):
-                best = (r["ms"], (label, impl, opts))
-        if best is None:
+            job.log(f"tune {label}: {tune[label]} ({time.time() - t0:.1f} s)")
+            if r["ok"] and impl == "native":
+                ranked.append((r["ms"], (label, impl, opts)))
+        if not ranked:
             sys.stderr.write(f"every native candidate failed: {json.dumps(tune)}\n")
             return 1
-        chosen = best[1]
-    final = job.measure(chosen[1], chosen[2], a.steps, a.warmup, a.validate,
-                        a.candidate_timeout + a.steps * 0.05, prewarm_ms=a.prewarm_ms)
+        ranked.sort(key=lambda x: x[0])
+        chosen = ranked[0][1]
+        fallbacks = [c for _, c in ranked[1:3]]
+    # The winner runs the timed measurement; should it fail there (a flaky transport), the next
+    # fastest candidates are tried before giving up, so one bad path cannot sink the job.
+    final = None
+    for cand in [chosen] + (fallbacks if a.algorithm == "auto" else []):
+        t0 = time.time()
+        final = job.measure(cand[1], cand[2], a.steps, a.warmup, a.validate,
+                            a.candidate_timeout + a.steps * 0.05, prewarm_ms=a.prewarm_ms)
+        job.log(f"final {cand[0]}: {final.get('ms', final.get('error'))} "
+                f"({time.time() - t0:.1f} s)")
+        if final["ok"]:
+            if cand is not chosen:
+                tune["final_fallback_from"] = chosen[0]
+            chosen = cand
+            break
     if not final["ok"]:
-        sys.stderr.write(f"final measurement failed: {final['error']}\n")
+        sys.stderr.write(f"final measurement failed: {final['error']} "
+                         f"(autotune: {json.dumps(tune)})\n")
         return 1
     ms = final["ms"]
     flop = 2.0 * a.m * a.n * a.k

@@ -2,14 +2,13 @@
 //
 // The hand-written kernels (gemm_kernels.h) stay the path for everything fused — arrival-flag
 // gated tiles, epilogue activations, fp8/MX — and for ragged groupings; a plain or
-// strided-batched bf16/f16/f32 GEMM may instead run on the vendor library, which is what the
+// bf16/f16/f32 GEMM may instead run on the vendor library, which is what the
 // reference's torch.matmul reaches (ddlb/primitives/TPColumnwise/pytorch.py:97). The autotuner
 // (bench.py) times both and reports which one ran.
 //
 // Mapping to hipBLASLt's column-major problem: C[M,N] = A[M,K] * Bt[N,K]^T (all row-major) is
 // C^T (N x M, ld = ldc) = op(Bt)^T-view (N x K) * A^T-view (K x M): "A" = Bt with TRANSA = T,
-// "B" = A with TRANSB = N. Grouped-row addressing with equal A and C groups becomes a strided
-// batch: batch = M / grp, A stride = a_gstride * lda, C stride = c_gstride * ldc, Bt stride 0.
+// "B" = A with TRANSB = N. Grouped-row addressing is not sent here (blaslt_supports).
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt.h>
 
@@ -130,8 +129,13 @@ bool blaslt_supports(const GemmArgs& p, int din, int dout) {
   if (!lt_type(din, &t) || !lt_type(dout, &t)) return false;
   if (p.flags != nullptr || p.act != ACT_NONE || p.tile_order != 0 || p.a_table) return false;
   if (p.M <= 0 || p.N <= 0 || p.K <= 0) return false;
+  // Plain GEMMs only. Grouped-row (pipeline-stage) addressing stays on the MFMA kernels, which
+  // read the grouped rows natively in one launch: the equivalent hipBLASLt strided batch with a
+  // broadcast (stride-0) weight returned wrong tiles and then faulted on MI355X at the flagship
+  // stage shapes (65536x1024x1024 split d=2..8, s=4; scripts/diag_blas_batch.py), while the
+  // same call passed at small shapes.
   const int64_t ag = p.a_grp > 0 ? p.a_grp : p.M, cg = p.c_grp > 0 ? p.c_grp : p.M;
-  if (ag != cg || p.M % ag != 0) return false;  // one strided batch for A and C
+  if (ag != p.M || cg != p.M) return false;
   return true;
 }
 

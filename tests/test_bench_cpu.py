@@ -48,3 +48,41 @@ def test_bench_world2_cpu():
     d = _json_line(r.stdout)
     assert d["n_gpus"] == 2 and d["valid"] is True
     assert abs(d["value"] - 2 * d["per_gpu_tflops"]) < 1e-2
+
+
+def _prewarm_worker(rank, world, port, q):
+    import time
+
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      LOCAL_WORLD_SIZE=str(world), DDLB_DEVICE="cpu",
+                      DDLB_CHILD_INIT_METHOD=f"tcp://127.0.0.1:{port}")
+    sys.path.insert(0, ROOT)
+    import bench
+    from ddlb_amd.communicator import Communicator
+
+    class SlowOnRank1:  # rank 1's run() is 4x slower: a wall-clock prewarm would diverge
+        def run(self):
+            time.sleep(0.004 if rank == 1 else 0.001)
+
+    comm = Communicator()
+    comm.ensure_process_group()
+    q.put((rank, bench.prewarm_runs(SlowOnRank1(), comm, prewarm_ms=40.0)))
+    comm.destroy()
+
+
+def test_prewarm_runs_agree_across_ranks():
+    """Every rank must issue the same number of run() calls (each holds collectives / epoch-
+    matched signals): the pre-warm count is MAX-reduced, not taken from each rank's clock."""
+    import multiprocessing as mp
+
+    from conftest import free_port
+
+    ctx = mp.get_context("spawn")
+    q, port = ctx.Queue(), free_port()
+    procs = [ctx.Process(target=_prewarm_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert got[0] == got[1] and got[0] >= 30, got

@@ -248,7 +248,8 @@ def test_ring_grouped_rows(gen):
                                 (torch.float16, torch.float16), (torch.float32, torch.float32)],
                          ids=lambda d: f"{str(d[0])[6:]}-{str(d[1])[6:]}")
 def test_blas_mode(dt, gen):
-    """gemm_mode=blas: hipBLASLt for plain and strided-batched GEMMs, same contract as ours."""
+    """gemm_mode=blas: hipBLASLt for plain GEMMs; grouped-row (pipeline stage) addressing falls
+    back to the MFMA kernels — same contract either way."""
     from ddlb_amd.ops.gemm import gemm
 
     din, dout = dt
@@ -257,7 +258,7 @@ def test_blas_mode(dt, gen):
     out = gemm(a, w, out_dtype=dout, mode="blas")
     torch.cuda.synchronize()
     torch.testing.assert_close(out.float(), _ref(a, w), rtol=0, atol=_tol(din, K))
-    # strided batch (pipeline stage addressing): rows j*blk.. of each of d blocks
+    # grouped rows (pipeline stage addressing): rows j*blk.. of each of d blocks
     d, blk, j = 4, 128, 1
     A = _rand((d * 512, K), din, gen)
     C = torch.zeros((d * 512, N), dtype=dout, device=DEV)
