@@ -239,6 +239,8 @@ def main(argv=None) -> int:
                    help="auto | a candidate label (see CANDIDATES)")
     p.add_argument("--tune-steps", type=int, default=10)
     p.add_argument("--candidate-timeout", type=float, default=180.0)
+    p.add_argument("--tune-budget-s", type=float, default=420.0,
+                   help="stop trying further candidates after this much autotuning wall time")
     p.add_argument("--no-validate", dest="validate", action="store_false", default=True)
     p.add_argument("--prewarm-ms", type=float, default=300.0,
                    help="untimed GPU pre-warm before the warmup steps (clock ramp)")
@@ -269,7 +271,13 @@ def main(argv=None) -> int:
         chosen = match[0]
     else:
         ranked = []
+        t_tune = time.time()
         for label, impl, opts in pool:
+            # wall-clock cap on the search (the decision is broadcast from rank 0, so every
+            # rank stops at the same candidate): the best candidate so far runs the final
+            if job.bcast(time.time() - t_tune > a.tune_budget_s if job.rank == 0 else None):
+                tune[label] = "skipped (tuning budget)"
+                continue
             t0 = time.time()
             r = job.measure(impl, opts, a.tune_steps, 3, False, a.candidate_timeout,
                             prewarm_ms=min(a.prewarm_ms, 100.0))
