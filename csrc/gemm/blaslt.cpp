@@ -13,6 +13,7 @@
 #include <hipblaslt/hipblaslt.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <unordered_map>
@@ -35,13 +36,22 @@ struct LtKeyHash {
     return (size_t)h;
   }
 };
+constexpr int kMaxAlgos = 16, kTuneReps = 10;
 struct LtPlan {
   hipblasLtMatmulDesc_t op = nullptr;
   hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr;
   hipblasLtMatmulAlgo_t algo;
   size_t ws = 0;
-  bool ok = false;
+  bool ok = false, tuned = false;
+  int ncand = 0, chosen = 0;
+  hipblasLtMatmulHeuristicResult_t cands[kMaxAlgos];
 };
+
+// DDLB_BLAS_TUNE=0 keeps the heuristic's first choice (default: time the top candidates).
+bool tune_enabled() {
+  const char* v = std::getenv("DDLB_BLAS_TUNE");
+  return v == nullptr || std::strcmp(v, "0") != 0;
+}
 struct LtDevice {
   hipblasLtHandle_t handle = nullptr;
   void* workspace = nullptr;
@@ -111,15 +121,57 @@ bool build_plan(LtDevice* d, const LtKey& key, LtPlan* pl) {
   const uint64_t wsb = d->ws_bytes;
   hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb,
                                         sizeof(wsb));
-  hipblasLtMatmulHeuristicResult_t res[1];
   int n = 0;
-  const hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(d->handle, pl->op, pl->la, pl->lb,
-                                                             pl->lc, pl->lc, pref, 1, res, &n);
+  const hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(
+      d->handle, pl->op, pl->la, pl->lb, pl->lc, pl->lc, pref, kMaxAlgos, pl->cands, &n);
   hipblasLtMatmulPreferenceDestroy(pref);
-  if (st != HIPBLAS_STATUS_SUCCESS || n < 1 || res[0].state != HIPBLAS_STATUS_SUCCESS) return false;
-  pl->algo = res[0].algo;
-  pl->ws = res[0].workspaceSize;
-  return pl->ws <= d->ws_bytes;
+  if (st != HIPBLAS_STATUS_SUCCESS) return false;
+  for (int i = 0; i < n; ++i)  // keep the usable candidates, heuristic order
+    if (pl->cands[i].state == HIPBLAS_STATUS_SUCCESS && pl->cands[i].workspaceSize <= d->ws_bytes)
+      pl->cands[pl->ncand++] = pl->cands[i];
+  if (pl->ncand == 0) return false;
+  pl->algo = pl->cands[0].algo;
+  pl->ws = pl->cands[0].workspaceSize;
+  return true;
+}
+
+// Time the heuristic's top candidates on the caller's stream with the real operands and keep
+// the fastest (the top-1 heuristic is not always the fastest kernel for tall-skinny shapes).
+// Runs once per shape, outside graph capture; C is overwritten by the real call that follows.
+void autotune(LtDevice* d, LtPlan* pl, const GemmArgs& p, hipStream_t s) {
+  pl->tuned = true;
+  if (pl->ncand < 2 || !tune_enabled()) return;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return;
+  hipEvent_t e0, e1;
+  if (hipEventCreate(&e0) != hipSuccess) return;
+  if (hipEventCreate(&e1) != hipSuccess) { hipEventDestroy(e0); return; }
+  const float alpha = 1.f, beta = 0.f;
+  float best = 1e30f;
+  int best_i = 0;
+  for (int i = 0; i < pl->ncand; ++i) {
+    auto run = [&]() {
+      return hipblasLtMatmul(d->handle, pl->op, &alpha, p.b, pl->la, p.a, pl->lb, &beta, p.c,
+                             pl->lc, p.c, pl->lc, &pl->cands[i].algo, d->workspace,
+                             pl->cands[i].workspaceSize, s);
+    };
+    bool ok = true;
+    for (int w = 0; w < 2 && ok; ++w) ok = run() == HIPBLAS_STATUS_SUCCESS;
+    if (!ok) continue;
+    hipEventRecord(e0, s);
+    for (int r = 0; r < kTuneReps; ++r) run();
+    hipEventRecord(e1, s);
+    if (hipEventSynchronize(e1) != hipSuccess) break;
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, e0, e1);
+    if (ms < best) { best = ms; best_i = i; }
+  }
+  (void)hipGetLastError();
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  pl->algo = pl->cands[best_i].algo;
+  pl->ws = pl->cands[best_i].workspaceSize;
+  pl->chosen = best_i;
 }
 
 }  // namespace
@@ -167,6 +219,7 @@ hipError_t blaslt_gemm(const GemmArgs& p, int din, int dout, hipStream_t s) {
     pl = &it->second;
   }
   if (!pl->ok) return hipErrorNotSupported;
+  if (!pl->tuned) autotune(d, pl, p, s);
   const float alpha = 1.f, beta = 0.f;
   const hipblasStatus_t st =
       hipblasLtMatmul(d->handle, pl->op, &alpha, p.b, pl->la, p.a, pl->lb, &beta, p.c, pl->lc,

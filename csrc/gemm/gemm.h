@@ -56,7 +56,7 @@ bool gemm_fast_path_ok(const GemmArgs& p, int din, int dout);
 int choose_tile(int64_t M, int64_t N, int64_t K, int din);
 int tile_rows(int tile);
 int tile_cols(int tile);
-// hipBLASLt backend (csrc/gemm/blaslt.cpp): plain / strided-batched bf16, f16, f32 GEMMs.
+// hipBLASLt backend (csrc/gemm/blaslt.cpp): plain bf16, f16, f32 GEMMs (algorithm autotuned).
 bool blaslt_supports(const GemmArgs& p, int din, int dout);
 hipError_t blaslt_gemm(const GemmArgs& p, int din, int dout, hipStream_t s);
 
