@@ -1,0 +1,10 @@
+// gemm_fp8_bf16: instantiations of the MFMA GEMM kernels for one (input, output) dtype pair, one
+// translation unit per pair so the heavy kernel templates compile in parallel (see gemm_mfma.hip).
+#include "gemm_kernels.h"
+#include "gemm_entry.h"
+
+namespace ddlb {
+hipError_t launch_fast_fp8_bf16(const GemmArgs& p, int tile, hipStream_t s) {
+  return launch_cfg<MmaFP8, DT_BF16>(p, tile, s);
+}
+}  // namespace ddlb

@@ -102,10 +102,7 @@ hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mo
       p.tile_order = 0;
     hipError_t e = hipErrorInvalidValue;
     if (din == DT_FP8 && mode == GEMM_MODE_MX) e = launch_fast_mx(p, dout, tile, s);
-    else if (din == DT_BF16) e = launch_fast_bf16(p, dout, tile, s);
-    else if (din == DT_F16) e = launch_fast_f16(p, dout, tile, s);
-    else if (din == DT_FP8) e = launch_fast_fp8(p, dout, tile, s);
-    else if (din == DT_F32) e = launch_fast_f32(p, dout, tile, s);
+    else e = launch_fast(p, din, dout, tile, s);
     if (e != hipErrorInvalidValue) return e;
   }
   if (p.flags != nullptr) return hipErrorNotSupported;  // arrival flags need the tiled kernel

@@ -28,11 +28,15 @@ PKG = os.path.join(ROOT, "ddlb_amd")
 ARCH = os.environ.get("DDLB_OFFLOAD_ARCH", os.environ.get("PYTORCH_ROCM_ARCH", "gfx950"))
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
-SOURCES = [
-    "gemm/gemm_bf16.hip",
-    "gemm/gemm_f16.hip",
-    "gemm/gemm_fp8.hip",
-    "gemm/gemm_f32.hip",
+SOURCES = [  # heaviest translation units first (the parallel build's critical path)
+    "gemm/gemm_bf16_bf16.hip",
+    "gemm/gemm_bf16_f32.hip",
+    "gemm/gemm_fp8_bf16.hip",
+    "gemm/gemm_fp8_f16.hip",
+    "gemm/gemm_fp8_f32.hip",
+    "gemm/gemm_f16_f16.hip",
+    "gemm/gemm_f16_f32.hip",
+    "gemm/gemm_f32_f32.hip",
     "gemm/gemm_mx.hip",
     "gemm/gemm_generic.hip",
     "gemm/gemm_mfma.hip",
