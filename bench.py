@@ -237,8 +237,11 @@ def main(argv=None) -> int:
     p.add_argument("--dtype", default="bfloat16")
     p.add_argument("--algorithm", default="auto",
                    help="auto | a candidate label (see CANDIDATES)")
+    p.add_argument("--candidates", default="",
+                   help="comma list of candidate labels to autotune over (default: all)")
     p.add_argument("--tune-steps", type=int, default=10)
-    p.add_argument("--candidate-timeout", type=float, default=180.0)
+    p.add_argument("--candidate-timeout", type=float, default=90.0,
+                   help="per-candidate child timeout (a healthy candidate takes ~5-15 s)")
     p.add_argument("--tune-budget-s", type=float, default=420.0,
                    help="stop trying further candidates after this much autotuning wall time")
     p.add_argument("--no-validate", dest="validate", action="store_false", default=True)
@@ -262,6 +265,12 @@ def main(argv=None) -> int:
     job = Job(a)
     tune = {}
     pool = WORLD1 if world == 1 else CANDIDATES
+    if a.candidates:
+        want = [c.strip() for c in a.candidates.split(",") if c.strip()]
+        unknown = [w for w in want if w not in [c[0] for c in WORLD1 + CANDIDATES]]
+        if unknown:
+            raise SystemExit(f"unknown candidates {unknown}")
+        pool = [c for c in WORLD1 + CANDIDATES if c[0] in want]
     fallbacks = []
     if a.algorithm != "auto":
         match = [c for c in WORLD1 + CANDIDATES if c[0] == a.algorithm]
