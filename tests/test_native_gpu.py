@@ -130,18 +130,26 @@ def _ipc_cfgs():
     return cfgs
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_ipc_shared_gpu(world):
     from conftest import free_port
 
     port = free_port()
     cfgs = _ipc_cfgs()
+    extra = {}
+    if world >= 4:
+        # 4+ processes on ONE device oversubscribe its hardware queues and cross-process stream
+        # waits stall (profiles/r01/s2/bench_4rank_shared_*.txt); one queue per process keeps the
+        # d=4 protocols testable here. The flag-gated fused GEMM spins tiles of every co-resident
+        # process and is covered at world 2-3.
+        extra["GPU_MAX_HW_QUEUES"] = "1"
+        cfgs = [c for c in cfgs if not c[2].get("fused")]
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world),
                    LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                    DDLB_PG_BACKEND="gloo", DDLB_ALLOW_SHARED_GPU="1",
-                   DDLB_TEST_CFGS=json.dumps(cfgs))
+                   DDLB_TEST_CFGS=json.dumps(cfgs), **extra)
         env.pop("DDLB_CHILD_INIT_METHOD", None)
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests",
                                                                     "_ipc_worker.py")],
