@@ -60,6 +60,11 @@ CANDIDATES = [
     ("coll_pipeline/ipc/memcpy/s4/blas", "native", _blas(_COLL_IPC)),
     ("default/ipc/kernel", "native", _DEF_K),
     ("default/ipc/kernel/blas", "native", _blas(_DEF_K)),
+    ("p2p_pipeline/ipc/push", "native", dict(_P2P, direction="push")),
+    ("p2p_pipeline/ipc/push/blas", "native", _blas(dict(_P2P, direction="push"))),
+    ("default/ipc/push", "native", dict(_P2P, algorithm="default", direction="push")),
+    ("coll_pipeline/ipc/push/s4", "native", dict(_COLL_IPC, direction="push")),
+    ("default/ipc/kernel/push", "native", dict(_DEF_K, direction="push")),
     ("coll_pipeline/rccl/s8", "native", dict(_COLL4, s=8)),
     ("pytorch(rccl+hipblaslt)", "pytorch", dict(backend="nccl", empty_cache=False)),
 ]

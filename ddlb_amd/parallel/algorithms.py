@@ -57,6 +57,7 @@ class AlgoConfig:
     copy_blocks: int = 64               # CU budget of the kernel copy protocol
     fused: bool = False                 # p2p columnwise: one flag-gated GEMM launch
     act: int = 0                        # columnwise: fused GEMM epilogue activation (ACT_*)
+    direction: str = "pull"             # columnwise ipc: pull peers' shards | push mine to peers
 
 
 @dataclass
@@ -146,6 +147,12 @@ def check_columnwise(d: int, m: int, n: int, k: int, cfg: AlgoConfig) -> None:
         raise ValueError("algorithm=direct reads peer shards over xGMI: backend=ipc, AG_before")
     if cfg.protocol not in ("memcpy", "batch_memcpy", "kernel"):
         raise ValueError(f"unknown protocol {cfg.protocol}")
+    if cfg.direction not in ("pull", "push"):
+        raise ValueError(f"unknown direction {cfg.direction}")
+    if cfg.direction == "push" and (cfg.backend != "ipc" or cfg.order != "AG_before" or
+                                    cfg.algorithm == "direct" or cfg.fused):
+        raise ValueError("direction=push applies to backend=ipc, order=AG_before, "
+                         "default / coll_pipeline / p2p_pipeline (not fused)")
     if d > 17:
         raise ValueError("at most 17 ranks per node are supported by the flag/reduce ops")
 
@@ -196,6 +203,9 @@ def build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, dou
         return plan, io
 
     alg, be = cfg.algorithm, cfg.backend
+    if be == "ipc" and cfg.direction == "push":
+        _col_push(plan, rank, d, ml, cfg, flags, arow, crow, gemm, k * ein)
+        return plan, io
     if alg == "default" and be == "rccl":
         plan.allgather(S_MAIN, arow(rank * ml), A, ml * k, comm_dt)
         gemm(S_MAIN, A, C, m)
@@ -263,6 +273,66 @@ def build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, dou
     else:  # pragma: no cover
         raise ValueError(f"unsupported combination {alg}/{be}")
     return plan, io
+
+
+def _col_push(plan, rank, d, ml, cfg, flags, arow, crow, gemm, row_bytes) -> None:
+    """Push variant of the IPC all-gather: every rank WRITES its own shard into each peer's
+    gather buffer (one copy queue per peer, so all d-1 links carry posted writes at once; a
+    write over xGMI needs no round trip, a pull's read does), then raises the peer's arrival flag.
+
+    Flags (peer-owned slots are written remotely, local ones are waited on):
+      * READY[p] (default / p2p) or CHUNK[j*d + p] (coll stage j): p's rows are in my buffer;
+      * ACK[p]: p finished the GEMMs that read the rows I pushed there in the previous epoch,
+        so I may overwrite them (waited with delta -1 before every push: first epoch passes).
+    The receiver's GEMM of shard / stage waits the arrival flags on the compute stream and the
+    ACKs go out after the last GEMM, so no rank overwrites rows a peer is still reading."""
+    alg = cfg.algorithm
+    peers = _peer_order(rank, d, cfg.ring)
+    s = cfg.s if alg == "coll_pipeline" else 1
+    rows = ml // s
+    own = rank * ml
+
+    def arrived(p: int, j: int, owner: Optional[int] = None) -> Ref:
+        return (flags.ref("CHUNK", j * d + p, owner) if alg == "coll_pipeline"
+                else flags.ref("READY", p, owner))
+
+    if cfg.protocol == "kernel":
+        st = _s_copy(0)
+        _wait(plan, st, [flags.ref("ACK", p) for p in peers], cfg, delta=-1)
+        for j in range(s):
+            segs = [(arow(own + j * rows).at(p), arow(own + j * rows), rows * row_bytes)
+                    for p in peers]
+            for i in range(0, len(segs), 8):
+                plan.copy_multi(st, segs[i:i + 8], max_blocks=cfg.copy_blocks)
+            _signal(plan, st, [arrived(rank, j, owner=p) for p in peers], cfg)
+    else:
+        prev_last = None
+        for idx, p in enumerate(peers):
+            st = _s_copy(0) if cfg.protocol == "batch_memcpy" else _s_copy(idx)
+            if cfg.inter_stream_sync and prev_last is not None and cfg.protocol != "batch_memcpy":
+                plan.wait(st, prev_last)
+            _wait(plan, st, [flags.ref("ACK", p)], cfg, delta=-1)
+            for j in range(s):
+                plan.copy(st, arow(own + j * rows).at(p), arow(own + j * rows), rows * row_bytes,
+                          method=COPY_ENGINE)
+                _signal(plan, st, [arrived(rank, j, owner=p)], cfg)
+            prev_last = plan.event()
+            plan.record(st, prev_last)
+    # receiver side, compute stream
+    if alg == "default":
+        _wait(plan, S_MAIN, [arrived(p, 0) for p in peers], cfg)
+        gemm(S_MAIN, arow(0), crow(0), d * ml)
+    elif alg == "coll_pipeline":
+        for j in range(s):
+            _wait(plan, S_MAIN, [arrived(p, j) for p in peers], cfg)
+            gemm(S_MAIN, arow(j * rows), crow(j * rows), d * rows, a_grp=rows, a_gstride=ml,
+                 c_grp=rows, c_gstride=ml)
+    else:  # p2p_pipeline: own shard first, then shards in ring order as they arrive
+        for p in _shard_order(rank, d, cfg.ring):
+            if p != rank:
+                _wait(plan, S_MAIN, [arrived(p, 0)], cfg)
+            gemm(S_MAIN, arow(p * ml), crow(p * ml), ml)
+    _signal(plan, S_MAIN, [flags.ref("ACK", rank, owner=p) for p in peers], cfg)
 
 
 def _col_direct(plan, rank, d, m, n, k, din, dout, ein, eout, cfg, gdt) -> Plan:
@@ -410,6 +480,9 @@ def check_rowwise(d: int, m: int, n: int, k: int, cfg: AlgoConfig) -> None:
         raise ValueError(f"unknown algorithm {cfg.algorithm} for tp_rowwise")
     if cfg.backend not in ("rccl", "ipc"):
         raise ValueError(f"unknown backend {cfg.backend}")
+    if cfg.direction != "pull":
+        raise ValueError("direction=push is a tp_columnwise all-gather option (the rowwise "
+                         "p2p_pipeline already pushes its partials)")
     if d > 16:
         raise ValueError("at most 16 ranks per node are supported by the reduce op")
 

@@ -24,7 +24,8 @@ kernels), ``tile`` (GEMM tile or ``auto``), ``gemm_mode`` (``auto`` | ``mx`` for
 ``blas`` = hipBLASLt for the plain GEMM ops of the plan, fused ones stay on the MFMA kernels),
 ``copy_blocks`` (CU budget of the kernel protocol), ``fused`` (p2p: one arrival-flag-gated GEMM),
 ``graph`` (capture the plan once and replay it as one hipGraph launch; ``auto`` = whenever the
-plan has no cross-process signals).
+plan has no cross-process signals), ``direction`` (columnwise ipc: ``pull`` peers' shards, or
+``push`` my shard into every peer's gather buffer with posted xGMI writes).
 """
 
 from __future__ import annotations
@@ -46,6 +47,7 @@ COMMON_DEFAULTS = {
     "copy_blocks": 64,
     "fused": False,
     "graph": False,
+    "direction": "pull",
 }
 COMMON_ALLOWED = {
     "backend": ["rccl", "ipc", *UCC_BACKENDS],
@@ -61,6 +63,7 @@ COMMON_ALLOWED = {
     "copy_blocks": (1, 4096),
     "fused": [True, False],
     "graph": [True, False, "auto"],
+    "direction": ["pull", "push"],
 }
 COMMON_ALIASES = {
     "backend": {"nccl": "rccl", "cuda": "ipc"},
@@ -89,7 +92,8 @@ def algo_config(options, order: str = "AG_before") -> AlgoConfig:
         inter_stream_sync=bool(options["inter_stream_synchronization"]),
         signal=SIG_STREAM if options["signal"] == "stream" else SIG_KERNEL,
         tile=TILE_CODE[options["tile"]], mode=MODE_CODE[options["gemm_mode"]],
-        copy_blocks=int(options["copy_blocks"]), fused=bool(options["fused"]))
+        copy_blocks=int(options["copy_blocks"]), fused=bool(options["fused"]),
+        direction=options.get("direction", "pull"))
 
 
 def dtype_codes(dtype_name: str):

@@ -124,6 +124,11 @@ def _ipc_cfgs():
                                                       signal=sig)))
     cfgs.append(("col/direct/128", "col", dict(algorithm="direct", backend="ipc",
                                                tile="128x128")))
+    for alg in ("default", "coll_pipeline", "p2p_pipeline"):  # push all-gather
+        for proto in ("memcpy", "kernel"):
+            cfgs.append((f"col/{alg}/ipc/push/{proto}", "col",
+                         dict(algorithm=alg, backend="ipc", multicast_protocol=proto, s=2,
+                              direction="push")))
     for alg in ("default", "coll_pipeline", "p2p_pipeline"):  # bench.py's "/blas" candidates
         cfgs.append((f"col/{alg}/ipc/blas", "col", dict(algorithm=alg, backend="ipc", s=2,
                                                         gemm_mode="blas")))

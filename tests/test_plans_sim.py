@@ -86,6 +86,29 @@ def test_ipc_protocols(protocol, alg, ring, sig):
     _run_row(3, m=24, n=8, k=9, cfg=cfg)
 
 
+@pytest.mark.parametrize("d", [2, 3, 4])
+@pytest.mark.parametrize("protocol", PROTOCOLS)
+@pytest.mark.parametrize("alg", ALGS)
+@pytest.mark.parametrize("sig", [SIG_STREAM, SIG_KERNEL])
+def test_ipc_push_plans(d, protocol, alg, sig):
+    """direction=push: writers fill every peer's gather buffer; arrival flags / ACK epochs."""
+    cfg = AlgoConfig(algorithm=alg, backend="ipc", protocol=protocol, signal=sig, s=2,
+                     direction="push")
+    _run_col(d, 8 * d, 8, 8, cfg, epochs=4)
+
+
+def test_push_rejected_where_meaningless():
+    for cfg in (AlgoConfig(algorithm="default", backend="rccl", direction="push"),
+                AlgoConfig(algorithm="direct", backend="ipc", direction="push"),
+                AlgoConfig(algorithm="p2p_pipeline", backend="ipc", fused=True, direction="push"),
+                AlgoConfig(backend="ipc", order="AG_after", direction="push")):
+        with pytest.raises(ValueError):
+            build_tp_columnwise(0, 2, 16, 8, 8, DT_F32, DT_F32, cfg)
+    with pytest.raises(ValueError):
+        build_tp_rowwise(0, 2, 16, 8, 8, DT_F32, DT_F32, AlgoConfig(backend="ipc",
+                                                                     direction="push"))
+
+
 @pytest.mark.parametrize("fused", [True, False])
 def test_p2p_fused_plan(fused):
     cfg = AlgoConfig(algorithm="p2p_pipeline", backend="ipc", fused=fused)
