@@ -11,6 +11,7 @@
 #include <ATen/dlpack.h>
 
 #include <memory>
+#include <tuple>
 
 #include "comm/comm.h"
 #include "gemm/gemm.h"
@@ -123,6 +124,19 @@ PYBIND11_MODULE(_C, m) {
           a.src[0] = (const void*)src;
           a.bytes[0] = bytes;
           check(copy_launch(a, max_blocks, (hipStream_t)s), "copy");
+        });
+  m.def("copy_multi",  // segments (dst, src, bytes) copied concurrently by one CU kernel
+        [](std::vector<std::tuple<uintptr_t, uintptr_t, int64_t>> segs, int max_blocks,
+           uintptr_t s) {
+          CopyArgs a;
+          a.nseg = (int)segs.size();
+          if (a.nseg < 1 || a.nseg > kMaxCopySeg) throw std::runtime_error("1..8 segments");
+          for (int i = 0; i < a.nseg; ++i) {
+            a.dst[i] = (void*)std::get<0>(segs[(size_t)i]);
+            a.src[i] = (const void*)std::get<1>(segs[(size_t)i]);
+            a.bytes[i] = std::get<2>(segs[(size_t)i]);
+          }
+          check(copy_launch(a, max_blocks, (hipStream_t)s), "copy_multi");
         });
   m.def("device_synchronize", []() { check(hipDeviceSynchronize(), "hipDeviceSynchronize"); });
   m.def("get_last_error", []() { return std::string(hipGetErrorString(hipGetLastError())); });

@@ -98,29 +98,33 @@ __global__ __launch_bounds__(256) void reduce_sum_kernel(ReduceArgs a) {
   }
 }
 
+// Blocks are dealt round-robin to the segments (one segment = one peer = one xGMI link in the
+// IPC all-gathers), so every link carries traffic at once; the blocks of a segment grid-stride
+// over it with 4 x 16 B in flight per lane. (Walking the segments one after another would keep
+// a single link busy at a time: d-1 times the transfer time of a full-mesh exchange.)
 __global__ __launch_bounds__(256) void copy_kernel(CopyArgs a) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int seg = 0; seg < a.nseg; ++seg) {
-    const char* src = (const char*)a.src[seg];
-    char* dst = (char*)a.dst[seg];
-    const int64_t bytes = a.bytes[seg];
-    const int64_t nvec = bytes / 16;
-    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    // 4 x 16 B in flight per lane
-    int64_t v = t0;
-    for (; v + 3 * stride < nvec; v += 4 * stride) {
-      const uint4 x0 = *(const uint4*)(src + v * 16);
-      const uint4 x1 = *(const uint4*)(src + (v + stride) * 16);
-      const uint4 x2 = *(const uint4*)(src + (v + 2 * stride) * 16);
-      const uint4 x3 = *(const uint4*)(src + (v + 3 * stride) * 16);
-      *(uint4*)(dst + v * 16) = x0;
-      *(uint4*)(dst + (v + stride) * 16) = x1;
-      *(uint4*)(dst + (v + 2 * stride) * 16) = x2;
-      *(uint4*)(dst + (v + 3 * stride) * 16) = x3;
-    }
-    for (; v < nvec; v += stride) *(uint4*)(dst + v * 16) = *(const uint4*)(src + v * 16);
-    for (int64_t b = nvec * 16 + t0; b < bytes; b += stride) dst[b] = src[b];
+  const int nseg = a.nseg;
+  const int seg = (int)blockIdx.x % nseg;
+  const int nb = ((int)gridDim.x - seg + nseg - 1) / nseg;  // blocks serving this segment
+  const int64_t stride = (int64_t)nb * blockDim.x;
+  const int64_t t0 = (int64_t)((int)blockIdx.x / nseg) * blockDim.x + threadIdx.x;
+  const char* src = (const char*)a.src[seg];
+  char* dst = (char*)a.dst[seg];
+  const int64_t bytes = a.bytes[seg];
+  const int64_t nvec = bytes / 16;
+  int64_t v = t0;
+  for (; v + 3 * stride < nvec; v += 4 * stride) {
+    const uint4 x0 = *(const uint4*)(src + v * 16);
+    const uint4 x1 = *(const uint4*)(src + (v + stride) * 16);
+    const uint4 x2 = *(const uint4*)(src + (v + 2 * stride) * 16);
+    const uint4 x3 = *(const uint4*)(src + (v + 3 * stride) * 16);
+    *(uint4*)(dst + v * 16) = x0;
+    *(uint4*)(dst + (v + stride) * 16) = x1;
+    *(uint4*)(dst + (v + 2 * stride) * 16) = x2;
+    *(uint4*)(dst + (v + 3 * stride) * 16) = x3;
   }
+  for (; v < nvec; v += stride) *(uint4*)(dst + v * 16) = *(const uint4*)(src + v * 16);
+  for (int64_t b = nvec * 16 + t0; b < bytes; b += stride) dst[b] = src[b];
 }
 
 __global__ void signal_kernel(SignalArgs a) {
@@ -180,6 +184,8 @@ hipError_t copy_launch(const CopyArgs& a, int max_blocks, hipStream_t s) {
   }
   int g = grid_for(total / 64 + 1);
   if (max_blocks > 0 && g > max_blocks) g = max_blocks;
+  // at least one block per segment, and a whole number of blocks per segment
+  g = g < a.nseg ? a.nseg : (g / a.nseg) * a.nseg;
   hipLaunchKernelGGL(copy_kernel, dim3(g), dim3(256), 0, s, a);
   return hipGetLastError();
 }

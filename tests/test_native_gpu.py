@@ -212,3 +212,24 @@ def test_graph_refused_for_signal_plans():
     assert not ex.graph_capturable()
     with pytest.raises(RuntimeError):
         ex.enable_graph(True)
+
+
+@pytest.mark.parametrize("nseg,max_blocks", [(1, 64), (3, 64), (7, 128), (8, 5), (5, 0)])
+def test_copy_multi_segments(nseg, max_blocks):
+    """The CU copy kernel of the `kernel` protocol moves every segment (one peer each in the IPC
+    all-gathers) concurrently: blocks are dealt round-robin to segments, so any block budget —
+    even fewer blocks than segments — must still copy every byte of every segment."""
+    from ddlb_amd.ops import load
+
+    C = load()
+    g = torch.Generator(device="cuda").manual_seed(nseg)
+    sizes = [(1 << 20) + 16 * i + (5 if i % 2 else 0) for i in range(nseg)]  # byte tails
+    srcs = [torch.randint(0, 255, (n,), dtype=torch.uint8, device="cuda", generator=g)
+            for n in sizes]
+    dsts = [torch.zeros_like(x) for x in srcs]
+    stream = torch.cuda.current_stream().cuda_stream
+    C.copy_multi([(d.data_ptr(), s.data_ptr(), s.numel()) for d, s in zip(dsts, srcs)],
+                 max_blocks, stream)
+    torch.cuda.synchronize()
+    for d, s in zip(dsts, srcs):
+        assert torch.equal(d, s)
