@@ -121,9 +121,9 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
         return out
     tl = _torch_lib_dir()
     cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", out + ".tmp",
-           f"-L{ROCM}/lib", "-lrccl", "-lhipblaslt", "-lamdhip64", f"-Wl,-rpath,{tl}" if tl else "",
-           "-Wl,--no-undefined" if False else ""]
-    cmd = [c for c in cmd if c]
+           f"-L{ROCM}/lib", "-lrccl", "-lhipblaslt", "-lamdhip64"]
+    if tl:
+        cmd.append(f"-Wl,-rpath,{tl}")
     if verbose:
         print(" ".join(cmd))
     r = subprocess.run(cmd, capture_output=True, text=True)
