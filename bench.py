@@ -290,7 +290,8 @@ def main(argv=None) -> int:
         for label, impl, opts in pool:
             # wall-clock cap on the search (the decision is broadcast from rank 0, so every
             # rank stops at the same candidate): the best candidate so far runs the final
-            if job.bcast(time.time() - t_tune > a.tune_budget_s if job.rank == 0 else None):
+            over = bool(ranked) and time.time() - t_tune > a.tune_budget_s  # keep going until
+            if job.bcast(over if job.rank == 0 else None):                     # one succeeded
                 tune[label] = "skipped (tuning budget)"
                 continue
             t0 = time.time()

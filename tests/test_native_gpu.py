@@ -233,3 +233,51 @@ def test_copy_multi_segments(nseg, max_blocks):
     torch.cuda.synchronize()
     for d, s in zip(dsts, srcs):
         assert torch.equal(d, s)
+
+
+def test_rccl_data_plane_world1(comm):
+    """Our own RCCL communicator (csrc/comm) driven by the plan executor on its own stream:
+    all-gather, reduce-scatter and a grouped send/recv to self, then a GEMM ordered after them
+    by an event. At world 1 the collectives are copies, but the linkage, ncclCommInitRank from
+    a unique id, dtype mapping and stream/event plumbing are the ones the N>1 plans use."""
+    from ddlb_amd.parallel.context import NativeContext
+    from ddlb_amd.parallel.plan import DT_BF16, DT_F32, Plan
+
+    n = 4096
+    plan = Plan(0, 1, nstreams=2, stream_priority=[0, 1])
+    src = plan.buffer("src", n * 4)
+    ag = plan.buffer("ag", n * 4)
+    rs = plan.buffer("rs", n * 4)
+    rv = plan.buffer("rv", n * 4)
+    a = plan.buffer("a", 256 * 128 * 2)
+    bt = plan.buffer("bt", 128 * 128 * 2)
+    c = plan.buffer("c", 256 * 128 * 4)
+    plan.allgather(1, src, ag, n, DT_F32)
+    plan.reduce_scatter(1, src, rs, n, DT_F32)
+    plan.group_start(1)
+    plan.send(1, src, n, DT_F32, 0)
+    plan.recv(1, rv, n, DT_F32, 0)
+    plan.group_end(1)
+    e = plan.event()
+    plan.record(1, e)
+    plan.wait(0, e)
+    plan.gemm(0, a, bt, c, M=256, N=128, K=128, lda=128, ldb=128, ldc=128, din=DT_BF16,
+              dout=DT_F32)
+    ctx = NativeContext(comm)
+    bound = ctx.bind(plan)
+    x = torch.randn(n, device="cuda")
+    bound.buffer("src").view(torch.float32).copy_(x)
+    A = torch.randn(256, 128, device="cuda").bfloat16()
+    W = torch.randn(128, 128, device="cuda").bfloat16()
+    bound.buffer("a").view(torch.bfloat16).view(256, 128).copy_(A)
+    bound.buffer("bt").view(torch.bfloat16).view(128, 128).copy_(W)
+    for _ in range(3):
+        bound.run()
+    torch.cuda.synchronize()
+    for name in ("ag", "rs", "rv"):
+        assert torch.equal(bound.buffer(name).view(torch.float32), x), name
+    out = bound.buffer("c").view(torch.float32).view(256, 128)
+    torch.testing.assert_close(out, A.float() @ W.float().T, rtol=0, atol=1e-3 * 128)
+    assert ctx.rccl().async_error() == ""
+    bound.close()
+    ctx.close()
