@@ -12,14 +12,20 @@ Contract (driver):  python bench.py --gpus N --steps K --warmup W
     (every rank computes the full [m,k]x[k,n] on its own N-slice of the weight: weak scaling in
     N); ``per_gpu_tflops`` is the reference harness's per-GPU number (``ddlb/benchmark.py:211``).
 
+Other BASELINE configs through the same machinery: ``--primitive tp_rowwise -m 16384 -n 8192
+-k 8192`` (config #3, GEMM + reduce-scatter; strong scaling: the harness number is the whole-job
+aggregate) and ``--dtype float8_e4m3fn`` (config #5; adds the block-scaled MX-fp8 candidates).
+
 Process model (robust by construction): the launched processes never touch the GPU. They form
 a gloo group and run every measurement in a child process per rank (fresh HIP context, its own
-rendezvous port, a hard timeout). With N>1 an autotuner first times each candidate native
-algorithm in its own children (MAX over ranks), then the winner runs the timed measurement; a
-candidate that fails or hangs is killed and skipped on every rank, so one bad path cannot hang
-the job. Candidate timings are reported in the JSON (``autotune_ms``). Synthetic U[-1,1) inputs
-of the named shape (no datasets exist offline); the result is validated against an fp32
-reference.
+rendezvous port, a hard timeout). An autotuner first times each candidate algorithm in its own
+children (MAX over ranks), then the winner runs the timed measurement (falling back to the next
+fastest if it fails there); a candidate that fails or hangs is killed and skipped on every rank,
+so one bad path cannot hang the job. Every rank issues the same number of run() calls (the
+pre-warm count is MAX-reduced), as each call holds collectives / epoch-matched signals.
+Candidate timings are reported in the JSON (``autotune_ms``), progress on stderr. Synthetic
+U[-1,1) inputs of the named shape (no datasets exist offline); the result is validated against
+an fp32 reference.
 """
 
 from __future__ import annotations
@@ -74,6 +80,37 @@ WORLD1 = [
     ("gemm (world=1)/hip", "native", _DEF),
     ("gemm (world=1)/blas", "native", _blas(_DEF)),
 ]
+# tp_rowwise (GEMM + sequence-parallel reduce-scatter; BASELINE config #3)
+_RK = dict(backend="ipc", multicast_protocol="kernel", copy_blocks=128)
+ROW_CANDIDATES = [
+    ("row/default/rccl", "native", dict(algorithm="default", backend="rccl")),
+    ("row/default/rccl/blas", "native", _blas(dict(algorithm="default", backend="rccl"))),
+    ("row/coll_pipeline/rccl/s4", "native", dict(algorithm="coll_pipeline", backend="rccl", s=4)),
+    ("row/p2p_pipeline/rccl", "native", dict(algorithm="p2p_pipeline", backend="rccl")),
+    ("row/default/ipc/kernel", "native", dict(_RK, algorithm="default")),
+    ("row/default/ipc/kernel/blas", "native", _blas(dict(_RK, algorithm="default"))),
+    ("row/coll_pipeline/ipc/kernel/s4", "native", dict(_RK, algorithm="coll_pipeline", s=4)),
+    ("row/p2p_pipeline/ipc/memcpy", "native", dict(algorithm="p2p_pipeline", backend="ipc")),
+    ("row/pytorch(rccl+hipblaslt)", "pytorch", dict(backend="nccl", empty_cache=False)),
+]
+ROW_WORLD1 = [
+    ("row/gemm (world=1)/hip", "native", dict(algorithm="default", backend="rccl")),
+    ("row/gemm (world=1)/blas", "native", _blas(dict(algorithm="default", backend="rccl"))),
+]
+
+
+def candidate_pool(primitive: str, dtype: str, world: int):
+    """(label, impl, options) list for one primitive / dtype / world size. fp8 inputs add the
+    block-scaled MX-fp8 MFMA (2x the bf16 rate) and drop hipBLASLt (no fp8 in the plain path)."""
+    if primitive == "tp_rowwise":
+        pool = ROW_WORLD1 if world == 1 else ROW_CANDIDATES
+    else:
+        pool = WORLD1 if world == 1 else CANDIDATES
+    if dtype == "float8_e4m3fn":
+        pool = [c for c in pool if c[2].get("gemm_mode") != "blas"]
+        pool = pool + [(lbl + "/mx", impl, dict(opts, gemm_mode="mx")) for lbl, impl, opts in pool
+                       if impl == "native"]
+    return pool
 
 
 # ------------------------------------------------------------------------------- child
@@ -107,7 +144,7 @@ def child_main(a) -> int:
     try:
         comm = Communicator()
         comm.ensure_process_group(timeout_s=a.child_timeout)
-        cls, opts, _ = resolve("tp_columnwise", a.child_impl, json.loads(a.child_opts))
+        cls, opts, _ = resolve(a.primitive, a.child_impl, json.loads(a.child_opts))
         impl = cls(m=a.m, n=a.n, k=a.k, dtype=a.dtype, **opts)
         valid = None
         if a.validate:
@@ -206,7 +243,8 @@ class Job:
         env["DDLB_CHILD_INIT_METHOD"] = f"tcp://127.0.0.1:{port}"
         cmd = [sys.executable, os.path.abspath(__file__), "--child", "--child-out", out,
                "--child-impl", impl, "--child-opts", json.dumps(opts), "--steps", str(steps),
-               "--warmup", str(warmup), "-m", str(self.a.m), "-n", str(self.a.n), "-k",
+               "--warmup", str(warmup), "--primitive", self.a.primitive,
+               "-m", str(self.a.m), "-n", str(self.a.n), "-k",
                str(self.a.k), "--dtype", self.a.dtype, "--child-timeout", str(timeout),
                "--prewarm-ms", str(prewarm_ms)]
         if validate:
@@ -241,6 +279,9 @@ def main(argv=None) -> int:
     p.add_argument("-n", type=int, default=1024)
     p.add_argument("-k", type=int, default=1024)
     p.add_argument("--dtype", default="bfloat16")
+    p.add_argument("--primitive", default="tp_columnwise", choices=["tp_columnwise", "tp_rowwise"],
+                   help="tp_columnwise = the flagship (AG+GEMM); tp_rowwise = GEMM+RS "
+                        "(BASELINE config #3: -m 16384 -n 8192 -k 8192)")
     p.add_argument("--algorithm", default="auto",
                    help="auto | a candidate label (see CANDIDATES)")
     p.add_argument("--candidates", default="",
@@ -270,19 +311,20 @@ def main(argv=None) -> int:
         return 2
     job = Job(a)
     tune = {}
-    pool = WORLD1 if world == 1 else CANDIDATES
+    pool = candidate_pool(a.primitive, a.dtype, world)
+    every = candidate_pool(a.primitive, a.dtype, 1) + candidate_pool(a.primitive, a.dtype, 2)
     if a.candidates:
         want = [c.strip() for c in a.candidates.split(",") if c.strip()]
-        unknown = [w for w in want if w not in [c[0] for c in WORLD1 + CANDIDATES]]
+        unknown = [w for w in want if w not in [c[0] for c in every]]
         if unknown:
             raise SystemExit(f"unknown candidates {unknown}")
-        pool = [c for c in WORLD1 + CANDIDATES if c[0] in want]
+        pool = [c for c in every if c[0] in want]
     fallbacks = []
     if a.algorithm != "auto":
-        match = [c for c in WORLD1 + CANDIDATES if c[0] == a.algorithm]
+        match = [c for c in every if c[0] == a.algorithm]
         if not match:
             raise SystemExit(f"unknown --algorithm {a.algorithm}; choose from "
-                             f"{[c[0] for c in WORLD1 + CANDIDATES]}")
+                             f"{[c[0] for c in every]}")
         chosen = match[0]
     else:
         ranked = []
@@ -327,18 +369,28 @@ def main(argv=None) -> int:
         return 1
     ms = final["ms"]
     flop = 2.0 * a.m * a.n * a.k
-    per_gpu = flop / (ms * 1e-3) / 1e12
+    harness_tflops = flop / (ms * 1e-3) / 1e12  # the reference's formula (ddlb/benchmark.py:211)
+    col = a.primitive == "tp_columnwise"
+    # whole-job aggregate: tp_columnwise = every rank computes the full [m,k]x[k,n] on its own
+    # N-slice (weak scaling, N x the harness number); tp_rowwise = the ranks share one
+    # [m,k]x[k,n] split along K (strong scaling, the harness number IS the aggregate)
+    value = harness_tflops * world if col else harness_tflops
     if job.rank == 0:
+        dt = {"bfloat16": "bf16", "float16": "fp16", "float32": "fp32",
+              "float8_e4m3fn": "fp8_e4m3"}.get(a.dtype, a.dtype)
         line = {
-            "metric": "tp_columnwise AG+GEMM effective TFLOP/s (whole job, m=65536 bf16)",
-            "value": round(per_gpu * world, 6), "unit": "TFLOP/s", "n_gpus": world,
+            "metric": (f"tp_columnwise AG+GEMM effective TFLOP/s (whole job, m={a.m} {dt})" if col
+                       else f"tp_rowwise GEMM+RS effective TFLOP/s (whole job, m={a.m} {dt})"),
+            "value": round(value, 6), "unit": "TFLOP/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 5),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "bf16" if a.dtype == "bfloat16" else a.dtype, "data": "synthetic",
-            "config": {"model": f"tp_columnwise AG+GEMM m={a.m} n={a.n} k={a.k}",
+            "higher_is_better": True, "scaling": "weak" if col else "strong",
+            "vs_baseline": None, "dtype": dt, "data": "synthetic",
+            "config": {"model": (f"tp_columnwise AG+GEMM m={a.m} n={a.n} k={a.k}" if col
+                                 else f"tp_rowwise GEMM+RS m={a.m} n={a.n} k={a.k}"),
                        "global_batch": 1, "seq_len": a.m, "parallelism": f"tp{world}-sp",
                        "implementation": chosen[1], "algorithm": chosen[0]},
-            "per_gpu_tflops": round(per_gpu, 6), "valid": final.get("valid"),
+            "per_gpu_tflops": round(harness_tflops if col else harness_tflops / world, 6),
+            "harness_tflops": round(harness_tflops, 6), "valid": final.get("valid"),
             "gemm": ("hipblaslt" if chosen[1] == "pytorch" or chosen[2].get("gemm_mode") == "blas"
                      else "ddlb_amd MFMA"),
             "prewarm_ms": a.prewarm_ms,

@@ -688,6 +688,169 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// t8: 256x256 tile, BK = 64 (128-byte LDS rows), 8 waves = 2 groups (wr) x 4 (wc), 128x64 per
+// wave as 2x2 quadrants of 64x32 (cdna guide §5 "256^2 8-phase template": T2+T3+T4+T5).
+// Group 1 runs one barrier behind group 0, so between any two barriers one group issues its
+// ds_reads / LDS-DMA while the other runs 16 MFMAs. K-tile data moves in 16 KB units of 128 rows:
+//   UA0 = A rows {0-63, 128-191} (quadrant row mq=0 of both groups), UA1 = {64-127, 192-255},
+//   UB0 = B rows {wc*64 + 0..31}, UB1 = {wc*64 + 32..63};
+// wave w stages unit rows [16w, 16w+16) (2 x 1 KB LDS-DMA). Per K-tile t (buffer t&1), phase p of
+// a group reads / stages (intervals I_k between barriers; group g reads in I_{8t+2p+g}):
+//   p0: read A(mq0) + B(nq0), stage UA1(t+1)   p1: read B(nq1), stage UB0(t+1)
+//   p2: read A(mq1),          stage UA0(t+2)   p3: read B(nq0), stage UB1(t+2), vmcnt(4)
+// RAW: vmcnt(4) (2 unit slices in flight) before barrier 8(t+1) retires every slice of K-tile t+1
+// on every wave (group 1 in its p3 read section, group 0 after its p3 MFMAs).
+// WAR: each unit is restaged 3 intervals after its last read (reads retire by lgkmcnt(0) in the
+// next interval), e.g. UA0 of t read in I_{8t}, I_{8t+1}, restaged in I_{8t+4}, I_{8t+5}.
+// Past the last K-tile the stage source is clamped to K-tile nk-1: identical bytes into units no
+// one reads again, so the vmcnt arithmetic stays uniform.
+__device__ __forceinline__ int t8_perm(int t) { return 8 * ((t & 15) >> 2) + 4 * (t >> 4) + (t & 3); }
+
+template <bool STAMP>
+__global__ __launch_bounds__(512) void t8_kernel(const Args p) {
+  constexpr int ROWB = 128, UNIT = 128 * ROWB, STAGE = 4 * UNIT;
+  constexpr int UA0 = 0, UA1 = UNIT, UB0 = 2 * UNIT, UB1 = 3 * UNIT;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int tiles_n = p.N / 256, ntiles = (p.M / 256) * tiles_n;
+  const int wg = xcd_remap((int)blockIdx.x, ntiles);
+  const int64_t m0 = (int64_t)(wg / tiles_n) * 256, n0 = (int64_t)(wg % tiles_n) * 256;
+  const int nk = p.K / 64;
+
+  // ---- LDS-DMA sources of this wave's slices (2 instructions x 8 rows per unit)
+  const int drow = lane >> 3, dpc = lane & 7;
+  const char* sA[2][2];
+  const char* sB[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int ur = wave * 16 + i * 8 + drow;
+    const int ch = (dpc ^ ((ur >> 1) & 7)) * 16;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int lr = (ur >> 6) * 128 + q * 64 + (ur & 63);
+      sA[q][i] = (const char*)p.a + (m0 + lr) * p.lda * 2 + ch;
+      const int lc = (ur >> 5) * 64 + q * 32 + t8_perm(ur & 31);
+      sB[q][i] = (const char*)p.b + (n0 + lc) * p.ldb * 2 + ch;
+    }
+  }
+  auto stage = [&](const char* const* src, int unit_off, int kt, int buf) {
+    kt = kt < nk ? kt : nk - 1;
+    char* dst = smem + buf * STAGE + unit_off + wave * 16 * ROWB;
+    glds16(src[0] + (int64_t)kt * ROWB, dst);
+    glds16(src[1] + (int64_t)kt * ROWB, dst + 8 * ROWB);
+  };
+
+  // ---- fragment reads: lane -> unit row base + (lane & 15), logical chunk kk*4 + (lane >> 4)
+  const int frow = lane & 15, fq = lane >> 4, sw = (frow >> 1) & 7;
+  const int c0 = ((0 + fq) ^ sw) * 16, c1 = ((4 + fq) ^ sw) * 16;
+  const int aoff = (wr * 64 + frow) * ROWB, boff = (wc * 32 + frow) * ROWB;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  i32x4 aR[4][2], bR[2][2];
+  auto loadA = [&](const char* base, int mq) {
+    const char* r = base + (mq ? UA1 : UA0) + aoff;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      aR[f][0] = *(const i32x4*)(r + f * 16 * ROWB + c0);
+      aR[f][1] = *(const i32x4*)(r + f * 16 * ROWB + c1);
+    }
+  };
+  auto loadB = [&](const char* base, int nq) {
+    const char* r = base + (nq ? UB1 : UB0) + boff;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      bR[g][0] = *(const i32x4*)(r + g * 16 * ROWB + c0);
+      bR[g][1] = *(const i32x4*)(r + g * 16 * ROWB + c1);
+    }
+  };
+  auto comp = [&](int mq, int nq) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+          acc[mq * 4 + f][nq * 2 + g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8, bR[g][kk]), __builtin_bit_cast(bf16x8, aR[f][kk]),
+              acc[mq * 4 + f][nq * 2 + g], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+#define T8_BAR()                         \
+  do {                                   \
+    __builtin_amdgcn_sched_barrier(0);   \
+    __builtin_amdgcn_s_barrier();        \
+    __builtin_amdgcn_sched_barrier(0);   \
+  } while (0)
+
+  // ---- prologue: K-tile 0 whole, UA0 / UB1 of K-tile 1 in flight
+  stage(sA[0], UA0, 0, 0);
+  stage(sB[1], UB1, 0, 0);
+  stage(sA[1], UA1, 0, 0);
+  stage(sB[0], UB0, 0, 0);
+  stage(sA[0], UA0, 1, 1);
+  stage(sB[1], UB1, 1, 1);
+  wait_vm<4>();
+  T8_BAR();
+  const bool g1 = wr == 1;  // wave-uniform
+  if (g1) T8_BAR();
+  for (int t = 0; t < nk; ++t) {
+    const int b = t & 1, nb = b ^ 1;
+    const char* cur = smem + b * STAGE;
+    // p0
+    loadA(cur, 0);
+    loadB(cur, 0);
+    stage(sA[1], UA1, t + 1, nb);
+    T8_BAR();
+    comp(0, 0);
+    T8_BAR();
+    // p1
+    loadB(cur, 1);
+    stage(sB[0], UB0, t + 1, nb);
+    T8_BAR();
+    comp(0, 1);
+    T8_BAR();
+    // p2
+    loadA(cur, 1);
+    stage(sA[0], UA0, t + 2, b);
+    T8_BAR();
+    comp(1, 1);
+    T8_BAR();
+    // p3
+    loadB(cur, 0);
+    stage(sB[1], UB1, t + 2, b);
+    if (g1) wait_vm<4>();
+    T8_BAR();
+    comp(1, 0);
+    if (!g1) wait_vm<4>();
+    T8_BAR();
+  }
+  if (!g1) T8_BAR();
+#undef T8_BAR
+  wait_vm<0>();
+  // ---- epilogue: lane holds columns 8*fq .. 8*fq+7 of each 32-column quadrant (B rows permuted)
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    char* crow = (char*)p.c + (m0 + wr * 128 + (i >> 2) * 64 + (i & 3) * 16 + frow) * p.ldc * 2;
+#pragma unroll
+    for (int nq = 0; nq < 2; ++nq) {
+      const f32x4 v0 = acc[i][nq * 2], v1 = acc[i][nq * 2 + 1];
+      bf16x8 o = {(__bf16)v0.x, (__bf16)v0.y, (__bf16)v0.z, (__bf16)v0.w,
+                  (__bf16)v1.x, (__bf16)v1.y, (__bf16)v1.z, (__bf16)v1.w};
+      *(uint4*)(crow + (n0 + wc * 64 + nq * 32 + fq * 8) * 2) = __builtin_bit_cast(uint4, o);
+    }
+  }
+}
+
 // fp32 reference: C[m][n] = sum_k A[m][k] * B[n][k]
 __global__ void ref_kernel(const __hip_bfloat16* A, const __hip_bfloat16* B, float* C, int M, int N,
                            int K) {
@@ -730,6 +893,7 @@ struct Variant {
   KFn fn;
   int ns;
   int threads;
+  int all_tiles = 0;  // 1: one workgroup per tile (non-persistent)
 };
 
 int main(int argc, char** argv) {
@@ -737,7 +901,7 @@ int main(int argc, char** argv) {
   const int N = argc > 2 ? atoi(argv[2]) : 1024;
   const int K = argc > 3 ? atoi(argv[3]) : 1024;
   const int rounds = 5, iters = 20;
-  if (M % 256 || N % 256 || K % 32) { fprintf(stderr, "shape must be multiple of 256/256/32\n"); return 2; }
+  if (M % 256 || N % 256 || K % 64) { fprintf(stderr, "shape must be multiple of 256/256/64\n"); return 2; }
   int dev = 0, ncu = 0;
   CHECK(hipGetDevice(&dev));
   CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
@@ -757,13 +921,8 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&stamps, ((size_t)grid * 8 * 5 + 8) * 8));
 
   Variant vs[] = {
-      {"ring2 dmaAC", ring2_kernel<4, false, 2>, 4, 512},
-      {"ring2 nost", ring2_kernel<4, false, 2, 0, 2>, 4, 512},
-      {"nost nodma", ring2_kernel<4, false, 2, 0, 2, 1>, 4, 512},
-      {"nost nodma nobar", ring2_kernel<4, false, 2, 0, 2, 3>, 4, 512},
-      {"nost nodma nords", ring2_kernel<4, false, 2, 0, 2, 5>, 4, 512},
-      {"nost nodma nobar nords", ring2_kernel<4, false, 2, 0, 2, 7>, 4, 512},
-      {"nost nobar", ring2_kernel<4, false, 2, 0, 2, 2>, 4, 512},
+      {"ring2 dmaAC", ring2_kernel<4, false, 2>, 4, 512, 0},
+      {"t8", t8_kernel<false>, 2, 512, 1},
   };
   Args a{A, B, C, K, K, N, M, N, K, nullptr};
   const double flop = 2.0 * M * N * K;
@@ -774,7 +933,8 @@ int main(int argc, char** argv) {
   for (size_t v = 0; v < sizeof(vs) / sizeof(vs[0]); ++v) {
     CHECK(hipMemset(C, 0, (size_t)M * N * 2));
     CHECK(hipMemset(err, 0, 4));
-    hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(vs[v].threads), 0, 0, a);
+    const int gv = vs[v].all_tiles ? (M / 256) * (N / 256) : grid;
+    hipLaunchKernelGGL(vs[v].fn, dim3(gv), dim3(vs[v].threads), 0, 0, a);
     CHECK(hipGetLastError());
     cmp_kernel<<<1024, 256>>>(C, R, (size_t)M * N, err);
     float e = 0;
@@ -783,9 +943,10 @@ int main(int argc, char** argv) {
   }
   for (int r = 0; r < rounds; ++r)
     for (size_t v = 0; v < sizeof(vs) / sizeof(vs[0]); ++v) {
-      for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(vs[v].threads), 0, 0, a);
+      const int gv = vs[v].all_tiles ? (M / 256) * (N / 256) : grid;
+      for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(vs[v].fn, dim3(gv), dim3(vs[v].threads), 0, 0, a);
       CHECK(hipEventRecord(e0));
-      for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(vs[v].fn, dim3(grid), dim3(vs[v].threads), 0, 0, a);
+      for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(vs[v].fn, dim3(gv), dim3(vs[v].threads), 0, 0, a);
       CHECK(hipEventRecord(e1));
       CHECK(hipEventSynchronize(e1));
       float ms;

@@ -86,3 +86,35 @@ def test_prewarm_runs_agree_across_ranks():
     for p in procs:
         p.join(timeout=60)
     assert got[0] == got[1] and got[0] >= 30, got
+
+
+def test_bench_rowwise_world2_cpu():
+    """--primitive tp_rowwise: GEMM + reduce-scatter; strong scaling, so the whole-job value is
+    the reference harness number itself (ranks share one [m,k]x[k,n])."""
+    from conftest import free_port
+
+    args = ["--steps", "3", "--warmup", "1", "-m", "256", "-n", "64", "-k", "64", "--dtype",
+            "float32", "--primitive", "tp_rowwise", "--algorithm", "row/pytorch(rccl+hipblaslt)"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", *args]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=_env())
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 2 and d["valid"] is True and d["scaling"] == "strong"
+    assert d["metric"].startswith("tp_rowwise")
+    assert abs(d["value"] - d["harness_tflops"]) < 1e-6
+    assert abs(d["per_gpu_tflops"] - d["harness_tflops"] / 2) < 1e-6
+
+
+def test_candidate_pools():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    col8 = bench.candidate_pool("tp_columnwise", "bfloat16", 8)
+    assert any(c[0] == "direct/ipc" for c in col8) and all(c[0][:4] != "row/" for c in col8)
+    row1 = bench.candidate_pool("tp_rowwise", "bfloat16", 1)
+    assert [c[0] for c in row1] == ["row/gemm (world=1)/hip", "row/gemm (world=1)/blas"]
+    fp8 = bench.candidate_pool("tp_columnwise", "float8_e4m3fn", 1)
+    labels = [c[0] for c in fp8]
+    assert "gemm (world=1)/hip/mx" in labels and not any("blas" in x for x in labels)
