@@ -934,6 +934,169 @@ __global__ __launch_bounds__(512) void gemm_tn_pp256_kernel(const GemmArgs p) {
   }
 }
 
+
+// ---------------------------------------------------------------- t8: 8-phase ping-pong kernel
+// 256x256 tile, BK = one 128-byte row (64 bf16 / 128 fp8 / 32 f32), 8 waves = 2 groups (wr) x 4
+// (wc), 128x64 per wave as 2x2 quadrants of 64x32 (cdna guide §5 "256^2 8-phase template",
+// T2+T3+T4+T5). Group 1 runs one barrier behind group 0, so between any two barriers one group
+// issues ds_reads + LDS-DMA while the other runs 16 MFMAs. K-tile data moves in 16 KB units of
+// 128 rows: UA0 = A rows {0-63, 128-191} (quadrant row mq=0 of both groups), UA1 = {64-127,
+// 192-255}, UB0 = B rows {wc*64 + 0..31}, UB1 = {wc*64 + 32..63}; wave w stages unit rows
+// [16w, 16w+16) (2 x 1 KB LDS-DMA). K-tile t lives in buffer t&1; phase p of a group
+// (intervals I_k between barriers, group g reads in I_{8t+2p+g}):
+//   p0: read A(mq0) + B(nq0), stage UA1(t+1)   p1: read B(nq1), stage UB0(t+1)
+//   p2: read A(mq1),          stage UA0(t+2)   p3: read B(nq0), stage UB1(t+2), vmcnt(4)
+// RAW: vmcnt(4) (2 unit slices in flight) before barrier 8(t+1) retires every slice of K-tile t+1
+// on every wave (group 1 in its p3 read section, group 0 after its p3 MFMAs).
+// WAR: each unit is restaged 3 intervals after its last read (reads retire by lgkmcnt(0) in the
+// next interval), e.g. UA0 of t is read in I_{8t}, I_{8t+1} and restaged in I_{8t+4}, I_{8t+5}.
+// Past the last K-tile the stage source is clamped to K-tile nk-1: identical bytes into units no
+// one reads again, so the vmcnt arithmetic stays uniform. B rows are loaded permuted within each
+// 32-row quadrant so a lane's two fragments of a quadrant hold 8 consecutive output columns (one
+// 16-byte store). Measured (profiles/r01/s2/lab/t8_vs_ring2.txt): 1425 TF at 8192^3 (+55 % over
+// the ring kernel, within 2 % of hipBLASLt), +7 % on the 65536x1024x1024 flagship.
+__device__ __forceinline__ int t8_perm(int t) { return 8 * ((t & 15) >> 2) + 4 * (t >> 4) + (t & 3); }
+
+template <class Mma, int OUT>
+__global__ __launch_bounds__(512) void gemm_tn_t8_kernel(const GemmArgs p) {
+  constexpr int ROWB = 128, UNIT = 128 * ROWB, STAGE = 4 * UNIT;
+  constexpr int UA0 = 0, UA1 = UNIT, UB0 = 2 * UNIT, UB1 = 3 * UNIT;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int tiles_n = p.N / 256, ntiles = (p.M / 256) * tiles_n;
+  const int wg = tile_index(p, ntiles);
+  const int64_t m0 = (int64_t)(wg / tiles_n) * 256, n0 = (int64_t)(wg % tiles_n) * 256;
+  const int esz = Mma::kElem;
+  const int nk = p.K * esz / ROWB;
+
+  // ---- LDS-DMA sources of this wave's slices (2 instructions x 8 rows per unit)
+  const int drow = lane >> 3, dpc = lane & 7;
+  const char* sA[2][2];
+  const char* sB[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int ur = wave * 16 + i * 8 + drow;
+    const int ch = (dpc ^ ((ur >> 1) & 7)) * 16;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int lr = (ur >> 6) * 128 + q * 64 + (ur & 63);
+      sA[q][i] = a_row(p, m0 + lr, esz) + ch;
+      const int lc = (ur >> 5) * 64 + q * 32 + t8_perm(ur & 31);
+      sB[q][i] = (const char*)p.b + (n0 + lc) * p.ldb * esz + ch;
+    }
+  }
+  wait_flag(p, m0);
+  auto stage = [&](const char* const* src, int unit_off, int kt, int buf) {
+    kt = kt < nk ? kt : nk - 1;
+    char* dst = smem + buf * STAGE + unit_off + wave * 16 * ROWB;
+    glds16(src[0] + (int64_t)kt * ROWB, dst);
+    glds16(src[1] + (int64_t)kt * ROWB, dst + 8 * ROWB);
+  };
+
+  // ---- fragment reads: unit row base + (lane & 15), logical chunk kk*4 + (lane >> 4)
+  const int frow = lane & 15, fq = lane >> 4, sw = (frow >> 1) & 7;
+  const int c0 = ((0 + fq) ^ sw) * 16, c1 = ((4 + fq) ^ sw) * 16;
+  const int aoff = (wr * 64 + frow) * ROWB, boff = (wc * 32 + frow) * ROWB;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  i32x4 aR[4][2], bR[2][2];
+  auto loadA = [&](const char* base, int mq) {
+    const char* r = base + (mq ? UA1 : UA0) + aoff;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      aR[f][0] = *(const i32x4*)(r + f * 16 * ROWB + c0);
+      aR[f][1] = *(const i32x4*)(r + f * 16 * ROWB + c1);
+    }
+  };
+  auto loadB = [&](const char* base, int nq) {
+    const char* r = base + (nq ? UB1 : UB0) + boff;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      bR[g][0] = *(const i32x4*)(r + g * 16 * ROWB + c0);
+      bR[g][1] = *(const i32x4*)(r + g * 16 * ROWB + c1);
+    }
+  };
+  auto comp = [&](int mq, int nq) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) Mma::step(acc[mq * 4 + f][nq * 2 + g], bR[g][kk], aR[f][kk]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+#define T8_BAR()                         \
+  do {                                   \
+    __builtin_amdgcn_sched_barrier(0);   \
+    __builtin_amdgcn_s_barrier();        \
+    __builtin_amdgcn_sched_barrier(0);   \
+  } while (0)
+
+  // ---- prologue: K-tile 0 whole, UA0 / UB1 of K-tile 1 in flight
+  stage(sA[0], UA0, 0, 0);
+  stage(sB[1], UB1, 0, 0);
+  stage(sA[1], UA1, 0, 0);
+  stage(sB[0], UB0, 0, 0);
+  stage(sA[0], UA0, 1, 1);
+  stage(sB[1], UB1, 1, 1);
+  wait_vm<4>();
+  T8_BAR();
+  const bool g1 = wr == 1;  // wave-uniform (wave came through readfirstlane)
+  if (g1) T8_BAR();
+  for (int t = 0; t < nk; ++t) {
+    const int b = t & 1, nb = b ^ 1;
+    const char* cur = smem + b * STAGE;
+    loadA(cur, 0);  // p0
+    loadB(cur, 0);
+    stage(sA[1], UA1, t + 1, nb);
+    T8_BAR();
+    comp(0, 0);
+    T8_BAR();
+    loadB(cur, 1);  // p1
+    stage(sB[0], UB0, t + 1, nb);
+    T8_BAR();
+    comp(0, 1);
+    T8_BAR();
+    loadA(cur, 1);  // p2
+    stage(sA[0], UA0, t + 2, b);
+    T8_BAR();
+    comp(1, 1);
+    T8_BAR();
+    loadB(cur, 0);  // p3
+    stage(sB[1], UB1, t + 2, b);
+    if (g1) wait_vm<4>();
+    T8_BAR();
+    comp(1, 0);
+    if (!g1) wait_vm<4>();
+    T8_BAR();
+  }
+  if (!g1) T8_BAR();
+#undef T8_BAR
+  wait_vm<0>();  // never leave an LDS-DMA in flight past the end of the workgroup
+
+  // ---- epilogue: a lane holds columns 8*fq .. 8*fq+7 of each 32-column quadrant
+  constexpr int OSZ = out_size<OUT>();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int64_t row = m0 + wr * 128 + (i >> 2) * 64 + (i & 3) * 16 + frow;
+    char* crow = (char*)p.c + map_row(row, p.c_grp, p.c_gstride) * p.ldc * OSZ;
+#pragma unroll
+    for (int nq = 0; nq < 2; ++nq) {
+      char* dst = crow + (n0 + wc * 64 + nq * 32 + fq * 8) * OSZ;
+      if (p.act == ACT_NONE) Store8<OUT>::st(dst, acc[i][nq * 2], acc[i][nq * 2 + 1]);
+      else Store8<OUT>::st(dst, act4(acc[i][nq * 2], p.act), act4(acc[i][nq * 2 + 1], p.act));
+    }
+  }
+}
+
 // ---------------------------------------------------------------- MX-fp8 (block-scaled) kernel
 // One v_mfma_scale_f32_16x16x128_f8f6f4 per 128-byte K-row (unit E8M0 scales = 127): 2x the bf16
 // MFMA rate (MI355X_MICROARCH.md "Matrix cores"). Same staging as above.
@@ -1160,6 +1323,16 @@ hipError_t launch_ring(const GemmArgs& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+// t8 takes whole 256x256 tiles (flags, grouped rows, shard tables and activations allowed)
+bool t8_ok(const GemmArgs& p) { return p.M % 256 == 0 && p.N % 256 == 0; }
+
+template <class Mma, int OUT>
+hipError_t launch_t8(const GemmArgs& p, hipStream_t s) {
+  const int tiles = (p.M / 256) * (p.N / 256);
+  hipLaunchKernelGGL((gemm_tn_t8_kernel<Mma, OUT>), dim3(tiles), dim3(512), 0, s, p);
+  return hipGetLastError();
+}
+
 template <class Mma, int OUT>
 hipError_t launch_pp256(const GemmArgs& p, hipStream_t s) {
   const int tiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
@@ -1170,6 +1343,9 @@ hipError_t launch_pp256(const GemmArgs& p, hipStream_t s) {
 template <class Mma, int OUT>
 hipError_t launch_cfg(const GemmArgs& p, int tile, hipStream_t s) {
   switch (tile) {
+    case TILE_T8:
+      if (t8_ok(p)) return launch_t8<Mma, OUT>(p, s);
+      return launch_tiled<Mma, OUT, 256, 256, 2, 4, true>(p, s);
     case TILE_R256:
       if (ring_ok(p)) return launch_ring<Mma, OUT>(p, s);
       return launch_tiled<Mma, OUT, 256, 256, 2, 4, true>(p, s);
@@ -1216,7 +1392,7 @@ hipError_t launch_mx_cfg(const GemmArgs& p, int tile, hipStream_t s) {
     case TILE_I256W4: return launch_mx<OUT, 256, 256, 2, 2>(p, s);
     case TILE_PI256: return launch_mx<OUT, 256, 256, 2, 4>(p, s);
     case TILE_PI256W4: return launch_mx<OUT, 256, 256, 2, 2>(p, s);
-    case TILE_R256: return launch_mx<OUT, 256, 256, 2, 4>(p, s);
+    case TILE_R256: case TILE_T8: return launch_mx<OUT, 256, 256, 2, 4>(p, s);
     case TILE_P128: return launch_mx<OUT, 128, 128, 2, 2>(p, s);
     case TILE_256x128_W4: return launch_mx<OUT, 256, 128, 2, 2>(p, s);
     default: return hipErrorInvalidValue;

@@ -61,8 +61,11 @@ int choose_tile(int64_t M, int64_t N, int64_t K, int din) {
   // one 256x256 tile per CU and the K extent is short (<= 2 KiB per row, e.g. K <= 1024 bf16:
   // the flagship 65536x1024x1024 and the row-parallel 16384x8192x1024 partial); long K prefers
   // the 128-byte-row interleaved kernel; fewer tiles than CUs want 128x128 blocks.
+  // The 8-phase ping-pong kernel (t8) beats both on whole 256x256 tiles at every K measured
+  // (profiles/r01/s2/lab/t8_vs_ring2.txt) once the grid covers most of the CUs.
   auto tiles = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
   const int64_t kbytes = K * dtype_size(din);
+  if (M % 256 == 0 && N % 256 == 0 && tiles(256, 256) >= 192) return TILE_T8;
   if (M % 256 == 0 && N % 256 == 0 && tiles(256, 256) >= 256 && kbytes <= 2048) return TILE_R256;
   if (tiles(256, 256) >= 384) return TILE_I256;
   if (tiles(256, 128) >= 384) return TILE_256x128;
@@ -83,9 +86,12 @@ hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mo
     if (tile == TILE_PP256 || tile == TILE_P256 || tile == TILE_PI256 || tile == TILE_PI256W4)
       tile = TILE_I256;
     if (tile == TILE_P128) tile = TILE_I128;
-    if (tile == TILE_AUTO || tile == TILE_R256)
-      tile = (p.M % 256 == 0 && p.N % 256 == 0 && p.shard_rows % 256 == 0) ? TILE_R256
+    if (tile == TILE_AUTO)
+      tile = (p.M % 256 == 0 && p.N % 256 == 0 && p.shard_rows % 256 == 0) ? TILE_T8
                                                                               : TILE_128x128;
+    if ((tile == TILE_R256 || tile == TILE_T8) &&
+        !(p.M % 256 == 0 && p.N % 256 == 0 && p.shard_rows % 256 == 0))
+      tile = TILE_128x128;
     if (mode == GEMM_MODE_GENERIC || !gemm_fast_path_ok(p, din, dout)) return hipErrorNotSupported;
   }
   if (mode == GEMM_MODE_BLAS) {
