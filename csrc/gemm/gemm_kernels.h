@@ -7,6 +7,8 @@
 #include <hip/hip_fp16.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "gemm.h"
 
 namespace ddlb {
@@ -222,7 +224,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_kernel(const GemmArgs p) 
 
   wait_flag(p, map_row(m0, p.a_grp, p.a_gstride));
 
-  auto stage = [&](int buf, int kt) {
+  auto stage = [&](int buf, int kt) __attribute__((always_inline)) {
     char* base = smem + buf * STAGE;
     const int64_t koff = (int64_t)kt * ROWB;
 #pragma unroll
@@ -240,7 +242,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_kernel(const GemmArgs p) 
 #pragma unroll
     for (int j = 0; j < NR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto compute = [&](int buf) {
+  auto compute = [&](int buf) __attribute__((always_inline)) {
     const char* As = smem + buf * STAGE;
     const char* Bs = As + A_BYTES;
 #pragma unroll
@@ -266,7 +268,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_kernel(const GemmArgs p) 
   // DMA per MR*NR/(LA+LB) MFMAs), so its issue cost hides behind the matrix pipe instead of
   // forming a burst at the top of every K-tile (cdna guide: "the per-phase interleave is the
   // lever"). The DMA writes the other LDS buffer, so it may be placed after this tile's reads.
-  auto compute_ilv = [&](int buf, int next_kt) {
+  auto compute_ilv = [&](int buf, int next_kt) __attribute__((always_inline)) {
     // First half: MFMAs on the c4=0 fragments, with the next tile's LDS-DMA (1 per PER MFMAs)
     // and the c4=4 fragment reads (into a second register set) interleaved between them.
     constexpr int NDMA = LA + LB, NRD = MR + NR, NQ = MR * NR;
@@ -283,11 +285,11 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_kernel(const GemmArgs p) 
 #pragma unroll
     for (int j = 0; j < NR; ++j)
       bf0[j] = *(const i32x4*)(Bs + (wn * TN + j * 16 + frow) * ROWB + ch0);
-    auto rd1 = [&](int r) {
+    auto rd1 = [&](int r) __attribute__((always_inline)) {
       if (r < MR) af1[r] = *(const i32x4*)(As + (wm * TM + r * 16 + frow) * ROWB + ch1);
       else bf1[r - MR] = *(const i32x4*)(Bs + (wn * TN + (r - MR) * 16 + frow) * ROWB + ch1);
     };
-    auto dma = [&](int d) {
+    auto dma = [&](int d) __attribute__((always_inline)) {
       if (d < LA) glds16(aptr[d] + koff, nbase + (wave * LA + d) * 1024);
       else glds16(bptr[d - LA] + koff, nbase + A_BYTES + (wave * LB + d - LA) * 1024);
     };
@@ -382,7 +384,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_persist_kernel(const Gemm
   const char* aptr[LA];
   const char* bptr[LB];
   int cur_tile = -1;
-  auto set_tile = [&](int i) {  // i-th tile of this block -> source pointers
+  auto set_tile = [&](int i) __attribute__((always_inline)) {  // i-th tile of this block -> source pointers
     const int wg = tile_index_virtual(p, (int)blockIdx.x + i * (int)gridDim.x, ntiles);
     const int64_t m0 = (int64_t)(wg / tiles_n) * BM, n0 = (int64_t)(wg % tiles_n) * BN;
 #pragma unroll
@@ -399,7 +401,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_persist_kernel(const Gemm
       bptr[r] = (const char*)p.b + (n0 + row) * p.ldb * esz + chunk * 16;
     }
   };
-  auto stage = [&](int buf, int g) {
+  auto stage = [&](int buf, int g) __attribute__((always_inline)) {
     const int ti = g / nk, kt = g - ti * nk;
     if (ti != cur_tile) {
       set_tile(ti);
@@ -421,7 +423,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_persist_kernel(const Gemm
 #pragma unroll
     for (int j = 0; j < NR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto compute = [&](int buf) {
+  auto compute = [&](int buf) __attribute__((always_inline)) {
     const char* As = smem + buf * STAGE;
     const char* Bs = As + A_BYTES;
 #pragma unroll
@@ -443,7 +445,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_persist_kernel(const Gemm
     }
   };
   constexpr int OSZ = out_size<OUT>();
-  auto epilogue = [&](int ti) {
+  auto epilogue = [&](int ti) __attribute__((always_inline)) {
     const int wg = tile_index_virtual(p, (int)blockIdx.x + ti * (int)gridDim.x, ntiles);
     const int64_t m0 = (int64_t)(wg / tiles_n) * BM, n0 = (int64_t)(wg % tiles_n) * BN;
 #pragma unroll
@@ -461,7 +463,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_persist_kernel(const Gemm
 
   // interleaved compute (see gemm_tn_kernel::compute_ilv): next step's DMA + second-half
   // fragment reads issued between the first-half MFMAs
-  auto compute_ilv = [&](int buf, int64_t koff) {
+  auto compute_ilv = [&](int buf, int64_t koff) __attribute__((always_inline)) {
     constexpr int NDMA = LA + LB, NRD = MR + NR, NQ = MR * NR;
     constexpr int PER = NQ / NDMA > 0 ? NQ / NDMA : 1;
     const char* As = smem + buf * STAGE;
@@ -475,11 +477,11 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_persist_kernel(const Gemm
 #pragma unroll
     for (int j = 0; j < NR; ++j)
       bf0[j] = *(const i32x4*)(Bs + (wn * TN + j * 16 + frow) * ROWB + ch0);
-    auto rd1 = [&](int r) {
+    auto rd1 = [&](int r) __attribute__((always_inline)) {
       if (r < MR) af1[r] = *(const i32x4*)(As + (wm * TM + r * 16 + frow) * ROWB + ch1);
       else bf1[r - MR] = *(const i32x4*)(Bs + (wn * TN + (r - MR) * 16 + frow) * ROWB + ch1);
     };
-    auto dma = [&](int d) {
+    auto dma = [&](int d) __attribute__((always_inline)) {
       if (d < LA) glds16(aptr[d] + koff, nbase + (wave * LA + d) * 1024);
       else glds16(bptr[d - LA] + koff, nbase + A_BYTES + (wave * LB + d - LA) * 1024);
     };
@@ -614,7 +616,7 @@ __global__ __launch_bounds__(512) void gemm_tn_ring_kernel(const GemmArgs p) {
   const char* abase[LA];
   const char* bbase[LB];
   int dma_tile = -1;
-  auto set_dma_tile = [&](int ti) {
+  auto set_dma_tile = [&](int ti) __attribute__((always_inline)) {
     const int wg = tile_index_virtual(p, (int)blockIdx.x + ti * (int)gridDim.x, ntiles);
     const int64_t m0 = (int64_t)(wg / tiles_n) * BM, n0 = (int64_t)(wg % tiles_n) * BN;
 #pragma unroll
@@ -641,7 +643,7 @@ __global__ __launch_bounds__(512) void gemm_tn_ring_kernel(const GemmArgs p) {
     }
     return (int64_t)(g - ti * nk) * ROWB;
   };
-  auto dma = [&](int d, int64_t koff, char* base) {
+  auto dma = [&](int d, int64_t koff, char* base) __attribute__((always_inline)) {
     if (d < LA) glds16(abase[d] + koff, base + (wave * LA + d) * 1024);
     else glds16(bbase[d - LA] + koff, base + A_BYTES + (wave * LB + d - LA) * 1024);
   };
@@ -815,7 +817,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pp256_kernel(const GemmArgs p) {
   wait_flag(p, map_row(m0, p.a_grp, p.a_gstride));
 
   // part 0: A rows 0-15 + B rows 0-15 of this wave's 32; part 1: the other 16 of each
-  auto stage_part = [&](int buf, int kt, int part) {
+  auto stage_part = [&](int buf, int kt, int part) __attribute__((always_inline)) {
     char* base = smem + buf * STAGE;
     const int64_t koff = (int64_t)kt * ROWB;
 #pragma unroll
@@ -836,7 +838,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pp256_kernel(const GemmArgs p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   i32x4 aR[4][2], bR[2][2];
 
-  auto loadA = [&](const char* As, int mq) {
+  auto loadA = [&](const char* As, int mq) __attribute__((always_inline)) {
 #pragma unroll
     for (int f = 0; f < 4; ++f) {
       const char* r = As + arow0 + (mq * 64 + f * 16) * ROWB;
@@ -844,7 +846,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pp256_kernel(const GemmArgs p) {
       aR[f][1] = *(const i32x4*)(r + c1);
     }
   };
-  auto loadB = [&](const char* Bs, int nq) {
+  auto loadB = [&](const char* Bs, int nq) __attribute__((always_inline)) {
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
       const char* r = Bs + brow0 + (nq * 32 + f * 16) * ROWB;
@@ -852,7 +854,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pp256_kernel(const GemmArgs p) {
       bR[f][1] = *(const i32x4*)(r + c1);
     }
   };
-  auto comp = [&](int mq, int nq) {
+  auto comp = [&](int mq, int nq) __attribute__((always_inline)) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -988,7 +990,7 @@ __global__ __launch_bounds__(512) void gemm_tn_t8_kernel(const GemmArgs p) {
     }
   }
   wait_flag(p, m0);
-  auto stage = [&](const char* const* src, int unit_off, int kt, int buf) {
+  auto stage = [&](const char* const* src, int unit_off, int kt, int buf) __attribute__((always_inline)) {
     kt = kt < nk ? kt : nk - 1;
     char* dst = smem + buf * STAGE + unit_off + wave * 16 * ROWB;
     glds16(src[0] + (int64_t)kt * ROWB, dst);
@@ -1005,7 +1007,7 @@ __global__ __launch_bounds__(512) void gemm_tn_t8_kernel(const GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   i32x4 aR[4][2], bR[2][2];
-  auto loadA = [&](const char* base, int mq) {
+  auto loadA = [&](const char* base, int mq) __attribute__((always_inline)) {
     const char* r = base + (mq ? UA1 : UA0) + aoff;
 #pragma unroll
     for (int f = 0; f < 4; ++f) {
@@ -1013,7 +1015,7 @@ __global__ __launch_bounds__(512) void gemm_tn_t8_kernel(const GemmArgs p) {
       aR[f][1] = *(const i32x4*)(r + f * 16 * ROWB + c1);
     }
   };
-  auto loadB = [&](const char* base, int nq) {
+  auto loadB = [&](const char* base, int nq) __attribute__((always_inline)) {
     const char* r = base + (nq ? UB1 : UB0) + boff;
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
@@ -1021,7 +1023,7 @@ __global__ __launch_bounds__(512) void gemm_tn_t8_kernel(const GemmArgs p) {
       bR[g][1] = *(const i32x4*)(r + g * 16 * ROWB + c1);
     }
   };
-  auto comp = [&](int mq, int nq) {
+  auto comp = [&](int mq, int nq) __attribute__((always_inline)) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
@@ -1097,6 +1099,200 @@ __global__ __launch_bounds__(512) void gemm_tn_t8_kernel(const GemmArgs p) {
   }
 }
 
+
+// ---------------------------------------------------------------- pt8: persistent t8
+// One workgroup per CU streams its tiles' K-tiles back to back (stream index h = tile * nk + kt;
+// the t8 unit schedule above runs unchanged across tile boundaries, so only the first tile pays
+// the staging fill). A tile's C quadrants are stored right after their last MFMAs (quadrant (0,0)
+// in phase 0 of the tile's last K-tile, ..., (1,0) in phase 3), which spreads the C burst over a
+// K-tile; the stores issued after that K-tile's UB0 stage are allowed to stay in flight across
+// its vmcnt (vmcnt counts loads, LDS-DMA and stores together, in issue order). The stage cursors
+// advance incrementally (no integer division in the loop) and the tile's last K-tile is a
+// separate instantiation of the body, so the steady-state loop carries no store code.
+// Measured (scripts/lab, profiles/r01/s2/lab/): 65536x1024x1024 bf16 0.1116 ms vs t8 0.1163.
+template <class Mma, int OUT>
+__global__ __launch_bounds__(512) void gemm_tn_pt8_kernel(const GemmArgs p) {
+  constexpr int ROWB = 128, UNIT = 128 * ROWB, STAGE = 4 * UNIT;
+  constexpr int UA0 = 0, UA1 = UNIT, UB0 = 2 * UNIT, UB1 = 3 * UNIT;
+  constexpr int NS = 4 * Store8<OUT>::kStores;  // C store instructions per quadrant per wave
+  constexpr int OSZ = out_size<OUT>();
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int tiles_n = p.N / 256, ntiles = (p.M / 256) * tiles_n;
+  const int esz = Mma::kElem;
+  const int nk = p.K * esz / ROWB;
+  const int my_tiles =
+      ((int)blockIdx.x < ntiles) ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  if (my_tiles == 0) return;
+
+  const int drow = lane >> 3, dpc = lane & 7;
+  const char* sA[2][2];
+  const char* sB[2][2];
+  int src_tile = -1;
+  auto tile_origin = [&](int ti, int64_t& m0, int64_t& n0) __attribute__((always_inline)) {
+    const int wg = tile_index_virtual(p, (int)blockIdx.x + ti * (int)gridDim.x, ntiles);
+    m0 = (int64_t)(wg / tiles_n) * 256;
+    n0 = (int64_t)(wg % tiles_n) * 256;
+  };
+  auto set_src = [&](int ti) __attribute__((always_inline)) {
+    int64_t m0, n0;
+    tile_origin(ti, m0, n0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int ur = wave * 16 + i * 8 + drow;
+      const int ch = (dpc ^ ((ur >> 1) & 7)) * 16;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int lr = (ur >> 6) * 128 + q * 64 + (ur & 63);
+        sA[q][i] = a_row(p, m0 + lr, esz) + ch;
+        const int lc = (ur >> 5) * 64 + q * 32 + t8_perm(ur & 31);
+        sB[q][i] = (const char*)p.b + (n0 + lc) * p.ldb * esz + ch;
+      }
+    }
+  };
+  // stage stream cursors: (tile, K-tile) of h+1 and h+2, clamped to the last K-tile of the last
+  // tile past the end of the stream (identical bytes into units no one reads again)
+  struct Cur { int ti, kt; };
+  auto adv = [&](Cur& c) __attribute__((always_inline)) {
+    if (c.ti == my_tiles - 1 && c.kt == nk - 1) return;
+    if (++c.kt == nk) { c.kt = 0; ++c.ti; }
+  };
+  auto stage = [&](int which, int unit_off, Cur c, int buf) __attribute__((always_inline)) {  // 0/1: A mq0/mq1, 2/3: B nq0/nq1
+    if (c.ti != src_tile) {
+      set_src(c.ti);
+      src_tile = c.ti;
+    }
+    const char* const* src = which < 2 ? sA[which] : sB[which - 2];
+    char* dst = smem + buf * STAGE + unit_off + wave * 16 * ROWB;
+    glds16(src[0] + (int64_t)c.kt * ROWB, dst);
+    glds16(src[1] + (int64_t)c.kt * ROWB, dst + 8 * ROWB);
+  };
+
+  const int frow = lane & 15, fq = lane >> 4, sw = (frow >> 1) & 7;
+  const int c0 = ((0 + fq) ^ sw) * 16, c1 = ((4 + fq) ^ sw) * 16;
+  const int aoff = (wr * 64 + frow) * ROWB, boff = (wc * 32 + frow) * ROWB;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  i32x4 aR[4][2], bR[2][2];
+  auto loadA = [&](const char* base, int mq) __attribute__((always_inline)) {
+    const char* r = base + (mq ? UA1 : UA0) + aoff;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      aR[f][0] = *(const i32x4*)(r + f * 16 * ROWB + c0);
+      aR[f][1] = *(const i32x4*)(r + f * 16 * ROWB + c1);
+    }
+  };
+  auto loadB = [&](const char* base, int nq) __attribute__((always_inline)) {
+    const char* r = base + (nq ? UB1 : UB0) + boff;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      bR[g][0] = *(const i32x4*)(r + g * 16 * ROWB + c0);
+      bR[g][1] = *(const i32x4*)(r + g * 16 * ROWB + c1);
+    }
+  };
+  auto comp = [&](int mq, int nq) __attribute__((always_inline)) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) Mma::step(acc[mq * 4 + f][nq * 2 + g], bR[g][kk], aR[f][kk]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  int ti = 0;
+  auto store_q = [&](int mq, int nq) __attribute__((always_inline)) {  // store + clear quadrant (mq, nq) of tile ti
+    int64_t m0, n0;
+    tile_origin(ti, m0, n0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const int i = mq * 4 + f;
+      const int64_t row = m0 + wr * 128 + mq * 64 + f * 16 + frow;
+      char* dst = (char*)p.c + map_row(row, p.c_grp, p.c_gstride) * p.ldc * OSZ +
+                  (n0 + wc * 64 + nq * 32 + fq * 8) * OSZ;
+      if (p.act == ACT_NONE) Store8<OUT>::st(dst, acc[i][nq * 2], acc[i][nq * 2 + 1]);
+      else Store8<OUT>::st(dst, act4(acc[i][nq * 2], p.act), act4(acc[i][nq * 2 + 1], p.act));
+      acc[i][nq * 2] = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc[i][nq * 2 + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+#define T8_BAR()                         \
+  do {                                   \
+    __builtin_amdgcn_sched_barrier(0);   \
+    __builtin_amdgcn_s_barrier();        \
+    __builtin_amdgcn_sched_barrier(0);   \
+  } while (0)
+
+  Cur q0{0, 0}, q1{0, 0};
+  adv(q1);
+  stage(0, UA0, q0, 0);
+  stage(3, UB1, q0, 0);
+  stage(1, UA1, q0, 0);
+  stage(2, UB0, q0, 0);
+  stage(0, UA0, q1, 1);
+  stage(3, UB1, q1, 1);
+  Cur q2 = q1;
+  adv(q2);
+  wait_vm<4>();
+  T8_BAR();
+  const bool g1 = wr == 1;  // wave-uniform (wave came through readfirstlane)
+  if (g1) T8_BAR();
+  // one K-tile of the stream; LAST = the tile's last K-tile (stores its quadrants)
+  auto iter = [&](int h, auto last_tag) __attribute__((always_inline)) {
+    constexpr bool LAST = decltype(last_tag)::value;
+    const int b = h & 1, nb = b ^ 1;
+    const char* cur = smem + b * STAGE;
+    loadA(cur, 0);  // p0
+    loadB(cur, 0);
+    stage(1, UA1, q1, nb);
+    T8_BAR();
+    comp(0, 0);
+    if constexpr (LAST) store_q(0, 0);
+    T8_BAR();
+    loadB(cur, 1);  // p1
+    stage(2, UB0, q1, nb);
+    T8_BAR();
+    comp(0, 1);
+    if constexpr (LAST) store_q(0, 1);
+    T8_BAR();
+    loadA(cur, 1);  // p2
+    stage(0, UA0, q2, b);
+    T8_BAR();
+    comp(1, 1);
+    if constexpr (LAST) store_q(1, 1);
+    T8_BAR();
+    loadB(cur, 0);  // p3
+    stage(3, UB1, q2, b);
+    // younger than UB0(h+1): UA0/UB1(h+2) and, in a tile's last K-tile, the Q01 + Q11 stores
+    if (g1) wait_vm<LAST ? 4 + 2 * NS : 4>();
+    T8_BAR();
+    comp(1, 0);
+    if constexpr (LAST) store_q(1, 0);
+    if (!g1) wait_vm<LAST ? 4 + 3 * NS : 4>();  // ... and Q10
+    T8_BAR();
+    q1 = q2;
+    adv(q2);
+  };
+  int h = 0;
+  for (ti = 0; ti < my_tiles; ++ti) {
+    for (int t = 0; t < nk - 1; ++t, ++h) iter(h, std::integral_constant<bool, false>{});
+    iter(h, std::integral_constant<bool, true>{});
+    ++h;
+  }
+  if (!g1) T8_BAR();
+#undef T8_BAR
+  wait_vm<0>();  // never leave an LDS-DMA in flight past the end of the workgroup
+}
+
 // ---------------------------------------------------------------- MX-fp8 (block-scaled) kernel
 // One v_mfma_scale_f32_16x16x128_f8f6f4 per 128-byte K-row (unit E8M0 scales = 127): 2x the bf16
 // MFMA rate (MI355X_MICROARCH.md "Matrix cores"). Same staging as above.
@@ -1132,7 +1328,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_mxfp8_kernel(const GemmAr
     bptr[i] = (const char*)p.b + gr * p.ldb + chunk * 16;
   }
   wait_flag(p, map_row(m0, p.a_grp, p.a_gstride));
-  auto stage = [&](int buf, int kt) {
+  auto stage = [&](int buf, int kt) __attribute__((always_inline)) {
     char* base = smem + buf * STAGE;
     const int64_t koff = (int64_t)kt * ROWB;
 #pragma unroll
@@ -1147,7 +1343,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_mxfp8_kernel(const GemmAr
   for (int i = 0; i < MR; ++i)
 #pragma unroll
     for (int j = 0; j < NR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto compute = [&](int buf) {
+  auto compute = [&](int buf) __attribute__((always_inline)) {
     const char* As = smem + buf * STAGE;
     const char* Bs = As + A_BYTES;
     const int c0 = ((fq) ^ swz) * 16, c1 = ((4 + fq) ^ swz) * 16;
@@ -1334,6 +1530,17 @@ hipError_t launch_t8(const GemmArgs& p, hipStream_t s) {
 }
 
 template <class Mma, int OUT>
+hipError_t launch_pt8(const GemmArgs& p, hipStream_t s) {
+  const int tiles = (p.M / 256) * (p.N / 256);
+  int grid = num_cus();
+  grid = (grid / 8) * 8;  // blockIdx % 8 == XCD group for every virtual tile id
+  if (grid > tiles) grid = tiles;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL((gemm_tn_pt8_kernel<Mma, OUT>), dim3(grid), dim3(512), 0, s, p);
+  return hipGetLastError();
+}
+
+template <class Mma, int OUT>
 hipError_t launch_pp256(const GemmArgs& p, hipStream_t s) {
   const int tiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
   hipLaunchKernelGGL((gemm_tn_pp256_kernel<Mma, OUT>), dim3(tiles), dim3(512), 0, s, p);
@@ -1343,6 +1550,10 @@ hipError_t launch_pp256(const GemmArgs& p, hipStream_t s) {
 template <class Mma, int OUT>
 hipError_t launch_cfg(const GemmArgs& p, int tile, hipStream_t s) {
   switch (tile) {
+    case TILE_PT8:  // persistent: no arrival flags (a block's tiles are fixed up front)
+      if (t8_ok(p) && p.flags == nullptr) return launch_pt8<Mma, OUT>(p, s);
+      if (t8_ok(p)) return launch_t8<Mma, OUT>(p, s);
+      return launch_tiled<Mma, OUT, 256, 256, 2, 4, true>(p, s);
     case TILE_T8:
       if (t8_ok(p)) return launch_t8<Mma, OUT>(p, s);
       return launch_tiled<Mma, OUT, 256, 256, 2, 4, true>(p, s);
@@ -1392,7 +1603,7 @@ hipError_t launch_mx_cfg(const GemmArgs& p, int tile, hipStream_t s) {
     case TILE_I256W4: return launch_mx<OUT, 256, 256, 2, 2>(p, s);
     case TILE_PI256: return launch_mx<OUT, 256, 256, 2, 4>(p, s);
     case TILE_PI256W4: return launch_mx<OUT, 256, 256, 2, 2>(p, s);
-    case TILE_R256: case TILE_T8: return launch_mx<OUT, 256, 256, 2, 4>(p, s);
+    case TILE_R256: case TILE_T8: case TILE_PT8: return launch_mx<OUT, 256, 256, 2, 4>(p, s);
     case TILE_P128: return launch_mx<OUT, 128, 128, 2, 2>(p, s);
     case TILE_256x128_W4: return launch_mx<OUT, 256, 128, 2, 2>(p, s);
     default: return hipErrorInvalidValue;

@@ -65,6 +65,10 @@ int choose_tile(int64_t M, int64_t N, int64_t K, int din) {
   // (profiles/r01/s2/lab/t8_vs_ring2.txt) once the grid covers most of the CUs.
   auto tiles = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
   const int64_t kbytes = K * dtype_size(din);
+  // Its persistent form (pt8) wins on short K with a narrow N (the flagship 65536x1024x1024:
+  // 0.1116 vs 0.1163 ms) and loses ~5 % on a wide N (16384x8192x1024).
+  if (M % 256 == 0 && N % 256 == 0 && tiles(256, 256) >= 256 && kbytes <= 2048 && N <= 2048)
+    return TILE_PT8;
   if (M % 256 == 0 && N % 256 == 0 && tiles(256, 256) >= 192) return TILE_T8;
   if (M % 256 == 0 && N % 256 == 0 && tiles(256, 256) >= 256 && kbytes <= 2048) return TILE_R256;
   if (tiles(256, 256) >= 384) return TILE_I256;
@@ -86,12 +90,12 @@ hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mo
     if (tile == TILE_PP256 || tile == TILE_P256 || tile == TILE_PI256 || tile == TILE_PI256W4)
       tile = TILE_I256;
     if (tile == TILE_P128) tile = TILE_I128;
-    if (tile == TILE_AUTO)
-      tile = (p.M % 256 == 0 && p.N % 256 == 0 && p.shard_rows % 256 == 0) ? TILE_T8
-                                                                              : TILE_128x128;
-    if ((tile == TILE_R256 || tile == TILE_T8) &&
-        !(p.M % 256 == 0 && p.N % 256 == 0 && p.shard_rows % 256 == 0))
-      tile = TILE_128x128;
+    const bool whole = p.M % 256 == 0 && p.N % 256 == 0 && p.shard_rows % 256 == 0;
+    if (tile == TILE_AUTO) {
+      tile = choose_tile(p.M, p.N, p.K, din);
+      if (tile != TILE_PT8 && tile != TILE_R256) tile = TILE_T8;
+    }
+    if ((tile == TILE_R256 || tile == TILE_T8 || tile == TILE_PT8) && !whole) tile = TILE_128x128;
     if (mode == GEMM_MODE_GENERIC || !gemm_fast_path_ok(p, din, dout)) return hipErrorNotSupported;
   }
   if (mode == GEMM_MODE_BLAS) {

@@ -15,6 +15,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
 #define CHECK(x)                                                                      \
@@ -851,6 +852,193 @@ __global__ __launch_bounds__(512) void t8_kernel(const Args p) {
   }
 }
 
+
+// pt8: persistent t8. One workgroup per CU streams its tiles' K-tiles back to back (stream index
+// h = tile * nk + kt; the unit schedule of t8 runs across tile boundaries, so only the first tile
+// pays the ring fill). A tile's C quadrants are stored right after their last MFMAs (quadrant
+// (0,0) in phase 0 of the tile's last K-tile, ..., (1,0) in phase 3), spreading the C burst over
+// a K-tile; stores issued after the UB0 stage of that K-tile stay in flight across its vmcnt.
+template <bool STAMP>
+__global__ __launch_bounds__(512) void pt8_kernel(const Args p) {
+  constexpr int ROWB = 128, UNIT = 128 * ROWB, STAGE = 4 * UNIT;
+  constexpr int UA0 = 0, UA1 = UNIT, UB0 = 2 * UNIT, UB1 = 3 * UNIT;
+  constexpr int NS = 4;  // 16-byte C stores per quadrant per wave (bf16 out)
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int tiles_n = p.N / 256, ntiles = (p.M / 256) * tiles_n;
+  const int nk = p.K / 64;
+  const int my_tiles =
+      ((int)blockIdx.x < ntiles) ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int total = my_tiles * nk;
+  if (total == 0) return;
+
+  const int drow = lane >> 3, dpc = lane & 7;
+  const char* sA[2][2];
+  const char* sB[2][2];
+  int src_tile = -1;
+  auto set_src = [&](int ti) {
+    const int wg = xcd_remap((int)blockIdx.x + ti * (int)gridDim.x, ntiles);
+    const int64_t m0 = (int64_t)(wg / tiles_n) * 256, n0 = (int64_t)(wg % tiles_n) * 256;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int ur = wave * 16 + i * 8 + drow;
+      const int ch = (dpc ^ ((ur >> 1) & 7)) * 16;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int lr = (ur >> 6) * 128 + q * 64 + (ur & 63);
+        sA[q][i] = (const char*)p.a + (m0 + lr) * p.lda * 2 + ch;
+        const int lc = (ur >> 5) * 64 + q * 32 + t8_perm(ur & 31);
+        sB[q][i] = (const char*)p.b + (n0 + lc) * p.ldb * 2 + ch;
+      }
+    }
+  };
+  // stage stream cursors (no integer division in the loop): (ti, kt) of h+1 and h+2, clamped
+  // to the last K-tile of the last tile past the end of the stream
+  struct Cur { int ti, kt; };
+  auto adv = [&](Cur& c) {
+    if (c.ti == my_tiles - 1 && c.kt == nk - 1) return;
+    if (++c.kt == nk) { c.kt = 0; ++c.ti; }
+  };
+  auto stage = [&](int which, int unit_off, Cur c, int buf) {  // which: 0 A mq0, 1 A mq1, 2 B nq0, 3 B nq1
+    const int ti = c.ti, kt = c.kt;
+    if (ti != src_tile) {
+      set_src(ti);
+      src_tile = ti;
+    }
+    const char* const* src = which < 2 ? sA[which] : sB[which - 2];
+    char* dst = smem + buf * STAGE + unit_off + wave * 16 * ROWB;
+    glds16(src[0] + (int64_t)kt * ROWB, dst);
+    glds16(src[1] + (int64_t)kt * ROWB, dst + 8 * ROWB);
+  };
+
+  const int frow = lane & 15, fq = lane >> 4, sw = (frow >> 1) & 7;
+  const int c0 = ((0 + fq) ^ sw) * 16, c1 = ((4 + fq) ^ sw) * 16;
+  const int aoff = (wr * 64 + frow) * ROWB, boff = (wc * 32 + frow) * ROWB;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  i32x4 aR[4][2], bR[2][2];
+  auto loadA = [&](const char* base, int mq) {
+    const char* r = base + (mq ? UA1 : UA0) + aoff;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      aR[f][0] = *(const i32x4*)(r + f * 16 * ROWB + c0);
+      aR[f][1] = *(const i32x4*)(r + f * 16 * ROWB + c1);
+    }
+  };
+  auto loadB = [&](const char* base, int nq) {
+    const char* r = base + (nq ? UB1 : UB0) + boff;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      bR[g][0] = *(const i32x4*)(r + g * 16 * ROWB + c0);
+      bR[g][1] = *(const i32x4*)(r + g * 16 * ROWB + c1);
+    }
+  };
+  auto comp = [&](int mq, int nq) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+          acc[mq * 4 + f][nq * 2 + g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8, bR[g][kk]), __builtin_bit_cast(bf16x8, aR[f][kk]),
+              acc[mq * 4 + f][nq * 2 + g], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // store + clear quadrant (mq, nq) of tile ti
+  auto store_q = [&](int ti, int mq, int nq) {
+    const int wg = xcd_remap((int)blockIdx.x + ti * (int)gridDim.x, ntiles);
+    const int64_t m0 = (int64_t)(wg / tiles_n) * 256, n0 = (int64_t)(wg % tiles_n) * 256;
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const int i = mq * 4 + f;
+      char* crow = (char*)p.c + (m0 + wr * 128 + mq * 64 + f * 16 + frow) * p.ldc * 2;
+      const f32x4 v0 = acc[i][nq * 2], v1 = acc[i][nq * 2 + 1];
+      bf16x8 o = {(__bf16)v0.x, (__bf16)v0.y, (__bf16)v0.z, (__bf16)v0.w,
+                  (__bf16)v1.x, (__bf16)v1.y, (__bf16)v1.z, (__bf16)v1.w};
+      *(uint4*)(crow + (n0 + wc * 64 + nq * 32 + fq * 8) * 2) = __builtin_bit_cast(uint4, o);
+      acc[i][nq * 2] = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc[i][nq * 2 + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+#define T8_BAR()                         \
+  do {                                   \
+    __builtin_amdgcn_sched_barrier(0);   \
+    __builtin_amdgcn_s_barrier();        \
+    __builtin_amdgcn_sched_barrier(0);   \
+  } while (0)
+
+  Cur q0{0, 0}, q1{0, 0};
+  adv(q1);  // q0 = h, q1 = h + 1 (clamped)
+  stage(0, UA0, q0, 0);
+  stage(3, UB1, q0, 0);
+  stage(1, UA1, q0, 0);
+  stage(2, UB0, q0, 0);
+  stage(0, UA0, q1, 1);
+  stage(3, UB1, q1, 1);
+  Cur q2 = q1;
+  adv(q2);  // h + 2
+  int ti = 0;
+  wait_vm<4>();
+  T8_BAR();
+  const bool g1 = wr == 1;
+  if (g1) T8_BAR();
+  // one K-tile of the stream; LAST = the tile's last K-tile (stores its quadrants)
+  auto iter = [&](int h, auto last_tag) {
+    constexpr bool LAST = decltype(last_tag)::value;
+    const int b = h & 1, nb = b ^ 1;
+    const char* cur = smem + b * STAGE;
+    loadA(cur, 0);  // p0
+    loadB(cur, 0);
+    stage(1, UA1, q1, nb);
+    T8_BAR();
+    comp(0, 0);
+    if constexpr (LAST) store_q(ti, 0, 0);
+    T8_BAR();
+    loadB(cur, 1);  // p1
+    stage(2, UB0, q1, nb);
+    T8_BAR();
+    comp(0, 1);
+    if constexpr (LAST) store_q(ti, 0, 1);
+    T8_BAR();
+    loadA(cur, 1);  // p2
+    stage(0, UA0, q2, b);
+    T8_BAR();
+    comp(1, 1);
+    if constexpr (LAST) store_q(ti, 1, 1);
+    T8_BAR();
+    loadB(cur, 0);  // p3
+    stage(3, UB1, q2, b);
+    if (g1) wait_vm<LAST ? 4 + 2 * NS : 4>();  // younger than UB0(h+1): UA0/UB1(h+2), Q01, Q11
+    T8_BAR();
+    comp(1, 0);
+    if constexpr (LAST) store_q(ti, 1, 0);
+    if (!g1) wait_vm<LAST ? 4 + 3 * NS : 4>();  // ... and Q10
+    T8_BAR();
+    q1 = q2;
+    adv(q2);
+  };
+  int h = 0;
+  for (ti = 0; ti < my_tiles; ++ti) {
+    for (int t = 0; t < nk - 1; ++t, ++h) iter(h, std::integral_constant<bool, false>{});
+    iter(h, std::integral_constant<bool, true>{});
+    ++h;
+  }
+  if (!g1) T8_BAR();
+#undef T8_BAR
+  wait_vm<0>();
+}
+
 // fp32 reference: C[m][n] = sum_k A[m][k] * B[n][k]
 __global__ void ref_kernel(const __hip_bfloat16* A, const __hip_bfloat16* B, float* C, int M, int N,
                            int K) {
@@ -923,6 +1111,7 @@ int main(int argc, char** argv) {
   Variant vs[] = {
       {"ring2 dmaAC", ring2_kernel<4, false, 2>, 4, 512, 0},
       {"t8", t8_kernel<false>, 2, 512, 1},
+      {"pt8", pt8_kernel<false>, 2, 512, 0},
   };
   Args a{A, B, C, K, K, N, M, N, K, nullptr};
   const double flop = 2.0 * M * N * K;

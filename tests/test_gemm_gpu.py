@@ -161,7 +161,7 @@ def test_host_checks_reject_bad_shapes(gen):
         gemm(a, _rand((64, 128), torch.bfloat16, gen), M=128)
 
 
-@pytest.mark.parametrize("tile", ["p256", "p128", "pi256", "r256"])
+@pytest.mark.parametrize("tile", ["p256", "p128", "pi256", "r256", "pt8"])
 def test_persistent_many_tiles_grouped(gen, tile):
     """Persistent streaming kernel: more tiles than blocks, grouped C rows, repeat-identical."""
     from ddlb_amd.ops.gemm import gemm
@@ -184,7 +184,7 @@ def test_persistent_many_tiles_grouped(gen, tile):
 
 
 @pytest.mark.parametrize("act", ["gelu", "relu", "silu"])
-@pytest.mark.parametrize("tile", ["auto", "128x128", "pi256", "r256", "t8"])
+@pytest.mark.parametrize("tile", ["auto", "128x128", "pi256", "r256", "t8", "pt8"])
 def test_fused_activation_epilogue(gen, act, tile):
     from ddlb_amd.ops.gemm import gemm
     from ddlb_amd.parallel.sim import apply_act
@@ -286,12 +286,14 @@ def test_blas_mode_falls_back_for_fused(gen):
     torch.testing.assert_close(out8.float(), _ref(a8, w8), rtol=0, atol=_tol(torch.float8_e4m3fn, 256))
 
 
+@pytest.mark.parametrize("tile", ["t8", "pt8"])
 @pytest.mark.parametrize("dt", _RING_DT, ids=lambda d: f"{str(d[0])[6:]}-{str(d[1])[6:]}")
 @pytest.mark.parametrize("shape", [(256, 256, 64), (256, 256, 128), (8192, 1024, 512),
-                                   (4096, 768, 1024), (2048, 2048, 3072)])
-def test_t8_kernel(dt, shape, gen):
-    """8-phase ping-pong kernel: one K-tile (the clamped prefetch path), two, odd K-tile counts,
-    N not a power of two; every input/output dtype; repeat-identical."""
+                                   (4096, 768, 1024), (2048, 2048, 3072), (65536, 1024, 128)])
+def test_t8_kernel(dt, shape, gen, tile):
+    """8-phase ping-pong kernel and its persistent form: one K-tile (the clamped prefetch path),
+    two, odd K-tile counts, N not a power of two, several tiles per persistent block (C quadrant
+    stores in flight across the next tile's staging); every input/output dtype; repeat-identical."""
     from ddlb_amd.ops.gemm import gemm
 
     din, dout = dt
@@ -299,16 +301,17 @@ def test_t8_kernel(dt, shape, gen):
     if K * din.itemsize % 128:
         pytest.skip("K row must be a whole number of 128-byte K-tiles")
     a, w = _rand((M, K), din, gen), _rand((N, K), din, gen)
-    out = gemm(a, w, tile="t8", out_dtype=dout)
+    out = gemm(a, w, tile=tile, out_dtype=dout)
     torch.cuda.synchronize()
     assert out.dtype == dout
     torch.testing.assert_close(out.float(), _ref(a, w), rtol=0, atol=_tol(din, K))
-    again = gemm(a, w, tile="t8", out_dtype=dout)
+    again = gemm(a, w, tile=tile, out_dtype=dout)
     torch.cuda.synchronize()
     assert torch.equal(out, again)
 
 
-def test_t8_grouped_rows_and_race_screen(gen):
+@pytest.mark.parametrize("tile", ["t8", "pt8"])
+def test_t8_grouped_rows_and_race_screen(gen, tile):
     """t8 with the pipelines' strided A and C row blocks, then 50 launches of a large square
     GEMM compared bit for bit (a new sync template: RAW/WAR screen over many runs)."""
     from ddlb_amd.ops.gemm import gemm
@@ -318,17 +321,17 @@ def test_t8_grouped_rows_and_race_screen(gen):
     w = _rand((N, K), torch.bfloat16, gen)
     C = torch.zeros((d * 2048, N), dtype=torch.bfloat16, device=DEV)
     gemm(A[blk:], w, C[blk:], M=d * blk, a_grp=blk, a_gstride=2048, c_grp=blk, c_gstride=2048,
-         tile="t8")
+         tile=tile)
     torch.cuda.synchronize()
     ref = _ref(A, w)
     for r in range(d):
         rows = slice(r * 2048 + blk, r * 2048 + 2 * blk)
         torch.testing.assert_close(C[rows].float(), ref[rows], rtol=0, atol=_tol(torch.bfloat16, K))
     a, w = _rand((4096, 4096), torch.bfloat16, gen), _rand((4096, 4096), torch.bfloat16, gen)
-    first = gemm(a, w, tile="t8").clone()
+    first = gemm(a, w, tile=tile).clone()
     out = torch.empty_like(first)
     for _ in range(50):
-        gemm(a, w, out, tile="t8")
+        gemm(a, w, out, tile=tile)
     torch.cuda.synchronize()
     assert torch.equal(out, first)
     torch.testing.assert_close(first.float(), _ref(a, w), rtol=0, atol=_tol(torch.bfloat16, 4096))
