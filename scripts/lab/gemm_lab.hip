@@ -1114,12 +1114,14 @@ int main(int argc, char** argv) {
       {"pt8", pt8_kernel<false>, 2, 512, 0},
   };
   Args a{A, B, C, K, K, N, M, N, K, nullptr};
+  const char* only = getenv("LAB_ONLY");  // profile one variant: skip the others
   const double flop = 2.0 * M * N * K;
   std::vector<std::vector<float>> times(sizeof(vs) / sizeof(vs[0]));
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
   for (size_t v = 0; v < sizeof(vs) / sizeof(vs[0]); ++v) {
+    if (only && strcmp(only, vs[v].name) != 0) continue;
     CHECK(hipMemset(C, 0, (size_t)M * N * 2));
     CHECK(hipMemset(err, 0, 4));
     const int gv = vs[v].all_tiles ? (M / 256) * (N / 256) : grid;
@@ -1132,6 +1134,7 @@ int main(int argc, char** argv) {
   }
   for (int r = 0; r < rounds; ++r)
     for (size_t v = 0; v < sizeof(vs) / sizeof(vs[0]); ++v) {
+      if (only && strcmp(only, vs[v].name) != 0) continue;
       const int gv = vs[v].all_tiles ? (M / 256) * (N / 256) : grid;
       for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(vs[v].fn, dim3(gv), dim3(vs[v].threads), 0, 0, a);
       CHECK(hipEventRecord(e0));
@@ -1145,10 +1148,12 @@ int main(int argc, char** argv) {
   printf("\n%dx%dx%d bf16, grid %d\n", M, N, K, grid);
   for (size_t v = 0; v < sizeof(vs) / sizeof(vs[0]); ++v) {
     auto t = times[v];
+    if (t.empty()) continue;
     std::sort(t.begin(), t.end());
     const float med = t[t.size() / 2];
     printf("  %-20s %8.4f ms  %7.1f TFLOP/s\n", vs[v].name, med, flop / (med * 1e-3) / 1e12);
   }
+  if (only) return 0;
   // stamps for NS=4
   Args s = a;
   s.stamps = stamps;
