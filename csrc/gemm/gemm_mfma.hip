@@ -65,9 +65,10 @@ int choose_tile(int64_t M, int64_t N, int64_t K, int din) {
   // (profiles/r01/s2/lab/t8_vs_ring2.txt) once the grid covers most of the CUs.
   auto tiles = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
   const int64_t kbytes = K * dtype_size(din);
-  // Its persistent form (pt8) wins on short K with a narrow N (the flagship 65536x1024x1024:
-  // 0.1116 vs 0.1163 ms) and loses ~5 % on a wide N (16384x8192x1024).
-  if (M % 256 == 0 && N % 256 == 0 && tiles(256, 256) >= 256 && kbytes <= 2048 && N <= 2048)
+  // Its persistent form (pt8) wins on short K with a narrow N once every block streams several
+  // tiles (the flagship 65536x1024x1024, 4 tiles per CU: 0.1116-0.1188 vs 0.1163-0.1229 ms); with
+  // one tile per CU (16384x1024x1024) or a wide N (16384x8192x1024) t8 is 4-9 % faster.
+  if (M % 256 == 0 && N % 256 == 0 && tiles(256, 256) >= 512 && kbytes <= 2048 && N <= 2048)
     return TILE_PT8;
   if (M % 256 == 0 && N % 256 == 0 && tiles(256, 256) >= 192) return TILE_T8;
   if (M % 256 == 0 && N % 256 == 0 && tiles(256, 256) >= 256 && kbytes <= 2048) return TILE_R256;
