@@ -106,6 +106,19 @@ struct MmaF32 {  // exact f32 MFMA; 4 instructions per 16 B
   }
 };
 
+// Block-scaled MX-fp8 (e4m3 x e4m3, unit E8M0 scales = 127): ONE v_mfma_scale_f32_16x16x128_f8f6f4
+// consumes both 16-byte chunks of a 128-byte K-row (kPair), at 2x the bf16 MFMA rate.
+struct MmaMX {
+  static constexpr int kElem = 1, kMfma = 1;
+  static constexpr bool kPair = true;
+  static __device__ __forceinline__ void step8(f32x4& acc, const i32x8& b, const i32x8& a) {
+    acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(b, a, acc, 0, 0, 0, 127, 0, 127);
+  }
+};
+template <class Mma, class = void> struct is_pair : std::false_type {};
+template <class Mma> struct is_pair<Mma, std::void_t<decltype(Mma::kPair)>>
+    : std::integral_constant<bool, Mma::kPair> {};
+
 // Compile-time emission of the {PER x MFMA, 1 x VMEM, n_g x DS_READ} interleave pattern
 // (sched_group_barrier arguments must be literal constants).
 template <int G, int NG, int PER, int NRD, int NDMA>
@@ -1006,33 +1019,60 @@ __global__ __launch_bounds__(512) void gemm_tn_t8_kernel(const GemmArgs p) {
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  i32x4 aR[4][2], bR[2][2];
+  i32x4 aR[4][2], bR[2][2];  // fragments: [f or g][K-half]
+  i32x8 aP[4], bP[2];        // MX (kPair): both K-halves in one register tuple, loaded in place
+  constexpr bool PAIR = is_pair<Mma>::value;
   auto loadA = [&](const char* base, int mq) __attribute__((always_inline)) {
     const char* r = base + (mq ? UA1 : UA0) + aoff;
 #pragma unroll
     for (int f = 0; f < 4; ++f) {
-      aR[f][0] = *(const i32x4*)(r + f * 16 * ROWB + c0);
-      aR[f][1] = *(const i32x4*)(r + f * 16 * ROWB + c1);
+      if constexpr (PAIR) {
+        aP[f].lo = *(const i32x4*)(r + f * 16 * ROWB + c0);
+        aP[f].hi = *(const i32x4*)(r + f * 16 * ROWB + c1);
+      } else {
+        aR[f][0] = *(const i32x4*)(r + f * 16 * ROWB + c0);
+        aR[f][1] = *(const i32x4*)(r + f * 16 * ROWB + c1);
+      }
     }
   };
   auto loadB = [&](const char* base, int nq) __attribute__((always_inline)) {
     const char* r = base + (nq ? UB1 : UB0) + boff;
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
-      bR[g][0] = *(const i32x4*)(r + g * 16 * ROWB + c0);
-      bR[g][1] = *(const i32x4*)(r + g * 16 * ROWB + c1);
+      if constexpr (PAIR) {
+        bP[g].lo = *(const i32x4*)(r + g * 16 * ROWB + c0);
+        bP[g].hi = *(const i32x4*)(r + g * 16 * ROWB + c1);
+      } else {
+        bR[g][0] = *(const i32x4*)(r + g * 16 * ROWB + c0);
+        bR[g][1] = *(const i32x4*)(r + g * 16 * ROWB + c1);
+      }
     }
   };
   auto comp = [&](int mq, int nq) __attribute__((always_inline)) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+    if constexpr (PAIR) {  // one MFMA per 128-byte K-row
 #pragma unroll
       for (int f = 0; f < 4; ++f)
 #pragma unroll
-        for (int g = 0; g < 2; ++g) Mma::step(acc[mq * 4 + f][nq * 2 + g], bR[g][kk], aR[f][kk]);
+        for (int g = 0; g < 2; ++g) Mma::step8(acc[mq * 4 + f][nq * 2 + g], bP[g], aP[f]);
+      // The scaled MFMA is a pure intrinsic: without a use here LLVM sinks all four phases' MFMAs
+      // past the barriers to the end of the K-tile (observed: 32 back-to-back MFMAs, spills and
+      // vmcnt(0) drains in the loop). An empty asm that "modifies" the quadrant's accumulators
+      // pins them inside this phase's compute section.
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) asm volatile("" : "+v"(acc[mq * 4 + f][nq * 2 + g]));
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int f = 0; f < 4; ++f)
+#pragma unroll
+          for (int g = 0; g < 2; ++g) Mma::step(acc[mq * 4 + f][nq * 2 + g], bR[g][kk], aR[f][kk]);
+    }
     __builtin_amdgcn_s_setprio(0);
   };
 #define T8_BAR()                         \
@@ -1178,33 +1218,60 @@ __global__ __launch_bounds__(512) void gemm_tn_pt8_kernel(const GemmArgs p) {
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  i32x4 aR[4][2], bR[2][2];
+  i32x4 aR[4][2], bR[2][2];  // fragments: [f or g][K-half]
+  i32x8 aP[4], bP[2];        // MX (kPair): both K-halves in one register tuple, loaded in place
+  constexpr bool PAIR = is_pair<Mma>::value;
   auto loadA = [&](const char* base, int mq) __attribute__((always_inline)) {
     const char* r = base + (mq ? UA1 : UA0) + aoff;
 #pragma unroll
     for (int f = 0; f < 4; ++f) {
-      aR[f][0] = *(const i32x4*)(r + f * 16 * ROWB + c0);
-      aR[f][1] = *(const i32x4*)(r + f * 16 * ROWB + c1);
+      if constexpr (PAIR) {
+        aP[f].lo = *(const i32x4*)(r + f * 16 * ROWB + c0);
+        aP[f].hi = *(const i32x4*)(r + f * 16 * ROWB + c1);
+      } else {
+        aR[f][0] = *(const i32x4*)(r + f * 16 * ROWB + c0);
+        aR[f][1] = *(const i32x4*)(r + f * 16 * ROWB + c1);
+      }
     }
   };
   auto loadB = [&](const char* base, int nq) __attribute__((always_inline)) {
     const char* r = base + (nq ? UB1 : UB0) + boff;
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
-      bR[g][0] = *(const i32x4*)(r + g * 16 * ROWB + c0);
-      bR[g][1] = *(const i32x4*)(r + g * 16 * ROWB + c1);
+      if constexpr (PAIR) {
+        bP[g].lo = *(const i32x4*)(r + g * 16 * ROWB + c0);
+        bP[g].hi = *(const i32x4*)(r + g * 16 * ROWB + c1);
+      } else {
+        bR[g][0] = *(const i32x4*)(r + g * 16 * ROWB + c0);
+        bR[g][1] = *(const i32x4*)(r + g * 16 * ROWB + c1);
+      }
     }
   };
   auto comp = [&](int mq, int nq) __attribute__((always_inline)) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+    if constexpr (PAIR) {  // one MFMA per 128-byte K-row
 #pragma unroll
       for (int f = 0; f < 4; ++f)
 #pragma unroll
-        for (int g = 0; g < 2; ++g) Mma::step(acc[mq * 4 + f][nq * 2 + g], bR[g][kk], aR[f][kk]);
+        for (int g = 0; g < 2; ++g) Mma::step8(acc[mq * 4 + f][nq * 2 + g], bP[g], aP[f]);
+      // The scaled MFMA is a pure intrinsic: without a use here LLVM sinks all four phases' MFMAs
+      // past the barriers to the end of the K-tile (observed: 32 back-to-back MFMAs, spills and
+      // vmcnt(0) drains in the loop). An empty asm that "modifies" the quadrant's accumulators
+      // pins them inside this phase's compute section.
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) asm volatile("" : "+v"(acc[mq * 4 + f][nq * 2 + g]));
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int f = 0; f < 4; ++f)
+#pragma unroll
+          for (int g = 0; g < 2; ++g) Mma::step(acc[mq * 4 + f][nq * 2 + g], bR[g][kk], aR[f][kk]);
+    }
     __builtin_amdgcn_s_setprio(0);
   };
   int ti = 0;
@@ -1591,6 +1658,13 @@ hipError_t launch_cfg(const GemmArgs& p, int tile, hipStream_t s) {
 }
 template <int OUT>
 hipError_t launch_mx_cfg(const GemmArgs& p, int tile, hipStream_t s) {
+  // whole 256x256 tiles: the 8-phase ping-pong schedule (persistent with >= 2 tiles per CU)
+  if ((tile == TILE_T8 || tile == TILE_PT8 || tile == TILE_R256 || tile == TILE_AUTO) && t8_ok(p)) {
+    const int tiles = (p.M / 256) * (p.N / 256);
+    if (tile != TILE_T8 && p.flags == nullptr && tiles >= 2 * num_cus())
+      return launch_pt8<MmaMX, OUT>(p, s);
+    return launch_t8<MmaMX, OUT>(p, s);
+  }
   switch (tile) {
     case TILE_PP256:
     case TILE_256x256: return launch_mx<OUT, 256, 256, 2, 4>(p, s);

@@ -96,7 +96,7 @@ def test_gemm_fp8(mode, odt, gen):
     torch.testing.assert_close(out.float(), _ref(a, w), rtol=0, atol=_tol(torch.float8_e4m3fn, K))
 
 
-@pytest.mark.parametrize("tile", ["auto", "pp256", "128x128", "256x256w4", "256x128w4", "p256", "p128", "i256", "i128", "i256w4", "pi256", "r256", "t8"])
+@pytest.mark.parametrize("tile", ["auto", "pp256", "128x128", "256x256w4", "256x128w4", "p256", "p128", "i256", "i128", "i256w4", "pi256", "r256", "t8", "pt8"])
 def test_fp8_integer_exact(gen, tile):
     """Small integers are exact in e4m3: both fp8 paths must match bit for bit."""
     from ddlb_amd.ops.gemm import gemm
@@ -335,3 +335,25 @@ def test_t8_grouped_rows_and_race_screen(gen, tile):
     torch.cuda.synchronize()
     assert torch.equal(out, first)
     torch.testing.assert_close(first.float(), _ref(a, w), rtol=0, atol=_tol(torch.bfloat16, 4096))
+
+
+@pytest.mark.parametrize("tile", ["t8", "pt8"])
+@pytest.mark.parametrize("shape", [(256, 256, 128), (2048, 768, 1024), (65536, 1024, 256)])
+def test_t8_mx_fp8(tile, shape, gen):
+    """Block-scaled MX-fp8 on the 8-phase schedule (one 16x16x128 scaled MFMA per 128-byte
+    K-row): integer data is exact, random data within the fp8 tolerance; repeat-identical."""
+    from ddlb_amd.ops.gemm import gemm
+
+    M, N, K = shape
+    a = torch.randint(-3, 4, (M, K), device=DEV, generator=gen).float().to(torch.float8_e4m3fn)
+    w = torch.randint(-3, 4, (N, K), device=DEV, generator=gen).float().to(torch.float8_e4m3fn)
+    out = gemm(a, w, out_dtype=torch.float32, mode="mx", tile=tile)
+    torch.cuda.synchronize()
+    assert torch.equal(out, _ref(a, w))
+    a, w = _rand((M, K), torch.float8_e4m3fn, gen), _rand((N, K), torch.float8_e4m3fn, gen)
+    out = gemm(a, w, mode="mx", tile=tile)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out.float(), _ref(a, w), rtol=0, atol=_tol(torch.float8_e4m3fn, K))
+    again = gemm(a, w, mode="mx", tile=tile)
+    torch.cuda.synchronize()
+    assert torch.equal(out, again)
