@@ -1196,6 +1196,151 @@ __global__ __launch_bounds__(512) void t8b_kernel(const Args p) {
   }
 }
 
+
+// t4: the ping-pong with 2 phases per K-tile and 32 MFMAs per compute section (half the barriers
+// of t8). Phase A: read A0 + B0 + B1 (16), compute (0,0)+(0,1); phase B: read A1 (8), compute
+// (1,1)+(1,0). Intervals per K-tile t: g0 reads I_{4t}, I_{4t+2}; g1 one later. Every read
+// section ends with lgkmcnt(0) before its barrier, so a unit is restaged from the interval after
+// its last read: phase B of t stages UB0/UB1(t+2), phase A of t+1 stages UA0/UA1(t+2) (buffer t&1).
+// RAW: vmcnt(6) after phase B (retires A0 of K-tile t+1, the youngest unit phase A of t+1 reads),
+// vmcnt(8) after phase A (retires A1 of the current K-tile).
+template <bool STAMP>
+__global__ __launch_bounds__(512) void t4_kernel(const Args p) {
+  constexpr int ROWB = 128, UNIT = 128 * ROWB, STAGE = 4 * UNIT;
+  constexpr int UA0 = 0, UA1 = UNIT, UB0 = 2 * UNIT, UB1 = 3 * UNIT;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int tiles_n = p.N / 256, ntiles = (p.M / 256) * tiles_n;
+  const int wg = xcd_remap((int)blockIdx.x, ntiles);
+  const int64_t m0 = (int64_t)(wg / tiles_n) * 256, n0 = (int64_t)(wg % tiles_n) * 256;
+  const int nk = p.K / 64;
+  const int drow = lane >> 3, dpc = lane & 7;
+  const char* sA[2][2];
+  const char* sB[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int ur = wave * 16 + i * 8 + drow;
+    const int ch = (dpc ^ ((ur >> 1) & 7)) * 16;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int lr = (ur >> 6) * 128 + q * 64 + (ur & 63);
+      sA[q][i] = (const char*)p.a + (m0 + lr) * p.lda * 2 + ch;
+      const int lc = (ur >> 5) * 64 + q * 32 + t8_perm(ur & 31);
+      sB[q][i] = (const char*)p.b + (n0 + lc) * p.ldb * 2 + ch;
+    }
+  }
+  auto stage = [&](const char* const* src, int unit_off, int kt, int buf) __attribute__((always_inline)) {
+    kt = kt < nk ? kt : nk - 1;
+    char* dst = smem + buf * STAGE + unit_off + wave * 16 * ROWB;
+    glds16(src[0] + (int64_t)kt * ROWB, dst);
+    glds16(src[1] + (int64_t)kt * ROWB, dst + 8 * ROWB);
+  };
+  const int frow = lane & 15, fq = lane >> 4, sw = (frow >> 1) & 7;
+  const int c0 = ((0 + fq) ^ sw) * 16, c1 = ((4 + fq) ^ sw) * 16;
+  const int aoff = (wr * 64 + frow) * ROWB, boff = (wc * 32 + frow) * ROWB;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  i32x4 aR[4][2], b0R[2][2], b1R[2][2];
+  auto loadA = [&](const char* base, int mq) __attribute__((always_inline)) {
+    const char* r = base + (mq ? UA1 : UA0) + aoff;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      aR[f][0] = *(const i32x4*)(r + f * 16 * ROWB + c0);
+      aR[f][1] = *(const i32x4*)(r + f * 16 * ROWB + c1);
+    }
+  };
+  auto loadB = [&](const char* base, int nq, i32x4 (&dst)[2][2]) __attribute__((always_inline)) {
+    const char* r = base + (nq ? UB1 : UB0) + boff;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      dst[g][0] = *(const i32x4*)(r + g * 16 * ROWB + c0);
+      dst[g][1] = *(const i32x4*)(r + g * 16 * ROWB + c1);
+    }
+  };
+  auto mm = [&](int mq, int nq, const i32x4 (&bR)[2][2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+          acc[mq * 4 + f][nq * 2 + g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8, bR[g][kk]), __builtin_bit_cast(bf16x8, aR[f][kk]),
+              acc[mq * 4 + f][nq * 2 + g], 0, 0, 0);
+  };
+#define T4_BAR()                         \
+  do {                                   \
+    __builtin_amdgcn_sched_barrier(0);   \
+    __builtin_amdgcn_s_barrier();        \
+    __builtin_amdgcn_sched_barrier(0);   \
+  } while (0)
+#define T4_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+  const bool g1 = wr == 1;
+  // prologue = the steady-state issue order up to "end of phase B of K-tile -1":
+  // B0 B1 A0 A1 of K-tile 0, B0 B1 of K-tile 1; vmcnt(6) retires B0, B1, A0 of K-tile 0
+  stage(sB[0], UB0, 0, 0);
+  stage(sB[1], UB1, 0, 0);
+  stage(sA[0], UA0, 0, 0);
+  stage(sA[1], UA1, 0, 0);
+  stage(sB[0], UB0, 1, 1);
+  stage(sB[1], UB1, 1, 1);
+  wait_vm<6>();
+  T4_BAR();
+  if (g1) T4_BAR();
+  for (int t = 0; t < nk; ++t) {
+    const int b = t & 1;
+    const char* cur = smem + b * STAGE;
+    // phase A: read A0 + B0 + B1 of t; stage UA0/UA1(t+1) into the other buffer
+    loadB(cur, 0, b0R);
+    loadB(cur, 1, b1R);
+    loadA(cur, 0);
+    stage(sA[0], UA0, t + 1, b ^ 1);
+    stage(sA[1], UA1, t + 1, b ^ 1);
+    T4_LGKM0();
+    if (g1) wait_vm<8>();  // retires A1 of K-tile t (younger: B0/B1(t+1), A0/A1(t+1))
+    T4_BAR();
+    __builtin_amdgcn_s_setprio(1);
+    mm(0, 0, b0R);
+    mm(0, 1, b1R);
+    __builtin_amdgcn_s_setprio(0);
+    if (!g1) wait_vm<8>();
+    T4_BAR();
+    // phase B: A1; stage B0/B1 of K-tile t+2 into this buffer (its B units were read in phase A)
+    loadA(cur, 1);
+    stage(sB[0], UB0, t + 2, b);
+    stage(sB[1], UB1, t + 2, b);
+    T4_LGKM0();
+    if (g1) wait_vm<6>();  // retires A0 of K-tile t+1 (younger: A1(t+1), B0/B1(t+2))
+    T4_BAR();
+    __builtin_amdgcn_s_setprio(1);
+    mm(1, 1, b1R);
+    mm(1, 0, b0R);
+    __builtin_amdgcn_s_setprio(0);
+    if (!g1) wait_vm<6>();
+    T4_BAR();
+  }
+  if (!g1) T4_BAR();
+#undef T4_BAR
+#undef T4_LGKM0
+  wait_vm<0>();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    char* crow = (char*)p.c + (m0 + wr * 128 + (i >> 2) * 64 + (i & 3) * 16 + frow) * p.ldc * 2;
+#pragma unroll
+    for (int nq = 0; nq < 2; ++nq) {
+      const f32x4 v0 = acc[i][nq * 2], v1 = acc[i][nq * 2 + 1];
+      bf16x8 o = {(__bf16)v0.x, (__bf16)v0.y, (__bf16)v0.z, (__bf16)v0.w,
+                  (__bf16)v1.x, (__bf16)v1.y, (__bf16)v1.z, (__bf16)v1.w};
+      *(uint4*)(crow + (n0 + wc * 64 + nq * 32 + fq * 8) * 2) = __builtin_bit_cast(uint4, o);
+    }
+  }
+}
+
 // fp32 reference: C[m][n] = sum_k A[m][k] * B[n][k]
 __global__ void ref_kernel(const __hip_bfloat16* A, const __hip_bfloat16* B, float* C, int M, int N,
                            int K) {
@@ -1270,6 +1415,7 @@ int main(int argc, char** argv) {
       {"t8", t8_kernel<false>, 2, 512, 1},
       {"pt8", pt8_kernel<false>, 2, 512, 0},
       {"t8b", t8b_kernel<false>, 2, 512, 1},
+      {"t4", t4_kernel<false>, 2, 512, 1},
   };
   Args a{A, B, C, K, K, N, M, N, K, nullptr};
   const char* only = getenv("LAB_ONLY");  // profile one variant: skip the others
