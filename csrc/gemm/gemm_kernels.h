@@ -1140,6 +1140,180 @@ __global__ __launch_bounds__(512) void gemm_tn_t8_kernel(const GemmArgs p) {
 }
 
 
+
+// ---------------------------------------------------------------- t4: 2-phase ping-pong kernel
+// The t8 geometry (256x256 tile, 8 waves in two groups one barrier apart, 16 KB units, 128-byte
+// K rows) with 2 phases per K-tile and 32 MFMAs per compute section, i.e. half the barriers:
+//   phase A: read A0 + B0 + B1 of K-tile t (16 fragments), stage UA0/UA1(t+1) into the other
+//            buffer, compute quadrants (0,0) + (0,1)
+//   phase B: read A1 of t (8), stage UB0/UB1(t+2) into this buffer, compute (1,1) + (1,0)
+// Every read section ends with lgkmcnt(0) before its barrier, so a unit may be restaged from the
+// interval after its last read (UB0/UB1 of t are read only in phase A and held in registers).
+// RAW: vmcnt(8) after phase A retires A1 of t (younger: B0/B1(t+1), A0/A1(t+1)); vmcnt(6) after
+// phase B retires A0 of t+1, the youngest unit phase A of t+1 reads. Clamped restaging past the
+// last K-tile as in t8. Measured (scripts/lab, profiles/r01/s2/lab/t8_vs_ring2.txt): 9 % faster
+// than t8 with one short-K tile per CU (16384x1024x1024), 3 % at 65536x1024x8192, 3 % slower at
+// 8192^3.
+template <class Mma, int OUT>
+__global__ __launch_bounds__(512) void gemm_tn_t4_kernel(const GemmArgs p) {
+  constexpr int ROWB = 128, UNIT = 128 * ROWB, STAGE = 4 * UNIT;
+  constexpr int UA0 = 0, UA1 = UNIT, UB0 = 2 * UNIT, UB1 = 3 * UNIT;
+  constexpr bool PAIR = is_pair<Mma>::value;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int tiles_n = p.N / 256, ntiles = (p.M / 256) * tiles_n;
+  const int wg = tile_index(p, ntiles);
+  const int64_t m0 = (int64_t)(wg / tiles_n) * 256, n0 = (int64_t)(wg % tiles_n) * 256;
+  const int esz = Mma::kElem;
+  const int nk = p.K * esz / ROWB;
+
+  const int drow = lane >> 3, dpc = lane & 7;
+  const char* sA[2][2];
+  const char* sB[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int ur = wave * 16 + i * 8 + drow;
+    const int ch = (dpc ^ ((ur >> 1) & 7)) * 16;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int lr = (ur >> 6) * 128 + q * 64 + (ur & 63);
+      sA[q][i] = a_row(p, m0 + lr, esz) + ch;
+      const int lc = (ur >> 5) * 64 + q * 32 + t8_perm(ur & 31);
+      sB[q][i] = (const char*)p.b + (n0 + lc) * p.ldb * esz + ch;
+    }
+  }
+  wait_flag(p, m0);
+  auto stage = [&](const char* const* src, int unit_off, int kt, int buf)
+                   __attribute__((always_inline)) {
+    kt = kt < nk ? kt : nk - 1;
+    char* dst = smem + buf * STAGE + unit_off + wave * 16 * ROWB;
+    glds16(src[0] + (int64_t)kt * ROWB, dst);
+    glds16(src[1] + (int64_t)kt * ROWB, dst + 8 * ROWB);
+  };
+  const int frow = lane & 15, fq = lane >> 4, sw = (frow >> 1) & 7;
+  const int c0 = ((0 + fq) ^ sw) * 16, c1 = ((4 + fq) ^ sw) * 16;
+  const int aoff = (wr * 64 + frow) * ROWB, boff = (wc * 32 + frow) * ROWB;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  i32x4 aR[4][2], bR[2][2][2];  // bR[nq][g][K-half]
+  i32x8 aP[4], bP[2][2];        // MX (kPair): both K-halves in one register tuple
+  auto loadA = [&](const char* base, int mq) __attribute__((always_inline)) {
+    const char* r = base + (mq ? UA1 : UA0) + aoff;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      if constexpr (PAIR) {
+        aP[f].lo = *(const i32x4*)(r + f * 16 * ROWB + c0);
+        aP[f].hi = *(const i32x4*)(r + f * 16 * ROWB + c1);
+      } else {
+        aR[f][0] = *(const i32x4*)(r + f * 16 * ROWB + c0);
+        aR[f][1] = *(const i32x4*)(r + f * 16 * ROWB + c1);
+      }
+    }
+  };
+  auto loadB = [&](const char* base, int nq) __attribute__((always_inline)) {
+    const char* r = base + (nq ? UB1 : UB0) + boff;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      if constexpr (PAIR) {
+        bP[nq][g].lo = *(const i32x4*)(r + g * 16 * ROWB + c0);
+        bP[nq][g].hi = *(const i32x4*)(r + g * 16 * ROWB + c1);
+      } else {
+        bR[nq][g][0] = *(const i32x4*)(r + g * 16 * ROWB + c0);
+        bR[nq][g][1] = *(const i32x4*)(r + g * 16 * ROWB + c1);
+      }
+    }
+  };
+  auto mm = [&](int mq, int nq) __attribute__((always_inline)) {
+    if constexpr (PAIR) {
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) Mma::step8(acc[mq * 4 + f][nq * 2 + g], bP[nq][g], aP[f]);
+#pragma unroll
+      for (int f = 0; f < 4; ++f)  // pin the pure scaled MFMAs in this section (see t8)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) asm volatile("" : "+v"(acc[mq * 4 + f][nq * 2 + g]));
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int f = 0; f < 4; ++f)
+#pragma unroll
+          for (int g = 0; g < 2; ++g)
+            Mma::step(acc[mq * 4 + f][nq * 2 + g], bR[nq][g][kk], aR[f][kk]);
+    }
+  };
+#define T4_BAR()                         \
+  do {                                   \
+    __builtin_amdgcn_sched_barrier(0);   \
+    __builtin_amdgcn_s_barrier();        \
+    __builtin_amdgcn_sched_barrier(0);   \
+  } while (0)
+#define T4_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+  const bool g1 = wr == 1;  // wave-uniform (wave came through readfirstlane)
+  // prologue = the steady-state issue order up to "end of phase B of K-tile -1"
+  stage(sB[0], UB0, 0, 0);
+  stage(sB[1], UB1, 0, 0);
+  stage(sA[0], UA0, 0, 0);
+  stage(sA[1], UA1, 0, 0);
+  stage(sB[0], UB0, 1, 1);
+  stage(sB[1], UB1, 1, 1);
+  wait_vm<6>();
+  T4_BAR();
+  if (g1) T4_BAR();
+  for (int t = 0; t < nk; ++t) {
+    const int b = t & 1;
+    const char* cur = smem + b * STAGE;
+    loadB(cur, 0);  // phase A
+    loadB(cur, 1);
+    loadA(cur, 0);
+    stage(sA[0], UA0, t + 1, b ^ 1);
+    stage(sA[1], UA1, t + 1, b ^ 1);
+    T4_LGKM0();
+    if (g1) wait_vm<8>();
+    T4_BAR();
+    __builtin_amdgcn_s_setprio(1);
+    mm(0, 0);
+    mm(0, 1);
+    __builtin_amdgcn_s_setprio(0);
+    if (!g1) wait_vm<8>();
+    T4_BAR();
+    loadA(cur, 1);  // phase B
+    stage(sB[0], UB0, t + 2, b);
+    stage(sB[1], UB1, t + 2, b);
+    T4_LGKM0();
+    if (g1) wait_vm<6>();
+    T4_BAR();
+    __builtin_amdgcn_s_setprio(1);
+    mm(1, 1);
+    mm(1, 0);
+    __builtin_amdgcn_s_setprio(0);
+    if (!g1) wait_vm<6>();
+    T4_BAR();
+  }
+  if (!g1) T4_BAR();
+#undef T4_BAR
+#undef T4_LGKM0
+  wait_vm<0>();  // never leave an LDS-DMA in flight past the end of the workgroup
+  constexpr int OSZ = out_size<OUT>();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int64_t row = m0 + wr * 128 + (i >> 2) * 64 + (i & 3) * 16 + frow;
+    char* crow = (char*)p.c + map_row(row, p.c_grp, p.c_gstride) * p.ldc * OSZ;
+#pragma unroll
+    for (int nq = 0; nq < 2; ++nq) {
+      char* dst = crow + (n0 + wc * 64 + nq * 32 + fq * 8) * OSZ;
+      if (p.act == ACT_NONE) Store8<OUT>::st(dst, acc[i][nq * 2], acc[i][nq * 2 + 1]);
+      else Store8<OUT>::st(dst, act4(acc[i][nq * 2], p.act), act4(acc[i][nq * 2 + 1], p.act));
+    }
+  }
+}
+
 // ---------------------------------------------------------------- pt8: persistent t8
 // One workgroup per CU streams its tiles' K-tiles back to back (stream index h = tile * nk + kt;
 // the t8 unit schedule above runs unchanged across tile boundaries, so only the first tile pays
@@ -1597,6 +1771,13 @@ hipError_t launch_t8(const GemmArgs& p, hipStream_t s) {
 }
 
 template <class Mma, int OUT>
+hipError_t launch_t4(const GemmArgs& p, hipStream_t s) {
+  const int tiles = (p.M / 256) * (p.N / 256);
+  hipLaunchKernelGGL((gemm_tn_t4_kernel<Mma, OUT>), dim3(tiles), dim3(512), 0, s, p);
+  return hipGetLastError();
+}
+
+template <class Mma, int OUT>
 hipError_t launch_pt8(const GemmArgs& p, hipStream_t s) {
   const int tiles = (p.M / 256) * (p.N / 256);
   int grid = num_cus();
@@ -1620,6 +1801,9 @@ hipError_t launch_cfg(const GemmArgs& p, int tile, hipStream_t s) {
     case TILE_PT8:  // persistent: no arrival flags (a block's tiles are fixed up front)
       if (t8_ok(p) && p.flags == nullptr) return launch_pt8<Mma, OUT>(p, s);
       if (t8_ok(p)) return launch_t8<Mma, OUT>(p, s);
+      return launch_tiled<Mma, OUT, 256, 256, 2, 4, true>(p, s);
+    case TILE_T4:
+      if (t8_ok(p)) return launch_t4<Mma, OUT>(p, s);
       return launch_tiled<Mma, OUT, 256, 256, 2, 4, true>(p, s);
     case TILE_T8:
       if (t8_ok(p)) return launch_t8<Mma, OUT>(p, s);
@@ -1659,6 +1843,7 @@ hipError_t launch_cfg(const GemmArgs& p, int tile, hipStream_t s) {
 template <int OUT>
 hipError_t launch_mx_cfg(const GemmArgs& p, int tile, hipStream_t s) {
   // whole 256x256 tiles: the 8-phase ping-pong schedule (persistent with >= 2 tiles per CU)
+  if (tile == TILE_T4 && t8_ok(p)) return launch_t4<MmaMX, OUT>(p, s);
   if ((tile == TILE_T8 || tile == TILE_PT8 || tile == TILE_R256 || tile == TILE_AUTO) && t8_ok(p)) {
     const int tiles = (p.M / 256) * (p.N / 256);
     if (tile != TILE_T8 && p.flags == nullptr && tiles >= 2 * num_cus())
@@ -1677,7 +1862,8 @@ hipError_t launch_mx_cfg(const GemmArgs& p, int tile, hipStream_t s) {
     case TILE_I256W4: return launch_mx<OUT, 256, 256, 2, 2>(p, s);
     case TILE_PI256: return launch_mx<OUT, 256, 256, 2, 4>(p, s);
     case TILE_PI256W4: return launch_mx<OUT, 256, 256, 2, 2>(p, s);
-    case TILE_R256: case TILE_T8: case TILE_PT8: return launch_mx<OUT, 256, 256, 2, 4>(p, s);
+    case TILE_R256: case TILE_T8: case TILE_PT8: case TILE_T4:
+      return launch_mx<OUT, 256, 256, 2, 4>(p, s);
     case TILE_P128: return launch_mx<OUT, 128, 128, 2, 2>(p, s);
     case TILE_256x128_W4: return launch_mx<OUT, 256, 128, 2, 2>(p, s);
     default: return hipErrorInvalidValue;
