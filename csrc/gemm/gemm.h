@@ -26,7 +26,8 @@ enum Tile : int { TILE_AUTO = 0, TILE_256x256 = 1, TILE_256x128 = 2, TILE_128x25
                   TILE_R256 = 15,     // R: persistent LDS-ring (3 K-steps in flight)
                   TILE_T8 = 16,       // T8: 8-phase ping-pong, counted vmcnt (gemm_kernels.h)
                   TILE_PT8 = 17,      // PT8: persistent T8 (tiles streamed, C stores spread)
-                  TILE_T4 = 18 };     // T4: 2-phase ping-pong (32 MFMAs per section)
+                  TILE_T4 = 18,       // T4: 2-phase ping-pong (32 MFMAs per section)
+                  TILE_PT4 = 19 };    // PT4: persistent T4
 enum GemmMode : int { GEMM_MODE_AUTO = 0, GEMM_MODE_GENERIC = 1, GEMM_MODE_MX = 2,
                       GEMM_MODE_BLAS = 3 };  // BLAS: hipBLASLt for plain GEMMs (blaslt.cpp)
 

@@ -1314,6 +1314,233 @@ __global__ __launch_bounds__(512) void gemm_tn_t4_kernel(const GemmArgs p) {
   }
 }
 
+
+// ---------------------------------------------------------------- pt4: persistent t4
+// t4 streamed across a block's tiles (as pt8 does for t8). A tile's quadrants are stored right
+// after their last MFMAs: Q00 + Q01 after phase A of its last K-tile, Q11 + Q10 after phase B.
+// vmcnt counts (NS = C store instructions per quadrant per wave), per K-tile kind:
+//   normal:             A end 8,        B end 6
+//   LAST of a tile:     A end g0 8+2NS / g1 8,   B end g0 6+4NS / g1 6+2NS
+//   FIRST after a LAST: A end 8+4NS (both),      B end 6
+// (stores count in issue order with the LDS-DMA; the counts keep exactly the ops issued after
+// the unit the next phase reads in flight). The A / B sources are per-lane 32-bit offsets inside
+// a tile's panels plus wave-uniform panel bases, so switching tiles costs two scalar pointers and
+// the kernel stays within 256 VGPRs. Plain A rows only (no shard table / grouped A / flags: t4).
+// Measured (scripts/lab, profiles/r01/s2/lab/t8_vs_ring2.txt): flagship 0.1127 vs t4 0.1160 ms.
+template <class Mma, int OUT>
+__global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
+  constexpr int ROWB = 128, UNIT = 128 * ROWB, STAGE = 4 * UNIT;
+  constexpr int UA0 = 0, UA1 = UNIT, UB0 = 2 * UNIT, UB1 = 3 * UNIT;
+  constexpr int NS = 4 * Store8<OUT>::kStores;
+  constexpr int OSZ = out_size<OUT>();
+  constexpr bool PAIR = is_pair<Mma>::value;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int tiles_n = p.N / 256, ntiles = (p.M / 256) * tiles_n;
+  const int esz = Mma::kElem;
+  const int nk = p.K * esz / ROWB;
+  const int my_tiles =
+      ((int)blockIdx.x < ntiles) ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  if (my_tiles == 0) return;
+
+  const int drow = lane >> 3, dpc = lane & 7;
+  unsigned offA[2][2], offB[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int ur = wave * 16 + i * 8 + drow;
+    const int ch = (dpc ^ ((ur >> 1) & 7)) * 16;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int lr = (ur >> 6) * 128 + q * 64 + (ur & 63);
+      offA[q][i] = (unsigned)(lr * p.lda * esz + ch);
+      const int lc = (ur >> 5) * 64 + q * 32 + t8_perm(ur & 31);
+      offB[q][i] = (unsigned)(lc * p.ldb * esz + ch);
+    }
+  }
+  const char* baseA = nullptr;
+  const char* baseB = nullptr;
+  int src_tile = -1;
+  auto origin = [&](int ti, int64_t& m0, int64_t& n0) __attribute__((always_inline)) {
+    const int wg = tile_index_virtual(p, (int)blockIdx.x + ti * (int)gridDim.x, ntiles);
+    m0 = (int64_t)(wg / tiles_n) * 256;
+    n0 = (int64_t)(wg % tiles_n) * 256;
+  };
+  struct Cur { int ti, kt; };
+  auto adv = [&](Cur& c) __attribute__((always_inline)) {
+    if (c.ti == my_tiles - 1 && c.kt == nk - 1) return;
+    if (++c.kt == nk) { c.kt = 0; ++c.ti; }
+  };
+  auto stage = [&](int which, int unit_off, Cur c, int buf) __attribute__((always_inline)) {
+    if (c.ti != src_tile) {
+      int64_t m0, n0;
+      origin(c.ti, m0, n0);
+      baseA = (const char*)p.a + m0 * p.lda * esz;
+      baseB = (const char*)p.b + n0 * p.ldb * esz;
+      src_tile = c.ti;
+    }
+    const char* base = (which < 2 ? baseA : baseB) + (int64_t)c.kt * ROWB;
+    const unsigned* off = which < 2 ? offA[which] : offB[which - 2];
+    char* dst = smem + buf * STAGE + unit_off + wave * 16 * ROWB;
+    glds16(base + off[0], dst);
+    glds16(base + off[1], dst + 8 * ROWB);
+  };
+  const int frow = lane & 15, fq = lane >> 4, sw = (frow >> 1) & 7;
+  const int c0 = ((0 + fq) ^ sw) * 16, c1 = ((4 + fq) ^ sw) * 16;
+  const int aoff = (wr * 64 + frow) * ROWB, boff = (wc * 32 + frow) * ROWB;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  i32x4 aR[4][2], bR[2][2][2];
+  i32x8 aP[4], bP[2][2];
+  auto loadA = [&](const char* base, int mq) __attribute__((always_inline)) {
+    const char* r = base + (mq ? UA1 : UA0) + aoff;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      if constexpr (PAIR) {
+        aP[f].lo = *(const i32x4*)(r + f * 16 * ROWB + c0);
+        aP[f].hi = *(const i32x4*)(r + f * 16 * ROWB + c1);
+      } else {
+        aR[f][0] = *(const i32x4*)(r + f * 16 * ROWB + c0);
+        aR[f][1] = *(const i32x4*)(r + f * 16 * ROWB + c1);
+      }
+    }
+  };
+  auto loadB = [&](const char* base, int nq) __attribute__((always_inline)) {
+    const char* r = base + (nq ? UB1 : UB0) + boff;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      if constexpr (PAIR) {
+        bP[nq][g].lo = *(const i32x4*)(r + g * 16 * ROWB + c0);
+        bP[nq][g].hi = *(const i32x4*)(r + g * 16 * ROWB + c1);
+      } else {
+        bR[nq][g][0] = *(const i32x4*)(r + g * 16 * ROWB + c0);
+        bR[nq][g][1] = *(const i32x4*)(r + g * 16 * ROWB + c1);
+      }
+    }
+  };
+  auto mm = [&](int mq, int nq) __attribute__((always_inline)) {
+    if constexpr (PAIR) {
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) Mma::step8(acc[mq * 4 + f][nq * 2 + g], bP[nq][g], aP[f]);
+#pragma unroll
+      for (int f = 0; f < 4; ++f)  // pin the pure scaled MFMAs in this section (see t8)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) asm volatile("" : "+v"(acc[mq * 4 + f][nq * 2 + g]));
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int f = 0; f < 4; ++f)
+#pragma unroll
+          for (int g = 0; g < 2; ++g)
+            Mma::step(acc[mq * 4 + f][nq * 2 + g], bR[nq][g][kk], aR[f][kk]);
+    }
+  };
+  int ti = 0;
+  auto store_q = [&](int mq, int nq) __attribute__((always_inline)) {
+    int64_t m0, n0;
+    origin(ti, m0, n0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const int i = mq * 4 + f;
+      const int64_t row = m0 + wr * 128 + mq * 64 + f * 16 + frow;
+      char* dst = (char*)p.c + map_row(row, p.c_grp, p.c_gstride) * p.ldc * OSZ +
+                  (n0 + wc * 64 + nq * 32 + fq * 8) * OSZ;
+      if (p.act == ACT_NONE) Store8<OUT>::st(dst, acc[i][nq * 2], acc[i][nq * 2 + 1]);
+      else Store8<OUT>::st(dst, act4(acc[i][nq * 2], p.act), act4(acc[i][nq * 2 + 1], p.act));
+      acc[i][nq * 2] = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc[i][nq * 2 + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+#define T4_BAR()                         \
+  do {                                   \
+    __builtin_amdgcn_sched_barrier(0);   \
+    __builtin_amdgcn_s_barrier();        \
+    __builtin_amdgcn_sched_barrier(0);   \
+  } while (0)
+#define T4_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+  const bool g1 = wr == 1;  // wave-uniform (wave came through readfirstlane)
+  Cur q0{0, 0}, q1{0, 0};
+  adv(q1);
+  stage(2, UB0, q0, 0);
+  stage(3, UB1, q0, 0);
+  stage(0, UA0, q0, 0);
+  stage(1, UA1, q0, 0);
+  stage(2, UB0, q1, 1);
+  stage(3, UB1, q1, 1);
+  Cur qa = q1, qb = q1;  // K-tile h+1 (A units, phase A) and h+2 (B units, phase B)
+  adv(qb);
+  wait_vm<6>();
+  T4_BAR();
+  if (g1) T4_BAR();
+  // KIND: 0 normal, 1 last K-tile of a tile, 2 first K-tile after a tile's last
+  auto iter = [&](int h, auto kind_tag) __attribute__((always_inline)) {
+    constexpr int KIND = decltype(kind_tag)::value;
+    const int b = h & 1;
+    const char* cur = smem + b * STAGE;
+    loadB(cur, 0);  // phase A
+    loadB(cur, 1);
+    loadA(cur, 0);
+    stage(0, UA0, qa, b ^ 1);
+    stage(1, UA1, qa, b ^ 1);
+    T4_LGKM0();
+    if (g1) wait_vm<KIND == 2 ? 8 + 4 * NS : 8>();
+    T4_BAR();
+    __builtin_amdgcn_s_setprio(1);
+    mm(0, 0);
+    mm(0, 1);
+    __builtin_amdgcn_s_setprio(0);
+    if constexpr (KIND == 1) {
+      store_q(0, 0);
+      store_q(0, 1);
+    }
+    if (!g1) wait_vm<KIND == 1 ? 8 + 2 * NS : (KIND == 2 ? 8 + 4 * NS : 8)>();
+    T4_BAR();
+    loadA(cur, 1);  // phase B
+    stage(2, UB0, qb, b);
+    stage(3, UB1, qb, b);
+    T4_LGKM0();
+    if (g1) wait_vm<KIND == 1 ? 6 + 2 * NS : 6>();
+    T4_BAR();
+    __builtin_amdgcn_s_setprio(1);
+    mm(1, 1);
+    mm(1, 0);
+    __builtin_amdgcn_s_setprio(0);
+    if constexpr (KIND == 1) {
+      store_q(1, 1);
+      store_q(1, 0);
+    }
+    if (!g1) wait_vm<KIND == 1 ? 6 + 4 * NS : 6>();
+    T4_BAR();
+    qa = qb;
+    adv(qb);
+  };
+  int h = 0;
+  for (ti = 0; ti < my_tiles; ++ti) {
+    int t = 0;
+    if (ti > 0) {
+      iter(h, std::integral_constant<int, 2>{});
+      ++h;
+      ++t;
+    }
+    for (; t < nk - 1; ++t, ++h) iter(h, std::integral_constant<int, 0>{});
+    iter(h, std::integral_constant<int, 1>{});
+    ++h;
+  }
+  if (!g1) T4_BAR();
+#undef T4_BAR
+#undef T4_LGKM0
+  wait_vm<0>();  // never leave an LDS-DMA in flight past the end of the workgroup
+}
+
 // ---------------------------------------------------------------- pt8: persistent t8
 // One workgroup per CU streams its tiles' K-tiles back to back (stream index h = tile * nk + kt;
 // the t8 unit schedule above runs unchanged across tile boundaries, so only the first tile pays
@@ -1777,6 +2004,25 @@ hipError_t launch_t4(const GemmArgs& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+// pt4 needs >= 2 K-tiles per tile (its FIRST and LAST K-tile kinds are distinct), plain A rows
+// and 32-bit panel offsets
+bool pt4_ok(const GemmArgs& p, int esz) {
+  return p.M % 256 == 0 && p.N % 256 == 0 && p.flags == nullptr && p.a_table == nullptr &&
+         p.a_grp == p.M && (int64_t)p.K * esz / 128 >= 2 && p.lda * esz <= (1 << 22) &&
+         p.ldb * esz <= (1 << 22);
+}
+
+template <class Mma, int OUT>
+hipError_t launch_pt4(const GemmArgs& p, hipStream_t s) {
+  const int tiles = (p.M / 256) * (p.N / 256);
+  int grid = num_cus();
+  grid = (grid / 8) * 8;  // blockIdx % 8 == XCD group for every virtual tile id
+  if (grid > tiles) grid = tiles;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT>), dim3(grid), dim3(512), 0, s, p);
+  return hipGetLastError();
+}
+
 template <class Mma, int OUT>
 hipError_t launch_pt8(const GemmArgs& p, hipStream_t s) {
   const int tiles = (p.M / 256) * (p.N / 256);
@@ -1801,6 +2047,10 @@ hipError_t launch_cfg(const GemmArgs& p, int tile, hipStream_t s) {
     case TILE_PT8:  // persistent: no arrival flags (a block's tiles are fixed up front)
       if (t8_ok(p) && p.flags == nullptr) return launch_pt8<Mma, OUT>(p, s);
       if (t8_ok(p)) return launch_t8<Mma, OUT>(p, s);
+      return launch_tiled<Mma, OUT, 256, 256, 2, 4, true>(p, s);
+    case TILE_PT4:
+      if (pt4_ok(p, Mma::kElem)) return launch_pt4<Mma, OUT>(p, s);
+      if (t8_ok(p)) return launch_t4<Mma, OUT>(p, s);
       return launch_tiled<Mma, OUT, 256, 256, 2, 4, true>(p, s);
     case TILE_T4:
       if (t8_ok(p)) return launch_t4<Mma, OUT>(p, s);
@@ -1843,7 +2093,8 @@ hipError_t launch_cfg(const GemmArgs& p, int tile, hipStream_t s) {
 template <int OUT>
 hipError_t launch_mx_cfg(const GemmArgs& p, int tile, hipStream_t s) {
   // whole 256x256 tiles: the 8-phase ping-pong schedule (persistent with >= 2 tiles per CU)
-  if (tile == TILE_T4 && t8_ok(p)) return launch_t4<MmaMX, OUT>(p, s);
+  if (tile == TILE_PT4 && pt4_ok(p, 1)) return launch_pt4<MmaMX, OUT>(p, s);
+  if ((tile == TILE_T4 || tile == TILE_PT4) && t8_ok(p)) return launch_t4<MmaMX, OUT>(p, s);
   if ((tile == TILE_T8 || tile == TILE_PT8 || tile == TILE_R256 || tile == TILE_AUTO) && t8_ok(p)) {
     const int tiles = (p.M / 256) * (p.N / 256);
     if (tile != TILE_T8 && p.flags == nullptr && tiles >= 2 * num_cus())
@@ -1862,7 +2113,7 @@ hipError_t launch_mx_cfg(const GemmArgs& p, int tile, hipStream_t s) {
     case TILE_I256W4: return launch_mx<OUT, 256, 256, 2, 2>(p, s);
     case TILE_PI256: return launch_mx<OUT, 256, 256, 2, 4>(p, s);
     case TILE_PI256W4: return launch_mx<OUT, 256, 256, 2, 2>(p, s);
-    case TILE_R256: case TILE_T8: case TILE_PT8: case TILE_T4:
+    case TILE_R256: case TILE_T8: case TILE_PT8: case TILE_T4: case TILE_PT4:
       return launch_mx<OUT, 256, 256, 2, 4>(p, s);
     case TILE_P128: return launch_mx<OUT, 128, 128, 2, 2>(p, s);
     case TILE_256x128_W4: return launch_mx<OUT, 256, 128, 2, 2>(p, s);

@@ -66,15 +66,17 @@ int choose_tile(int64_t M, int64_t N, int64_t K, int din) {
   auto tiles = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
   const int64_t kbytes = K * dtype_size(din);
   // Among the ping-pong kernels (profiles/r01/s2/s2_21_tune_t4.txt, s2_22_fp8_tiles.txt):
-  //  * 16-bit / f32 inputs: t4 (2 phases per K-tile) is fastest on narrow N — the flagship
-  //    65536x1024x1024 115.6 us vs t8 119.1 / pt8 118.4, 65536x1024x8192 747 vs 784 — and t8 on
-  //    wide N (8192^3, 16384x8192x1024: 2-3 % ahead of t4);
+  //  * 16-bit / f32 inputs: t4 (2 phases per K-tile) is faster than t8 / pt8 on narrow N — the
+  //    flagship 65536x1024x1024 115.6 us vs t8 119.1 / pt8 118.4, 65536x1024x8192 747 vs 784;
   //  * fp8 (plain or MX): the persistent pt8 wins with >= 2 short-K tiles per CU (flagship MX-fp8
   //    72.6 us, ahead of hipBLASLt _scaled_mm 73.6), t8 otherwise.
   const bool whole = M % 256 == 0 && N % 256 == 0 && tiles(256, 256) >= 192;
   if (whole && din == DT_FP8)
     return (tiles(256, 256) >= 512 && kbytes <= 2048 && N <= 2048) ? TILE_PT8 : TILE_T8;
-  if (whole) return N >= 4096 ? TILE_T8 : TILE_T4;
+  // pt4 (t4 made persistent) leads t4 / t8 everywhere measured except long K on a wide N
+  // (8192^3: t8 0.80 vs 0.83 ms); it falls back to t4 where it does not apply (shard tables,
+  // grouped A rows, flags, a single K-tile).
+  if (whole) return (kbytes >= 8192 && N >= 4096) ? TILE_T8 : TILE_PT4;
   if (M % 256 == 0 && N % 256 == 0 && tiles(256, 256) >= 256 && kbytes <= 2048) return TILE_R256;
   if (tiles(256, 256) >= 384) return TILE_I256;
   if (tiles(256, 128) >= 384) return TILE_256x128;
@@ -98,8 +100,10 @@ hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mo
     const bool whole = p.M % 256 == 0 && p.N % 256 == 0 && p.shard_rows % 256 == 0;
     if (tile == TILE_AUTO) {
       tile = choose_tile(p.M, p.N, p.K, din);
+      if (tile == TILE_PT4) tile = TILE_T4;  // pt4 reads A through panel offsets, not shard tables
       if (tile != TILE_PT8 && tile != TILE_R256 && tile != TILE_T4) tile = TILE_T8;
     }
+    if (tile == TILE_PT4) tile = TILE_T4;
     if ((tile == TILE_R256 || tile == TILE_T8 || tile == TILE_PT8 || tile == TILE_T4) && !whole)
       tile = TILE_128x128;
     if (mode == GEMM_MODE_GENERIC || !gemm_fast_path_ok(p, din, dout)) return hipErrorNotSupported;

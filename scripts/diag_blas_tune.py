@@ -47,7 +47,7 @@ def main():
         t_blas = timeit(lambda: gemm(A, W, C, mode="blas"))
         t_lin = timeit(lambda: torch.nn.functional.linear(A, W))
         t_own = timeit(lambda: gemm(A, W, C))
-        tiles = {t: timeit(lambda: gemm(A, W, C, tile=t)) for t in ("t8", "pt8", "t4")}
+        tiles = {t: timeit(lambda: gemm(A, W, C, tile=t)) for t in ("t8", "pt8", "t4", "pt4")}
         tf = 2 * m * n * k / 1e12
         print(f"{m}x{n}x{k}: blas[{tag}] {t_blas:7.1f} us ({tf / t_blas * 1e6:6.0f} TF, err "
               f"{err:.3f})  F.linear {t_lin:7.1f} us  own {t_own:7.1f} us  " +

@@ -96,7 +96,7 @@ def test_gemm_fp8(mode, odt, gen):
     torch.testing.assert_close(out.float(), _ref(a, w), rtol=0, atol=_tol(torch.float8_e4m3fn, K))
 
 
-@pytest.mark.parametrize("tile", ["auto", "pp256", "128x128", "256x256w4", "256x128w4", "p256", "p128", "i256", "i128", "i256w4", "pi256", "r256", "t8", "pt8", "t4"])
+@pytest.mark.parametrize("tile", ["auto", "pp256", "128x128", "256x256w4", "256x128w4", "p256", "p128", "i256", "i128", "i256w4", "pi256", "r256", "t8", "pt8", "t4", "pt4"])
 def test_fp8_integer_exact(gen, tile):
     """Small integers are exact in e4m3: both fp8 paths must match bit for bit."""
     from ddlb_amd.ops.gemm import gemm
@@ -161,7 +161,7 @@ def test_host_checks_reject_bad_shapes(gen):
         gemm(a, _rand((64, 128), torch.bfloat16, gen), M=128)
 
 
-@pytest.mark.parametrize("tile", ["p256", "p128", "pi256", "r256", "pt8"])
+@pytest.mark.parametrize("tile", ["p256", "p128", "pi256", "r256", "pt8", "pt4"])
 def test_persistent_many_tiles_grouped(gen, tile):
     """Persistent streaming kernel: more tiles than blocks, grouped C rows, repeat-identical."""
     from ddlb_amd.ops.gemm import gemm
@@ -184,7 +184,7 @@ def test_persistent_many_tiles_grouped(gen, tile):
 
 
 @pytest.mark.parametrize("act", ["gelu", "relu", "silu"])
-@pytest.mark.parametrize("tile", ["auto", "128x128", "pi256", "r256", "t8", "pt8", "t4"])
+@pytest.mark.parametrize("tile", ["auto", "128x128", "pi256", "r256", "t8", "pt8", "t4", "pt4"])
 def test_fused_activation_epilogue(gen, act, tile):
     from ddlb_amd.ops.gemm import gemm
     from ddlb_amd.parallel.sim import apply_act
@@ -286,7 +286,7 @@ def test_blas_mode_falls_back_for_fused(gen):
     torch.testing.assert_close(out8.float(), _ref(a8, w8), rtol=0, atol=_tol(torch.float8_e4m3fn, 256))
 
 
-@pytest.mark.parametrize("tile", ["t8", "pt8", "t4"])
+@pytest.mark.parametrize("tile", ["t8", "pt8", "t4", "pt4"])
 @pytest.mark.parametrize("dt", _RING_DT, ids=lambda d: f"{str(d[0])[6:]}-{str(d[1])[6:]}")
 @pytest.mark.parametrize("shape", [(256, 256, 64), (256, 256, 128), (8192, 1024, 512),
                                    (4096, 768, 1024), (2048, 2048, 3072), (65536, 1024, 128)])
@@ -310,7 +310,7 @@ def test_t8_kernel(dt, shape, gen, tile):
     assert torch.equal(out, again)
 
 
-@pytest.mark.parametrize("tile", ["t8", "pt8", "t4"])
+@pytest.mark.parametrize("tile", ["t8", "pt8", "t4", "pt4"])
 def test_t8_grouped_rows_and_race_screen(gen, tile):
     """t8 with the pipelines' strided A and C row blocks, then 50 launches of a large square
     GEMM compared bit for bit (a new sync template: RAW/WAR screen over many runs)."""
@@ -337,7 +337,7 @@ def test_t8_grouped_rows_and_race_screen(gen, tile):
     torch.testing.assert_close(first.float(), _ref(a, w), rtol=0, atol=_tol(torch.bfloat16, 4096))
 
 
-@pytest.mark.parametrize("tile", ["t8", "pt8", "t4"])
+@pytest.mark.parametrize("tile", ["t8", "pt8", "t4", "pt4"])
 @pytest.mark.parametrize("shape", [(256, 256, 128), (2048, 768, 1024), (65536, 1024, 256)])
 def test_t8_mx_fp8(tile, shape, gen):
     """Block-scaled MX-fp8 on the 8-phase schedule (one 16x16x128 scaled MFMA per 128-byte
