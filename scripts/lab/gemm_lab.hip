@@ -1531,6 +1531,166 @@ __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
   wait_vm<0>();
 }
 
+
+// q4: one wave per SIMD. 256x256 tile, 4 waves (2x2) of 128x128, accumulators (256 per lane) in
+// AGPRs, fragments double-buffered in VGPRs. Same 16 KB units / swizzle / B permutation as t8
+// (UA0 = A rows {0-63,128-191}, UB0 = B cols {0-63,128-191} permuted per 32). A K-tile is 4
+// sections of 32 MFMAs (one 64x64 quadrant each); each section reads one fragment set (8
+// ds_read_b128) for the next section, snake order by K-tile parity so a set is loaded into
+// registers whose last reader has finished:
+//   even h: Q00 (ld B1 h) Q01 (ld A1 h) | Q11 (ld A0 h+1) Q10 (ld B1 h+1)
+//   odd  h: Q01 (ld B0 h) Q00 (ld A1 h) | Q10 (ld A0 h+1) Q11 (ld B0 h+1)
+// "|" = the one barrier per K-tile: K-tile h+1 landed (vmcnt 0) and every read of K-tile h done,
+// so the LDS-DMA of K-tile h+2 into h's buffer is issued right after it (S3 + S4).
+template <int SCHED, int SKIP = 0>  // SKIP (timing ablations, wrong results): 1 no loop DMA,
+__global__ __launch_bounds__(256) void q4_kernel(const Args p) {  // 2 no loop barrier, 4 no MFMA
+  constexpr int ROWB = 128, UNIT = 128 * ROWB, STAGE = 4 * UNIT;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int tiles_n = p.N / 256, ntiles = (p.M / 256) * tiles_n;
+  const int wg = xcd_remap((int)blockIdx.x, ntiles);
+  const int64_t m0 = (int64_t)(wg / tiles_n) * 256, n0 = (int64_t)(wg % tiles_n) * 256;
+  const int nk = p.K / 64;
+  // LDS-DMA: wave stages unit rows [32w, 32w+32) of each unit, 4 x 1 KB instructions per unit.
+  // Sources = wave-uniform row bases + one of two per-lane 32-bit offsets (the swizzle repeats
+  // every 16 rows, so instructions i and i+2 share a lane pattern).
+  const int drow = lane >> 3, dpc = lane & 7;
+  int offA[2], offB[4];  // per-lane 32-bit source offsets
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int ch = (dpc ^ (((i * 8 + drow) >> 1) & 7)) * 16;
+    if (i < 2) offA[i] = (int)(drow * p.lda * 2) + ch;
+    offB[i] = (int)(t8_perm(i * 8 + drow) * p.ldb * 2) + ch;
+  }
+  // wave-uniform bases: A unit row ur = wave*32 + i*8 + drow -> A row (ur>>6)*128 + q*64 + (ur&63)
+  const char* baseA = (const char*)p.a + (m0 + (wave >> 1) * 128 + (wave & 1) * 32) * p.lda * 2;
+  //                   B unit row -> column (ur>>6)*128 + q*64 + ((ur&63)>>5)*32 + perm(ur&31)
+  const char* baseB = (const char*)p.b + (n0 + (wave >> 1) * 128 + (wave & 1) * 32) * p.ldb * 2;
+  auto stage_half = [&](int kt, int buf, int half) __attribute__((always_inline)) {
+    if ((SKIP & 1) && kt >= 2) return;
+    kt = kt < nk ? kt : nk - 1;  // past the end: K-tile nk-1 again into a buffer no one reads
+    char* st = smem + buf * STAGE + wave * 32 * ROWB;
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const char* src = half == 0
+            ? baseA + ((int64_t)(q * 64 + i * 8) * p.lda * 2 + (int64_t)kt * ROWB) + offA[i & 1]
+            : baseB + ((int64_t)(q * 64) * p.ldb * 2 + (int64_t)kt * ROWB) + offB[i];
+        glds16(src, st + (half * 2 + q) * UNIT + i * 8 * ROWB);
+      }
+  };
+  const int frow = lane & 15, fq = lane >> 4, sw = (frow >> 1) & 7;
+  const int c0 = ((0 + fq) ^ sw) * 16, c1 = ((4 + fq) ^ sw) * 16;
+  const int aoff = (wr * 64 + frow) * ROWB, boff = (wc * 64 + frow) * ROWB;
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  i32x4 aR[2][4][2], bR[2][4][2];  // [quadrant][fragment][K-half]
+  auto ldA = [&](int kt, int mq) __attribute__((always_inline)) {
+    const char* r = smem + (kt & 1) * STAGE + mq * UNIT + aoff;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      aR[mq][f][0] = *(const i32x4*)(r + f * 16 * ROWB + c0);
+      aR[mq][f][1] = *(const i32x4*)(r + f * 16 * ROWB + c1);
+    }
+  };
+  auto ldB = [&](int kt, int nq) __attribute__((always_inline)) {
+    const char* r = smem + (kt & 1) * STAGE + (2 + nq) * UNIT + boff;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bR[nq][g][0] = *(const i32x4*)(r + g * 16 * ROWB + c0);
+      bR[nq][g][1] = *(const i32x4*)(r + g * 16 * ROWB + c1);
+    }
+  };
+  auto mm = [&](int mq, int nq) __attribute__((always_inline)) {
+    if constexpr (SKIP & 4) {
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) asm volatile("" :: "v"(aR[mq][f][0]), "v"(bR[nq][g][1]));
+      return;
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          acc[mq * 4 + f][nq * 4 + g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8, bR[nq][g][kk]), __builtin_bit_cast(bf16x8, aR[mq][f][kk]),
+              acc[mq * 4 + f][nq * 4 + g], 0, 0, 0);
+#pragma unroll
+    for (int f = 0; f < 4; ++f)  // keep every accumulator in AGPRs (no loop-carried copies)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) asm volatile("" : "+a"(acc[mq * 4 + f][nq * 4 + g]));
+  };
+  // interleave: 1 MFMA then 1 DS read for the first 8 MFMAs (+ VMEM in the DMA sections)
+  auto pace = [&](int vmem) __attribute__((always_inline)) {
+    if constexpr (SCHED == 1) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        if (vmem) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 24, 0);
+    }
+  };
+// section boundary: the previous section's fragment reads (a whole section of MFMAs old) must
+// have landed before this section issues its own, so its MFMAs never wait on the new reads
+// (a real S_WAITCNT the compiler's waitcnt pass sees: lgkmcnt(0), vmcnt/expcnt untouched)
+#define Q4_SEC()                            \
+  do {                                      \
+    __builtin_amdgcn_sched_barrier(0);      \
+    __builtin_amdgcn_s_waitcnt(0xC07F);     \
+    __builtin_amdgcn_sched_barrier(0);      \
+  } while (0)
+  // prologue: K-tiles 0 and 1 in flight, K-tile 0 landed, first sets A0(0) B0(0) in registers
+  stage_half(0, 0, 0);
+  stage_half(0, 0, 1);
+  stage_half(1, 1, 0);
+  stage_half(1, 1, 1);
+  wait_vm<16>();
+  __builtin_amdgcn_s_barrier();
+  ldA(0, 0);
+  ldB(0, 0);
+  for (int h = 0; h < nk; h += 2) {
+    // ---- even K-tile h
+    Q4_SEC(); ldB(h, 1); mm(0, 0); pace(0);
+    Q4_SEC(); ldA(h, 1); mm(0, 1); pace(0);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    if constexpr (!(SKIP & 2)) __builtin_amdgcn_s_barrier();
+    Q4_SEC(); ldA(h + 1, 0); stage_half(h + 2, 0, 0); mm(1, 1); pace(1);
+    Q4_SEC(); ldB(h + 1, 1); stage_half(h + 2, 0, 1); mm(1, 0); pace(1);
+    // ---- odd K-tile h+1
+    Q4_SEC(); ldB(h + 1, 0); mm(0, 1); pace(0);
+    Q4_SEC(); ldA(h + 1, 1); mm(0, 0); pace(0);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    if constexpr (!(SKIP & 2)) __builtin_amdgcn_s_barrier();
+    Q4_SEC(); ldA(h + 2, 0); stage_half(h + 3, 1, 0); mm(1, 0); pace(1);
+    Q4_SEC(); ldB(h + 2, 0); stage_half(h + 3, 1, 1); mm(1, 1); pace(1);
+  }
+#undef Q4_SEC
+  wait_vm<0>();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    char* crow = (char*)p.c + (m0 + wr * 128 + (i >> 2) * 64 + (i & 3) * 16 + frow) * p.ldc * 2;
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      const f32x4 v0 = acc[i][j], v1 = acc[i][j + 1];
+      bf16x8 o = {(__bf16)v0.x, (__bf16)v0.y, (__bf16)v0.z, (__bf16)v0.w,
+                  (__bf16)v1.x, (__bf16)v1.y, (__bf16)v1.z, (__bf16)v1.w};
+      *(uint4*)(crow + (n0 + wc * 128 + (j >> 2) * 64 + ((j >> 1) & 1) * 32 + fq * 8) * 2) =
+          __builtin_bit_cast(uint4, o);
+    }
+  }
+}
+
 // fp32 reference: C[m][n] = sum_k A[m][k] * B[n][k]
 __global__ void ref_kernel(const __hip_bfloat16* A, const __hip_bfloat16* B, float* C, int M, int N,
                            int K) {
@@ -1607,6 +1767,11 @@ int main(int argc, char** argv) {
       {"t8b", t8b_kernel<false>, 2, 512, 1},
       {"t4", t4_kernel<false>, 2, 512, 1},
       {"pt4", pt4_kernel<false>, 2, 512, 0},
+      {"q4", q4_kernel<0>, 2, 256, 1},
+      {"q4 noDMA", q4_kernel<0, 1>, 2, 256, 1},
+      {"q4 noBAR", q4_kernel<0, 2>, 2, 256, 1},
+      {"q4 noDMA noBAR", q4_kernel<0, 3>, 2, 256, 1},
+      {"q4 noMFMA", q4_kernel<0, 4>, 2, 256, 1},
   };
   Args a{A, B, C, K, K, N, M, N, K, nullptr};
   const char* only = getenv("LAB_ONLY");  // profile one variant: skip the others
