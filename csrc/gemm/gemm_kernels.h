@@ -69,6 +69,24 @@ __device__ __forceinline__ int tile_index_virtual(const GemmArgs& p, int vid, in
   return shard * per + xcd_remap(local, per);
 }
 
+// Tile id -> (tm, tn). Row-major, except that without a shard order and with more than 4 column
+// tiles, ids are rastered in groups of 8 m-blocks (column-major inside a group): the 32 tiles an
+// XCD runs together (consecutive ids after xcd_remap) then cover 8 m-blocks x 4 n-blocks, i.e. 12
+// A / B panels in its L2 instead of 1 + 32 (guide §5, L2 reuse per XCD). Bijective.
+__device__ __forceinline__ void tile_mn(const GemmArgs& p, int wg, int tiles_m, int tiles_n,
+                                        int& tm, int& tn) {
+  constexpr int G = 8;
+  if (p.tile_order || tiles_n <= 4) {
+    tm = wg / tiles_n;
+    tn = wg % tiles_n;
+    return;
+  }
+  const int per = G * tiles_n, grp = wg / per, first = grp * G;
+  const int gs = tiles_m - first < G ? tiles_m - first : G, in = wg - grp * per;
+  tm = first + in % gs;
+  tn = in / gs;
+}
+
 // ---------------------------------------------------------------- MFMA "consume 16 bytes" ops
 struct MmaBF16 {
   static constexpr int kElem = 2, kMfma = 1;  // bytes per element, MFMAs per 16-byte step
@@ -982,7 +1000,9 @@ __global__ __launch_bounds__(512) void gemm_tn_t8_kernel(const GemmArgs p) {
   const int wr = wave >> 2, wc = wave & 3;
   const int tiles_n = p.N / 256, ntiles = (p.M / 256) * tiles_n;
   const int wg = tile_index(p, ntiles);
-  const int64_t m0 = (int64_t)(wg / tiles_n) * 256, n0 = (int64_t)(wg % tiles_n) * 256;
+  int tm_, tn_;
+  tile_mn(p, wg, p.M / 256, tiles_n, tm_, tn_);
+  const int64_t m0 = (int64_t)tm_ * 256, n0 = (int64_t)tn_ * 256;
   const int esz = Mma::kElem;
   const int nk = p.K * esz / ROWB;
 
@@ -1165,7 +1185,9 @@ __global__ __launch_bounds__(512) void gemm_tn_t4_kernel(const GemmArgs p) {
   const int wr = wave >> 2, wc = wave & 3;
   const int tiles_n = p.N / 256, ntiles = (p.M / 256) * tiles_n;
   const int wg = tile_index(p, ntiles);
-  const int64_t m0 = (int64_t)(wg / tiles_n) * 256, n0 = (int64_t)(wg % tiles_n) * 256;
+  int tm_, tn_;
+  tile_mn(p, wg, p.M / 256, tiles_n, tm_, tn_);
+  const int64_t m0 = (int64_t)tm_ * 256, n0 = (int64_t)tn_ * 256;
   const int esz = Mma::kElem;
   const int nk = p.K * esz / ROWB;
 
@@ -1364,8 +1386,10 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   int src_tile = -1;
   auto origin = [&](int ti, int64_t& m0, int64_t& n0) __attribute__((always_inline)) {
     const int wg = tile_index_virtual(p, (int)blockIdx.x + ti * (int)gridDim.x, ntiles);
-    m0 = (int64_t)(wg / tiles_n) * 256;
-    n0 = (int64_t)(wg % tiles_n) * 256;
+    int tm_, tn_;
+    tile_mn(p, wg, p.M / 256, tiles_n, tm_, tn_);
+    m0 = (int64_t)tm_ * 256;
+    n0 = (int64_t)tn_ * 256;
   };
   struct Cur { int ti, kt; };
   auto adv = [&](Cur& c) __attribute__((always_inline)) {
@@ -1574,8 +1598,10 @@ __global__ __launch_bounds__(512) void gemm_tn_pt8_kernel(const GemmArgs p) {
   int src_tile = -1;
   auto tile_origin = [&](int ti, int64_t& m0, int64_t& n0) __attribute__((always_inline)) {
     const int wg = tile_index_virtual(p, (int)blockIdx.x + ti * (int)gridDim.x, ntiles);
-    m0 = (int64_t)(wg / tiles_n) * 256;
-    n0 = (int64_t)(wg % tiles_n) * 256;
+    int tm_, tn_;
+    tile_mn(p, wg, p.M / 256, tiles_n, tm_, tn_);
+    m0 = (int64_t)tm_ * 256;
+    n0 = (int64_t)tn_ * 256;
   };
   auto set_src = [&](int ti) __attribute__((always_inline)) {
     int64_t m0, n0;

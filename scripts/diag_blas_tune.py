@@ -11,7 +11,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from ddlb_amd.ops.gemm import gemm  # noqa: E402
 
 SHAPES = [(65536, 1024, 1024), (8192, 1024, 1024), (16384, 1024, 1024), (8192, 1024, 8192),
-          (65536, 1024, 8192), (16384, 8192, 1024)]
+          (65536, 1024, 8192), (16384, 8192, 1024), (8192, 8192, 8192), (4096, 4096, 4096)]
 
 
 def timeit(fn, reps=50, rounds=5):

@@ -289,7 +289,8 @@ def test_blas_mode_falls_back_for_fused(gen):
 @pytest.mark.parametrize("tile", ["t8", "pt8", "t4", "pt4"])
 @pytest.mark.parametrize("dt", _RING_DT, ids=lambda d: f"{str(d[0])[6:]}-{str(d[1])[6:]}")
 @pytest.mark.parametrize("shape", [(256, 256, 64), (256, 256, 128), (8192, 1024, 512),
-                                   (4096, 768, 1024), (2048, 2048, 3072), (65536, 1024, 128)])
+                                   (4096, 768, 1024), (2048, 2048, 3072), (65536, 1024, 128),
+                                   (3328, 1536, 256)])  # grouped raster: 13 m-blocks, 6 n
 def test_t8_kernel(dt, shape, gen, tile):
     """8-phase ping-pong kernel and its persistent form: one K-tile (the clamped prefetch path),
     two, odd K-tile counts, N not a power of two, several tiles per persistent block (C quadrant
