@@ -1348,7 +1348,7 @@ __global__ __launch_bounds__(512) void t4_kernel(const Args p) {
 //   normal:            A end 8, B end 6
 //   LAST of a tile:    A end g0 8+2NS / g1 8,   B end g0 6+4NS / g1 6+2NS
 //   FIRST after LAST:  A end 8+4NS (both),      B end 6
-template <bool STAMP>
+template <bool STAMP, int SKIP = 0>  // SKIP (timing ablations): 1 no LDS-DMA after the first 2 K-tiles, 4 no MFMA
 __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
   constexpr int ROWB = 128, UNIT = 128 * ROWB, STAGE = 4 * UNIT;
   constexpr int UA0 = 0, UA1 = UNIT, UB0 = 2 * UNIT, UB1 = 3 * UNIT;
@@ -1392,6 +1392,9 @@ __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
     if (++c.kt == nk) { c.kt = 0; ++c.ti; }
   };
   auto stage = [&](int which, int unit_off, Cur c, int buf) __attribute__((always_inline)) {
+    if constexpr ((SKIP & 1) != 0) {
+      if (c.ti > 0 || c.kt >= 2) return;
+    }
     if (c.ti != src_tile) {
       int64_t m0, n0;
       origin(c.ti, m0, n0);
@@ -1431,6 +1434,11 @@ __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
     }
   };
   auto mm = [&](int mq, int nq) __attribute__((always_inline)) {
+    if constexpr ((SKIP & 4) != 0) {
+#pragma unroll
+      for (int f = 0; f < 4; ++f) asm volatile("" ::"v"(aR[f][0]), "v"(bR[nq][0][1]));
+      return;
+    }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -1530,6 +1538,203 @@ __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
 #undef T4_LGKM0
   wait_vm<0>();
 }
+
+
+template <bool STAMP, int SKIP = 0>  // SKIP (timing ablations): 1 no LDS-DMA after the first 2 K-tiles, 4 no MFMA
+__global__ __launch_bounds__(512) void pt4b_kernel(const Args p) {
+  constexpr int ROWB = 128, UNIT = 128 * ROWB, STAGE = 4 * UNIT;
+  constexpr int UA0 = 0, UA1 = UNIT, UB0 = 2 * UNIT, UB1 = 3 * UNIT;
+  constexpr int NS = 4;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int tiles_n = p.N / 256, ntiles = (p.M / 256) * tiles_n;
+  const int nk = p.K / 64;
+  const int my_tiles =
+      ((int)blockIdx.x < ntiles) ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  if (my_tiles == 0) return;
+  // LDS-DMA sources: per-lane 32-bit byte offsets inside a tile's A / B panels (row * ld + swizzled
+  // chunk) plus wave-uniform panel bases, so the per-tile state is two scalar pointers
+  const int drow = lane >> 3, dpc = lane & 7;
+  unsigned offA[2][2], offB[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int ur = wave * 16 + i * 8 + drow;
+    const int ch = (dpc ^ ((ur >> 1) & 7)) * 16;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int lr = (ur >> 6) * 128 + q * 64 + (ur & 63);
+      offA[q][i] = (unsigned)(lr * p.lda * 2 + ch);
+      const int lc = (ur >> 5) * 64 + q * 32 + t8_perm(ur & 31);
+      offB[q][i] = (unsigned)(lc * p.ldb * 2 + ch);
+    }
+  }
+  const char* baseA = nullptr;
+  const char* baseB = nullptr;
+  int src_tile = -1;
+  auto origin = [&](int ti, int64_t& m0, int64_t& n0) __attribute__((always_inline)) {
+    const int wg = xcd_remap((int)blockIdx.x + ti * (int)gridDim.x, ntiles);
+    m0 = (int64_t)(wg / tiles_n) * 256;
+    n0 = (int64_t)(wg % tiles_n) * 256;
+  };
+  struct Cur { int ti, kt; };
+  auto adv = [&](Cur& c) __attribute__((always_inline)) {
+    if (c.ti == my_tiles - 1 && c.kt == nk - 1) return;
+    if (++c.kt == nk) { c.kt = 0; ++c.ti; }
+  };
+  auto stage = [&](int which, int unit_off, Cur c, int buf) __attribute__((always_inline)) {
+    if constexpr ((SKIP & 1) != 0) {
+      if (c.ti > 0 || c.kt >= 2) return;
+    }
+    if (c.ti != src_tile) {
+      int64_t m0, n0;
+      origin(c.ti, m0, n0);
+      baseA = (const char*)p.a + m0 * p.lda * 2;
+      baseB = (const char*)p.b + n0 * p.ldb * 2;
+      src_tile = c.ti;
+    }
+    const char* base = (which < 2 ? baseA : baseB) + (int64_t)c.kt * ROWB;
+    const unsigned* off = which < 2 ? offA[which] : offB[which - 2];
+    char* dst = smem + buf * STAGE + unit_off + wave * 16 * ROWB;
+    glds16(base + off[0], dst);
+    glds16(base + off[1], dst + 8 * ROWB);
+  };
+  const int frow = lane & 15, fq = lane >> 4, sw = (frow >> 1) & 7;
+  const int c0 = ((0 + fq) ^ sw) * 16, c1 = ((4 + fq) ^ sw) * 16;
+  const int aoff = (wr * 64 + frow) * ROWB, boff = (wc * 32 + frow) * ROWB;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  i32x4 aR[4][2], bR[2][2][2];
+  auto loadA = [&](const char* base, int mq) __attribute__((always_inline)) {
+    const char* r = base + (mq ? UA1 : UA0) + aoff;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      aR[f][0] = *(const i32x4*)(r + f * 16 * ROWB + c0);
+      aR[f][1] = *(const i32x4*)(r + f * 16 * ROWB + c1);
+    }
+  };
+  auto loadB = [&](const char* base, int nq) __attribute__((always_inline)) {
+    const char* r = base + (nq ? UB1 : UB0) + boff;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      bR[nq][g][0] = *(const i32x4*)(r + g * 16 * ROWB + c0);
+      bR[nq][g][1] = *(const i32x4*)(r + g * 16 * ROWB + c1);
+    }
+  };
+  auto mm = [&](int mq, int nq) __attribute__((always_inline)) {
+    if constexpr ((SKIP & 4) != 0) {
+#pragma unroll
+      for (int f = 0; f < 4; ++f) asm volatile("" ::"v"(aR[f][0]), "v"(bR[nq][0][1]));
+      return;
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+          acc[mq * 4 + f][nq * 2 + g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8, bR[nq][g][kk]), __builtin_bit_cast(bf16x8, aR[f][kk]),
+              acc[mq * 4 + f][nq * 2 + g], 0, 0, 0);
+  };
+  int ti = 0;
+  auto store_q = [&](int mq, int nq) __attribute__((always_inline)) {
+    int64_t m0, n0;
+    origin(ti, m0, n0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const int i = mq * 4 + f;
+      char* crow = (char*)p.c + (m0 + wr * 128 + mq * 64 + f * 16 + frow) * p.ldc * 2;
+      const f32x4 v0 = acc[i][nq * 2], v1 = acc[i][nq * 2 + 1];
+      bf16x8 o = {(__bf16)v0.x, (__bf16)v0.y, (__bf16)v0.z, (__bf16)v0.w,
+                  (__bf16)v1.x, (__bf16)v1.y, (__bf16)v1.z, (__bf16)v1.w};
+      *(uint4*)(crow + (n0 + wc * 64 + nq * 32 + fq * 8) * 2) = __builtin_bit_cast(uint4, o);
+      acc[i][nq * 2] = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc[i][nq * 2 + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+#define T4_BAR()                         \
+  do {                                   \
+    __builtin_amdgcn_sched_barrier(0);   \
+    __builtin_amdgcn_s_barrier();        \
+    __builtin_amdgcn_sched_barrier(0);   \
+  } while (0)
+#define T4_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+  const bool g1 = wr == 1;
+  // every unit restaged right after its last read: phase A of h stages A1(h+1) (A1(h-1) was
+  // read in phase B of h-1), phase B of h stages A0 / B0 / B1 of h+2 (read in phase A of h).
+  // Cursors: qa = h+1, qb = h+2. Prologue = the steady-state issue order up to the end of phase B
+  // of K-tile -1: A0 B0 B1 (0), A1 (0), A0 B0 B1 (1); 8 younger than B1(0).
+  Cur q0{0, 0}, q1{0, 0};
+  adv(q1);
+  stage(0, UA0, q0, 0);
+  stage(2, UB0, q0, 0);
+  stage(3, UB1, q0, 0);
+  stage(1, UA1, q0, 0);
+  stage(0, UA0, q1, 1);
+  stage(2, UB0, q1, 1);
+  stage(3, UB1, q1, 1);
+  Cur qa = q1, qb = q1;
+  adv(qb);
+  wait_vm<8>();
+  T4_BAR();
+  if (g1) T4_BAR();
+  // KIND: 0 normal, 1 last K-tile of a tile, 2 first K-tile after a tile's last
+  auto iter = [&](int h, auto kind_tag) __attribute__((always_inline)) {
+    constexpr int KIND = decltype(kind_tag)::value;
+    const int b = h & 1;
+    const char* cur = smem + b * STAGE;
+    loadB(cur, 0);  // phase A
+    loadB(cur, 1);
+    loadA(cur, 0);
+    stage(1, UA1, qa, b ^ 1);
+    T4_LGKM0();
+    if (g1) wait_vm<KIND == 2 ? 8 + 4 * NS : 8>();
+    T4_BAR();
+    __builtin_amdgcn_s_setprio(1);
+    mm(0, 0);
+    mm(0, 1);
+    __builtin_amdgcn_s_setprio(0);
+    if constexpr (KIND == 1) { store_q(0, 0); store_q(0, 1); }
+    if (!g1) wait_vm<KIND == 1 ? 8 + 2 * NS : (KIND == 2 ? 8 + 4 * NS : 8)>();
+    T4_BAR();
+    loadA(cur, 1);  // phase B
+    stage(0, UA0, qb, b);
+    stage(2, UB0, qb, b);
+    stage(3, UB1, qb, b);
+    T4_LGKM0();
+    if (g1) wait_vm<KIND == 0 ? 8 : 8 + 2 * NS>();
+    T4_BAR();
+    __builtin_amdgcn_s_setprio(1);
+    mm(1, 1);
+    mm(1, 0);
+    __builtin_amdgcn_s_setprio(0);
+    if constexpr (KIND == 1) { store_q(1, 1); store_q(1, 0); }
+    if (!g1) wait_vm<KIND == 1 ? 8 + 4 * NS : (KIND == 2 ? 8 + 2 * NS : 8)>();
+    T4_BAR();
+    qa = qb;
+    adv(qb);
+  };
+  int h = 0;
+  for (ti = 0; ti < my_tiles; ++ti) {
+    int t = 0;
+    if (ti > 0) { iter(h, std::integral_constant<int, 2>{}); ++h; ++t; }
+    for (; t < nk - 1; ++t, ++h) iter(h, std::integral_constant<int, 0>{});
+    iter(h, std::integral_constant<int, 1>{});
+    ++h;
+  }
+  if (!g1) T4_BAR();
+#undef T4_BAR
+#undef T4_LGKM0
+  wait_vm<0>();
+}
+
 
 
 // q4: one wave per SIMD. 256x256 tile, 4 waves (2x2) of 128x128, accumulators (256 per lane) in
@@ -1767,6 +1972,9 @@ int main(int argc, char** argv) {
       {"t8b", t8b_kernel<false>, 2, 512, 1},
       {"t4", t4_kernel<false>, 2, 512, 1},
       {"pt4", pt4_kernel<false>, 2, 512, 0},
+      {"pt4b", pt4b_kernel<false>, 2, 512, 0},
+      {"pt4 noDMA", pt4_kernel<false, 1>, 2, 512, 0},
+      {"pt4 noMFMA", pt4_kernel<false, 4>, 2, 512, 0},
       {"q4", q4_kernel<0>, 2, 256, 1},
       {"q4 noDMA", q4_kernel<0, 1>, 2, 256, 1},
       {"q4 noBAR", q4_kernel<0, 2>, 2, 256, 1},
