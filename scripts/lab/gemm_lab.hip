@@ -1348,7 +1348,7 @@ __global__ __launch_bounds__(512) void t4_kernel(const Args p) {
 //   normal:            A end 8, B end 6
 //   LAST of a tile:    A end g0 8+2NS / g1 8,   B end g0 6+4NS / g1 6+2NS
 //   FIRST after LAST:  A end 8+4NS (both),      B end 6
-template <bool STAMP, int SKIP = 0>  // SKIP (timing ablations): 1 no LDS-DMA after the first 2 K-tiles, 4 no MFMA
+template <bool STAMP, int SKIP = 0>  // SKIP (timing ablations): 1 no LDS-DMA after the first 2 K-tiles, 2 no C stores, 4 no MFMA, 8 no LDS reads
 __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
   constexpr int ROWB = 128, UNIT = 128 * ROWB, STAGE = 4 * UNIT;
   constexpr int UA0 = 0, UA1 = UNIT, UB0 = 2 * UNIT, UB1 = 3 * UNIT;
@@ -1418,6 +1418,7 @@ __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   i32x4 aR[4][2], bR[2][2][2];
   auto loadA = [&](const char* base, int mq) __attribute__((always_inline)) {
+    if constexpr ((SKIP & 8) != 0) return;
     const char* r = base + (mq ? UA1 : UA0) + aoff;
 #pragma unroll
     for (int f = 0; f < 4; ++f) {
@@ -1426,6 +1427,7 @@ __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
     }
   };
   auto loadB = [&](const char* base, int nq) __attribute__((always_inline)) {
+    if constexpr ((SKIP & 8) != 0) return;
     const char* r = base + (nq ? UB1 : UB0) + boff;
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
@@ -1451,6 +1453,11 @@ __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
   };
   int ti = 0;
   auto store_q = [&](int mq, int nq) __attribute__((always_inline)) {
+    if constexpr ((SKIP & 2) != 0) {
+#pragma unroll
+      for (int f = 0; f < 4; ++f) asm volatile("" ::"v"(acc[mq * 4 + f][nq * 2]), "v"(acc[mq * 4 + f][nq * 2 + 1]));
+      return;
+    }
     int64_t m0, n0;
     origin(ti, m0, n0);
     __builtin_amdgcn_sched_barrier(0);
@@ -1461,7 +1468,12 @@ __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
       const f32x4 v0 = acc[i][nq * 2], v1 = acc[i][nq * 2 + 1];
       bf16x8 o = {(__bf16)v0.x, (__bf16)v0.y, (__bf16)v0.z, (__bf16)v0.w,
                   (__bf16)v1.x, (__bf16)v1.y, (__bf16)v1.z, (__bf16)v1.w};
-      *(uint4*)(crow + (n0 + wc * 64 + nq * 32 + fq * 8) * 2) = __builtin_bit_cast(uint4, o);
+      if constexpr ((SKIP & 16) != 0) {  // non-temporal (streaming) store: C is never re-read
+        __builtin_nontemporal_store(__builtin_bit_cast(i32x4, o),
+                                    (i32x4*)(crow + (n0 + wc * 64 + nq * 32 + fq * 8) * 2));
+      } else {
+        *(uint4*)(crow + (n0 + wc * 64 + nq * 32 + fq * 8) * 2) = __builtin_bit_cast(uint4, o);
+      }
       acc[i][nq * 2] = f32x4{0.f, 0.f, 0.f, 0.f};
       acc[i][nq * 2 + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
@@ -1540,7 +1552,7 @@ __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
 }
 
 
-template <bool STAMP, int SKIP = 0>  // SKIP (timing ablations): 1 no LDS-DMA after the first 2 K-tiles, 4 no MFMA
+template <bool STAMP, int SKIP = 0>  // SKIP (timing ablations): 1 no LDS-DMA after the first 2 K-tiles, 2 no C stores, 4 no MFMA, 8 no LDS reads
 __global__ __launch_bounds__(512) void pt4b_kernel(const Args p) {
   constexpr int ROWB = 128, UNIT = 128 * ROWB, STAGE = 4 * UNIT;
   constexpr int UA0 = 0, UA1 = UNIT, UB0 = 2 * UNIT, UB1 = 3 * UNIT;
@@ -1975,6 +1987,11 @@ int main(int argc, char** argv) {
       {"pt4b", pt4b_kernel<false>, 2, 512, 0},
       {"pt4 noDMA", pt4_kernel<false, 1>, 2, 512, 0},
       {"pt4 noMFMA", pt4_kernel<false, 4>, 2, 512, 0},
+      {"pt4 nt", pt4_kernel<false, 16>, 2, 512, 0},
+      {"pt4 noST", pt4_kernel<false, 2>, 2, 512, 0},
+      {"pt4 noLDSrd", pt4_kernel<false, 8>, 2, 512, 0},
+      {"pt4 noDMA noST", pt4_kernel<false, 3>, 2, 512, 0},
+      {"pt4 noDMA noST noLDSrd", pt4_kernel<false, 11>, 2, 512, 0},
       {"q4", q4_kernel<0>, 2, 256, 1},
       {"q4 noDMA", q4_kernel<0, 1>, 2, 256, 1},
       {"q4 noBAR", q4_kernel<0, 2>, 2, 256, 1},
