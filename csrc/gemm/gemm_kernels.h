@@ -1157,8 +1157,14 @@ __global__ __launch_bounds__(512) void gemm_tn_t8_kernel(const GemmArgs p) {
 #pragma unroll
     for (int nq = 0; nq < 2; ++nq) {
       char* dst = crow + (n0 + wc * 64 + nq * 32 + fq * 8) * OSZ;
-      if (p.act == ACT_NONE) Store8<OUT>::st(dst, acc[i][nq * 2], acc[i][nq * 2 + 1]);
-      else Store8<OUT>::st(dst, act4(acc[i][nq * 2], p.act), act4(acc[i][nq * 2 + 1], p.act));
+      // one store site (two branch-local stores get merged by the optimizer, which drops the
+      // non-temporal hint)
+      f32x4 v0 = acc[i][nq * 2], v1 = acc[i][nq * 2 + 1];
+      if (p.act != ACT_NONE) {
+        v0 = act4(v0, p.act);
+        v1 = act4(v1, p.act);
+      }
+      Store8<OUT>::st(dst, v0, v1);
     }
   }
 }
@@ -1334,8 +1340,14 @@ __global__ __launch_bounds__(512) void gemm_tn_t4_kernel(const GemmArgs p) {
 #pragma unroll
     for (int nq = 0; nq < 2; ++nq) {
       char* dst = crow + (n0 + wc * 64 + nq * 32 + fq * 8) * OSZ;
-      if (p.act == ACT_NONE) Store8<OUT>::st(dst, acc[i][nq * 2], acc[i][nq * 2 + 1]);
-      else Store8<OUT>::st(dst, act4(acc[i][nq * 2], p.act), act4(acc[i][nq * 2 + 1], p.act));
+      // one store site (two branch-local stores get merged by the optimizer, which drops the
+      // non-temporal hint)
+      f32x4 v0 = acc[i][nq * 2], v1 = acc[i][nq * 2 + 1];
+      if (p.act != ACT_NONE) {
+        v0 = act4(v0, p.act);
+        v1 = act4(v1, p.act);
+      }
+      Store8<OUT>::st(dst, v0, v1);
     }
   }
 }
@@ -1481,8 +1493,14 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
       const int64_t row = m0 + wr * 128 + mq * 64 + f * 16 + frow;
       char* dst = (char*)p.c + map_row(row, p.c_grp, p.c_gstride) * p.ldc * OSZ +
                   (n0 + wc * 64 + nq * 32 + fq * 8) * OSZ;
-      if (p.act == ACT_NONE) Store8<OUT>::st(dst, acc[i][nq * 2], acc[i][nq * 2 + 1]);
-      else Store8<OUT>::st(dst, act4(acc[i][nq * 2], p.act), act4(acc[i][nq * 2 + 1], p.act));
+      // one store site (two branch-local stores get merged by the optimizer, which drops the
+      // non-temporal hint)
+      f32x4 v0 = acc[i][nq * 2], v1 = acc[i][nq * 2 + 1];
+      if (p.act != ACT_NONE) {
+        v0 = act4(v0, p.act);
+        v1 = act4(v1, p.act);
+      }
+      Store8<OUT>::st(dst, v0, v1);
       acc[i][nq * 2] = f32x4{0.f, 0.f, 0.f, 0.f};
       acc[i][nq * 2 + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
@@ -1716,8 +1734,14 @@ __global__ __launch_bounds__(512) void gemm_tn_pt8_kernel(const GemmArgs p) {
       const int64_t row = m0 + wr * 128 + mq * 64 + f * 16 + frow;
       char* dst = (char*)p.c + map_row(row, p.c_grp, p.c_gstride) * p.ldc * OSZ +
                   (n0 + wc * 64 + nq * 32 + fq * 8) * OSZ;
-      if (p.act == ACT_NONE) Store8<OUT>::st(dst, acc[i][nq * 2], acc[i][nq * 2 + 1]);
-      else Store8<OUT>::st(dst, act4(acc[i][nq * 2], p.act), act4(acc[i][nq * 2 + 1], p.act));
+      // one store site (two branch-local stores get merged by the optimizer, which drops the
+      // non-temporal hint)
+      f32x4 v0 = acc[i][nq * 2], v1 = acc[i][nq * 2 + 1];
+      if (p.act != ACT_NONE) {
+        v0 = act4(v0, p.act);
+        v1 = act4(v1, p.act);
+      }
+      Store8<OUT>::st(dst, v0, v1);
       acc[i][nq * 2] = f32x4{0.f, 0.f, 0.f, 0.f};
       acc[i][nq * 2 + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
     }

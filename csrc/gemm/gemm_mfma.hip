@@ -73,11 +73,11 @@ int choose_tile(int64_t M, int64_t N, int64_t K, int din) {
   const bool whole = M % 256 == 0 && N % 256 == 0 && tiles(256, 256) >= 192;
   if (whole && din == DT_FP8)
     return (tiles(256, 256) >= 512 && kbytes <= 2048 && N <= 2048) ? TILE_PT8 : TILE_T8;
-  // pt4 (t4 made persistent) leads t4 / t8 on narrow N; with the grouped tile raster, plain t4
-  // leads on wide N (profiles/r01/s2/s2_32_tune_grouped.txt: 16384x8192x1024 t4 243 vs pt4 252 /
-  // t8 255 us, 8192^3 727 vs 728 / 751, 4096^3 94.7 vs 94.6 / 96.8). pt4 falls back to t4 where it
-  // does not apply (shard tables, grouped A rows, flags, a single K-tile).
-  if (whole) return N >= 4096 ? TILE_T4 : TILE_PT4;
+  // pt4 (t4 made persistent) leads t4 / t8 on every shape measured once the C stores are
+  // non-temporal (profiles/r01/s2/s2_41_tune_nt.txt: flagship 108.9 vs t4 121.1 us, 16384x8192x1024
+  // 231.7 vs 251.9, 8192^3 695.7 vs 703.4, 4096^3 91.2 vs 93.8). It falls back to t4 where it does
+  // not apply (shard tables, grouped A rows, flags, a single K-tile).
+  if (whole) return TILE_PT4;
   if (M % 256 == 0 && N % 256 == 0 && tiles(256, 256) >= 256 && kbytes <= 2048) return TILE_R256;
   if (tiles(256, 256) >= 384) return TILE_I256;
   if (tiles(256, 128) >= 384) return TILE_256x128;

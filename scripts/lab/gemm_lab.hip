@@ -1468,7 +1468,13 @@ __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
       const f32x4 v0 = acc[i][nq * 2], v1 = acc[i][nq * 2 + 1];
       bf16x8 o = {(__bf16)v0.x, (__bf16)v0.y, (__bf16)v0.z, (__bf16)v0.w,
                   (__bf16)v1.x, (__bf16)v1.y, (__bf16)v1.z, (__bf16)v1.w};
-      if constexpr ((SKIP & 16) != 0) {  // non-temporal (streaming) store: C is never re-read
+      if constexpr ((SKIP & 32) != 0) {  // timing only: same bytes, one full 128 B line per 8 lanes
+        const int rl = lane >> 3, ch = lane & 7;
+        char* rrow = (char*)p.c + (m0 + wr * 128 + mq * 64 + f * 16 + nq * 8 + rl) * p.ldc * 2;
+        char* dst = rrow + (n0 + wc * 64 + ch * 8) * 2;
+        if constexpr ((SKIP & 16) != 0) __builtin_nontemporal_store(__builtin_bit_cast(i32x4, o), (i32x4*)dst);
+        else *(uint4*)dst = __builtin_bit_cast(uint4, o);
+      } else if constexpr ((SKIP & 16) != 0) {  // non-temporal (streaming) store: C is never re-read
         __builtin_nontemporal_store(__builtin_bit_cast(i32x4, o),
                                     (i32x4*)(crow + (n0 + wc * 64 + nq * 32 + fq * 8) * 2));
       } else {
@@ -1988,6 +1994,8 @@ int main(int argc, char** argv) {
       {"pt4 noDMA", pt4_kernel<false, 1>, 2, 512, 0},
       {"pt4 noMFMA", pt4_kernel<false, 4>, 2, 512, 0},
       {"pt4 nt", pt4_kernel<false, 16>, 2, 512, 0},
+      {"pt4 fullline", pt4_kernel<false, 32>, 2, 512, 0},
+      {"pt4 fullline nt", pt4_kernel<false, 48>, 2, 512, 0},
       {"pt4 noST", pt4_kernel<false, 2>, 2, 512, 0},
       {"pt4 noLDSrd", pt4_kernel<false, 8>, 2, 512, 0},
       {"pt4 noDMA noST", pt4_kernel<false, 3>, 2, 512, 0},
