@@ -65,18 +65,12 @@ int choose_tile(int64_t M, int64_t N, int64_t K, int din) {
   // (profiles/r01/s2/lab/t8_vs_ring2.txt) once the grid covers most of the CUs.
   auto tiles = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
   const int64_t kbytes = K * dtype_size(din);
-  // Among the ping-pong kernels (profiles/r01/s2/s2_21_tune_t4.txt, s2_22_fp8_tiles.txt):
-  //  * 16-bit / f32 inputs: t4 (2 phases per K-tile) is faster than t8 / pt8 on narrow N — the
-  //    flagship 65536x1024x1024 115.6 us vs t8 119.1 / pt8 118.4, 65536x1024x8192 747 vs 784;
-  //  * fp8 (plain or MX): the persistent pt8 wins with >= 2 short-K tiles per CU (flagship MX-fp8
-  //    72.6 us, ahead of hipBLASLt _scaled_mm 73.6), t8 otherwise.
+  // Among the ping-pong kernels, pt4 (t4 made persistent) leads t4 / t8 / pt8 on every shape and
+  // dtype measured once the C stores are non-temporal (profiles/r01/s2/s2_41_tune_nt.txt: bf16
+  // flagship 108.9 vs t4 121.1 us, 16384x8192x1024 231.7 vs 251.9, 8192^3 695.7 vs 703.4;
+  // s2_44_fp8_tiles.txt: MX-fp8 flagship 63.6 vs pt8 67.4 us, 8192^3 363 vs t8 380). It falls back
+  // to t4 where it does not apply (shard tables, grouped A rows, flags, a single K-tile).
   const bool whole = M % 256 == 0 && N % 256 == 0 && tiles(256, 256) >= 192;
-  if (whole && din == DT_FP8)
-    return (tiles(256, 256) >= 512 && kbytes <= 2048 && N <= 2048) ? TILE_PT8 : TILE_T8;
-  // pt4 (t4 made persistent) leads t4 / t8 on every shape measured once the C stores are
-  // non-temporal (profiles/r01/s2/s2_41_tune_nt.txt: flagship 108.9 vs t4 121.1 us, 16384x8192x1024
-  // 231.7 vs 251.9, 8192^3 695.7 vs 703.4, 4096^3 91.2 vs 93.8). It falls back to t4 where it does
-  // not apply (shard tables, grouped A rows, flags, a single K-tile).
   if (whole) return TILE_PT4;
   if (M % 256 == 0 && N % 256 == 0 && tiles(256, 256) >= 256 && kbytes <= 2048) return TILE_R256;
   if (tiles(256, 256) >= 384) return TILE_I256;

@@ -36,7 +36,7 @@ for m, n, k in [(65536, 1024, 1024), (8192, 8192, 8192)]:
     res = {"_scaled_mm": timeit(lambda: torch._scaled_mm(A, W.t(), scale_a=one, scale_b=one,
                                                          out_dtype=torch.bfloat16))}
     for mode in ("auto", "mx"):
-        for tile in ("auto", "t8", "pt8", "t4"):
+        for tile in ("auto", "t8", "pt8", "t4", "pt4"):
             res[f"{mode}/{tile}"] = timeit(lambda: gemm(A, W, C, mode=mode, tile=tile))
     tf = 2 * m * n * k / 1e12
     print(f"{m}x{n}x{k} fp8: " + "  ".join(f"{k_} {v:.1f}us({tf / v * 1e6:.0f}TF)"
