@@ -17,7 +17,7 @@ MI355X-first differences:
 from __future__ import annotations
 
 from abc import ABC, abstractmethod
-from typing import Any, Dict, Mapping, Optional, Tuple
+from typing import Any, Dict, Mapping, Tuple
 
 from ddlb_amd.communicator import Communicator
 from ddlb_amd.utils.options import OptionsManager

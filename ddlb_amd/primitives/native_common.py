@@ -73,7 +73,8 @@ COMMON_ALIASES = {
 
 TILE_CODE = {"auto": 0, "256x256": 1, "256x128": 2, "128x256": 3, "128x128": 4, "pp256": 5,
              "256x256w4": 6, "256x128w4": 7, "p256": 8, "p128": 9, "i256": 10,
-             "i128": 11, "i256w4": 12, "pi256": 13, "pi256w4": 14, "r256": 15, "t8": 16, "pt8": 17, "t4": 18, "pt4": 19}
+             "i128": 11, "i256w4": 12, "pi256": 13, "pi256w4": 14, "r256": 15, "t8": 16, "pt8": 17,
+             "t4": 18, "pt4": 19}
 MODE_CODE = {"auto": 0, "generic": 1, "mx": 2, "blas": 3}
 
 

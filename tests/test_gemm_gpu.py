@@ -35,7 +35,9 @@ def gen():
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
-@pytest.mark.parametrize("tile", ["256x256", "256x128", "128x256", "128x128", "pp256", "256x256w4", "256x128w4", "p256", "p128", "i256", "i128", "i256w4", "pi256", "pi256w4", "r256", "t8"])
+@pytest.mark.parametrize("tile", ["256x256", "256x128", "128x256", "128x128", "pp256", "256x256w4",
+                                  "256x128w4", "p256", "p128", "i256", "i128", "i256w4", "pi256",
+                                  "pi256w4", "r256", "t8"])
 def test_gemm_tiles(dtype, tile, gen):
     from ddlb_amd.ops.gemm import gemm
 
@@ -96,7 +98,8 @@ def test_gemm_fp8(mode, odt, gen):
     torch.testing.assert_close(out.float(), _ref(a, w), rtol=0, atol=_tol(torch.float8_e4m3fn, K))
 
 
-@pytest.mark.parametrize("tile", ["auto", "pp256", "128x128", "256x256w4", "256x128w4", "p256", "p128", "i256", "i128", "i256w4", "pi256", "r256", "t8", "pt8", "t4", "pt4"])
+@pytest.mark.parametrize("tile", ["auto", "pp256", "128x128", "256x256w4", "256x128w4", "p256", "p128",
+                                  "i256", "i128", "i256w4", "pi256", "r256", "t8", "pt8", "t4", "pt4"])
 def test_fp8_integer_exact(gen, tile):
     """Small integers are exact in e4m3: both fp8 paths must match bit for bit."""
     from ddlb_amd.ops.gemm import gemm
@@ -133,7 +136,8 @@ def test_grouped_rows(gen):
     assert torch.count_nonzero(C[untouched].float()) == 0
 
 
-@pytest.mark.parametrize("tile", ["auto", "pp256", "128x128", "256x256w4", "256x128w4", "p256", "p128", "i256", "i128", "i256w4", "pi256", "r256", "t8"])
+@pytest.mark.parametrize("tile", ["auto", "pp256", "128x128", "256x256w4", "256x128w4", "p256", "p128",
+                                  "i256", "i128", "i256w4", "pi256", "r256", "t8"])
 @pytest.mark.parametrize("shape", [(2048, 1024, 1024), (4096, 2048, 2048), (768, 512, 192)])
 def test_repeat_race_screen(gen, tile, shape):
     """Same inputs, 20 launches: identical bits every time (LDS-DMA/barrier race screen)."""

@@ -1,7 +1,6 @@
 """The simulator's checker must catch broken schedules (negative tests), not only pass good ones."""
 
 import pytest
-import torch
 
 from ddlb_amd.parallel.plan import DT_F32, SIG_STREAM, Plan
 from ddlb_amd.parallel.sim import Deadlock, RaceDetected, Simulator, make_buffers
