@@ -11,6 +11,7 @@
 #include <hip/hip_bf16.h>
 #include <hip/hip_fp16.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "kernels.h"
 
@@ -18,6 +19,7 @@ namespace ddlb {
 namespace {
 
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
 
@@ -98,6 +100,41 @@ __global__ __launch_bounds__(256) void reduce_sum_kernel(ReduceArgs a) {
   }
 }
 
+// Fixed source count: all NS 16-byte loads of a lane are issued before the first add, so NS
+// requests per lane are in flight at once (the runtime-count loop above waits on each load before
+// issuing the next). Matters when the sources are peers' buffers read over xGMI, where latency
+// is several microseconds. Loads and the store are non-temporal (streamed once). Summation order is src[0] + src[1] + ... as above (bitwise equal).
+template <int DT, int NS>
+__global__ __launch_bounds__(256) void reduce_sum_fixed_kernel(ReduceArgs a) {
+  using V = V8<DT>;
+  const int64_t nvec = a.count / V::N;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    u32x4 raw[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      raw[s] = __builtin_nontemporal_load((const u32x4*)((const char*)a.src[s] + v * 16));
+    float acc[V::N], t[V::N];
+    V::load(&raw[0], acc);
+#pragma unroll
+    for (int s = 1; s < NS; ++s) {
+      V::load(&raw[s], t);
+#pragma unroll
+      for (int i = 0; i < V::N; ++i) acc[i] += t[i];
+    }
+    u32x4 o;
+    V::store(&o, acc);
+    __builtin_nontemporal_store(o, (u32x4*)((char*)a.dst + v * 16));  // streamed, read by no one here
+  }
+  const int64_t tail0 = nvec * V::N;
+  for (int64_t i = tail0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.count;
+       i += stride) {
+    float acc = 0.f;
+    for (int s = 0; s < NS; ++s) acc += load1<DT>(a.src[s], i);
+    store1<DT>(a.dst, i, acc);
+  }
+}
+
 // Blocks are dealt round-robin to the segments (one segment = one peer = one xGMI link in the
 // IPC all-gathers), so every link carries traffic at once; the blocks of a segment grid-stride
 // over it with 4 x 16 B in flight per lane. (Walking the segments one after another would keep
@@ -166,6 +203,21 @@ hipError_t reduce_sum_launch(const ReduceArgs& a, int dtype, hipStream_t s) {
   if ((uintptr_t)a.dst & 15) return hipErrorInvalidValue;
   const int per = dtype == 0 ? 4 : 8;
   const int g = grid_for(a.count / per + 1);
+  static const bool generic = getenv("DDLB_REDUCE_GENERIC") != nullptr;  // A/B knob (benches)
+  if (!generic && a.nsrc >= 2 && a.nsrc <= 8 && dtype >= 0 && dtype <= 2) {
+#define DDLB_RS_CASE(NS)                                                                    \
+  case NS:                                                                                  \
+    if (dtype == 0) hipLaunchKernelGGL((reduce_sum_fixed_kernel<0, NS>), dim3(g), dim3(256), 0, s, a); \
+    else if (dtype == 1) hipLaunchKernelGGL((reduce_sum_fixed_kernel<1, NS>), dim3(g), dim3(256), 0, s, a); \
+    else hipLaunchKernelGGL((reduce_sum_fixed_kernel<2, NS>), dim3(g), dim3(256), 0, s, a); \
+    break;
+    switch (a.nsrc) {
+      DDLB_RS_CASE(2) DDLB_RS_CASE(3) DDLB_RS_CASE(4) DDLB_RS_CASE(5)
+      DDLB_RS_CASE(6) DDLB_RS_CASE(7) DDLB_RS_CASE(8)
+    }
+#undef DDLB_RS_CASE
+    return hipGetLastError();
+  }
   switch (dtype) {
     case 0: hipLaunchKernelGGL(reduce_sum_kernel<0>, dim3(g), dim3(256), 0, s, a); break;
     case 1: hipLaunchKernelGGL(reduce_sum_kernel<1>, dim3(g), dim3(256), 0, s, a); break;
