@@ -139,6 +139,17 @@ __global__ __launch_bounds__(256) void reduce_sum_fixed_kernel(ReduceArgs a) {
 // IPC all-gathers), so every link carries traffic at once; the blocks of a segment grid-stride
 // over it with 4 x 16 B in flight per lane. (Walking the segments one after another would keep
 // a single link busy at a time: d-1 times the transfer time of a full-mesh exchange.)
+template <bool NT>  // NT: non-temporal source loads (each source byte is read exactly once)
+__device__ __forceinline__ uint4 copy_ld(const char* p) {
+  if constexpr (NT) {
+    const u32x4 v = __builtin_nontemporal_load((const u32x4*)p);
+    return uint4{v.x, v.y, v.z, v.w};
+  } else {
+    return *(const uint4*)p;
+  }
+}
+
+template <bool NT>
 __global__ __launch_bounds__(256) void copy_kernel(CopyArgs a) {
   const int nseg = a.nseg;
   const int seg = (int)blockIdx.x % nseg;
@@ -151,16 +162,16 @@ __global__ __launch_bounds__(256) void copy_kernel(CopyArgs a) {
   const int64_t nvec = bytes / 16;
   int64_t v = t0;
   for (; v + 3 * stride < nvec; v += 4 * stride) {
-    const uint4 x0 = *(const uint4*)(src + v * 16);
-    const uint4 x1 = *(const uint4*)(src + (v + stride) * 16);
-    const uint4 x2 = *(const uint4*)(src + (v + 2 * stride) * 16);
-    const uint4 x3 = *(const uint4*)(src + (v + 3 * stride) * 16);
+    const uint4 x0 = copy_ld<NT>(src + v * 16);
+    const uint4 x1 = copy_ld<NT>(src + (v + stride) * 16);
+    const uint4 x2 = copy_ld<NT>(src + (v + 2 * stride) * 16);
+    const uint4 x3 = copy_ld<NT>(src + (v + 3 * stride) * 16);
     *(uint4*)(dst + v * 16) = x0;
     *(uint4*)(dst + (v + stride) * 16) = x1;
     *(uint4*)(dst + (v + 2 * stride) * 16) = x2;
     *(uint4*)(dst + (v + 3 * stride) * 16) = x3;
   }
-  for (; v < nvec; v += stride) *(uint4*)(dst + v * 16) = *(const uint4*)(src + v * 16);
+  for (; v < nvec; v += stride) *(uint4*)(dst + v * 16) = copy_ld<NT>(src + v * 16);
   for (int64_t b = nvec * 16 + t0; b < bytes; b += stride) dst[b] = src[b];
 }
 
@@ -238,7 +249,9 @@ hipError_t copy_launch(const CopyArgs& a, int max_blocks, hipStream_t s) {
   if (max_blocks > 0 && g > max_blocks) g = max_blocks;
   // at least one block per segment, and a whole number of blocks per segment
   g = g < a.nseg ? a.nseg : (g / a.nseg) * a.nseg;
-  hipLaunchKernelGGL(copy_kernel, dim3(g), dim3(256), 0, s, a);
+  static const bool plain = getenv("DDLB_COPY_PLAIN") != nullptr;  // A/B knob (benches)
+  if (plain) hipLaunchKernelGGL(copy_kernel<false>, dim3(g), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(copy_kernel<true>, dim3(g), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
