@@ -249,9 +249,11 @@ hipError_t copy_launch(const CopyArgs& a, int max_blocks, hipStream_t s) {
   if (max_blocks > 0 && g > max_blocks) g = max_blocks;
   // at least one block per segment, and a whole number of blocks per segment
   g = g < a.nseg ? a.nseg : (g / a.nseg) * a.nseg;
-  static const bool plain = getenv("DDLB_COPY_PLAIN") != nullptr;  // A/B knob (benches)
-  if (plain) hipLaunchKernelGGL(copy_kernel<false>, dim3(g), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(copy_kernel<true>, dim3(g), dim3(256), 0, s, a);
+  // Plain loads by default: non-temporal source loads measured slower on HBM (7 x 16 MiB:
+  // 52 vs 34 us at 128 blocks, 36 vs 35 at 512; profiles/r01/s3/copy_ab_nt.txt). A/B knob kept.
+  static const bool nt = getenv("DDLB_COPY_NT") != nullptr;
+  if (nt) hipLaunchKernelGGL(copy_kernel<true>, dim3(g), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(copy_kernel<false>, dim3(g), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

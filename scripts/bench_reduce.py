@@ -3,7 +3,7 @@
     python scripts/bench_reduce.py                          # fixed-count unrolled kernels
     DDLB_REDUCE_GENERIC=1 python scripts/bench_reduce.py    # runtime-count kernel (A/B)
     python scripts/bench_reduce.py --copy                   # CU copy kernel, 7 segments
-    DDLB_COPY_PLAIN=1 python scripts/bench_reduce.py --copy # without non-temporal loads (A/B)
+    DDLB_COPY_NT=1 python scripts/bench_reduce.py --copy    # with non-temporal loads (A/B)
 
 Prints one line per source count: time and effective bandwidth (nsrc reads + 1 write).
 """
@@ -19,7 +19,7 @@ from ddlb_amd.ops import load  # noqa: E402
 
 def bench_copy(C) -> None:
     """The IPC all-gather's CU copy: 7 segments (one per peer at d=8) of 16 MiB each."""
-    kind = "plain" if os.environ.get("DDLB_COPY_PLAIN") else "nt-load"
+    kind = "nt-load" if os.environ.get("DDLB_COPY_NT") else "plain"
     s = torch.cuda.current_stream().cuda_stream
     seg = 16 << 20
     src = torch.empty(7 * seg, device="cuda", dtype=torch.uint8).random_()
