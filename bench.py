@@ -137,6 +137,16 @@ def prewarm_runs(impl, comm, prewarm_ms: float, calib: int = 4) -> int:
     return int(want.item())
 
 
+def _check(impl, out, res) -> bool:
+    """Validate one output; a mismatch is recorded in ``res`` (not raised)."""
+    try:
+        impl.validate(out)
+        return True
+    except AssertionError as e:
+        res["validation"] = str(e).splitlines()[0][:200]
+        return False
+
+
 def child_main(a) -> int:
     """One measurement on this rank's GPU; writes a JSON result file (rank 0 aggregates)."""
     import torch
@@ -154,12 +164,7 @@ def child_main(a) -> int:
         if a.validate:
             out = impl.run()
             comm.synchronize()
-            try:
-                impl.validate(out)
-                valid = True
-            except AssertionError as e:
-                valid = False
-                res["validation"] = str(e).splitlines()[0][:200]
+            valid = _check(impl, out, res)
         # untimed pre-warm: keep the GPU busy for ~prewarm_ms so the timed window does not
         # include the clock ramp out of idle (measured: 10 warmups of this step leave the
         # first 50 timed steps ~14 % slow). Then the W warmup steps of the contract.
@@ -174,12 +179,19 @@ def child_main(a) -> int:
         comm.barrier()
         t0 = time.perf_counter()
         for _ in range(a.steps):
-            impl.run()
+            out = impl.run()
         comm.synchronize()
         t1 = time.perf_counter()
         comm.barrier()
         t = torch.tensor([(t1 - t0) * 1e3 / a.steps], dtype=torch.float64, device=comm.device)
         comm.all_reduce_max(t)
+        # after the timed loop: no device-side spin may have given up (a peer that never
+        # signalled leaves stale data behind a "successful" step), and the output of the LAST
+        # timed step must validate too (cross-rank ordering bugs show up under back-to-back
+        # epochs, not on the first, isolated run)
+        impl.check_health()
+        if a.validate and valid:
+            valid = _check(impl, out, res)
         res.update(ok=True, ms=float(t.item()), valid=valid)
         impl.close()
         comm.destroy()
@@ -269,9 +281,93 @@ class Job:
         if all(r.get("ok") for r in results):
             ms = max(r["ms"] for r in results)
             valid = all(r.get("valid") is not False for r in results)
-            return {"ok": True, "ms": ms, "valid": valid if validate else None}
+            why = [r["validation"] for r in results if r.get("validation")]
+            return {"ok": True, "ms": ms, "valid": valid if validate else None,
+                    "validation": why[0] if why else ""}
         errs = [r.get("error") for r in results if not r.get("ok")]
         return {"ok": False, "error": errs[0] if errs else "unknown"}
+
+
+def autotune(job, pool, a, world: int, tune: dict):
+    """Time every candidate (validated) in its own children; returns (winner, fallbacks) or
+    None when every candidate failed. ``tune`` collects per-candidate results for the report."""
+    t_tune = time.time()
+    rounds = a.tune_rounds if a.tune_rounds > 0 else (2 if world == 1 else 1)
+    tune_steps = a.tune_steps if a.tune_steps > 0 else (50 if world == 1 else 20)
+    best_ms = {}
+    # several rounds over the pool in the same order, best time per candidate: a candidate
+    # measured first after an idle gap otherwise pays the clock ramp the others do not
+    for label, impl, opts in pool * rounds:
+        # wall-clock cap on the search (the decision is broadcast from rank 0, so every
+        # rank stops at the same candidate): the best candidate so far runs the final
+        native_ok = any(lb in best_ms for lb, i, _ in pool if i == "native")
+        spent = time.time() - t_tune
+        over = (native_ok and spent > a.tune_budget_s) or (best_ms and spent > a.tune_cap_s)
+        if job.bcast(over if job.rank == 0 else None):
+            tune.setdefault(label, "skipped (tuning budget)")
+            continue
+        t0 = time.time()
+        # tuning runs validate too (first run and last timed step): a fast candidate that
+        # computes the wrong numbers must never win the search
+        r = job.measure(impl, opts, tune_steps, 3, a.validate, a.candidate_timeout,
+                        prewarm_ms=min(a.prewarm_ms, 100.0))
+        if r["ok"] and r.get("valid") is False:
+            r = {"ok": False, "error": f"invalid result: {r.get('validation', '')}"}
+        if r["ok"]:
+            best_ms[label] = min(r["ms"], best_ms.get(label, float("inf")))
+            tune[label] = round(best_ms[label], 4)
+        elif label not in best_ms:
+            tune[label] = r["error"][:160]
+        job.log(f"tune {label}: {round(r['ms'], 4) if r['ok'] else r['error'][:160]} "
+                f"({time.time() - t0:.1f} s)")
+    ranked = [(best_ms[label], (label, impl, opts)) for label, impl, opts in pool
+              if impl == "native" and label in best_ms]
+    if not ranked:
+        # every native path failed on this machine: report the vendor-library slot (our
+        # pytorch implementation, RCCL + hipBLASLt) rather than no number; the result line
+        # names the implementation
+        ranked = [(best_ms[label], (label, impl, opts)) for label, impl, opts in pool
+                  if label in best_ms]
+        tune["native_failed"] = True
+    if not ranked:
+        return None
+    ranked.sort(key=lambda x: x[0])
+    chosen = ranked[0][1]
+    fallbacks = [c for _, c in ranked[1:4]]
+    # last resort: the vendor-library slot, so a job whose native paths all break in the
+    # final run still reports a measured (and labelled) number
+    vendor = sorted(((best_ms[lbl], (lbl, i, o)) for lbl, i, o in pool
+                     if i != "native" and lbl in best_ms), key=lambda x: x[0])
+    if vendor and vendor[0][1] not in fallbacks and vendor[0][1] is not chosen:
+        fallbacks.append(vendor[0][1])
+    return chosen, fallbacks
+
+
+def final_measure(job, chosen, fallbacks, a, tune: dict):
+    """The timed measurement of the contract. Should the winner fail or not validate there (a
+    flaky transport, a cross-rank ordering bug under back-to-back epochs), the next fastest
+    candidates are tried before giving up, so one bad path cannot sink the job. Returns
+    (candidate, result); result is None if nothing ran, or has valid=False if nothing
+    validated (then the first completed run is reported, with a nonzero exit code)."""
+    final, invalid = None, None
+    first = chosen
+    for cand in [chosen] + list(fallbacks):
+        t0 = time.time()
+        r = job.measure(cand[1], cand[2], a.steps, a.warmup, a.validate,
+                        a.candidate_timeout + a.steps * 0.05, prewarm_ms=a.prewarm_ms)
+        job.log(f"final {cand[0]}: {r.get('ms', r.get('error'))} valid={r.get('valid')} "
+                f"({time.time() - t0:.1f} s)")
+        if r["ok"] and r.get("valid") is not False:
+            if cand is not first:
+                tune["final_fallback_from"] = first[0]
+            return cand, r
+        if r["ok"] and invalid is None:
+            invalid = (cand, r)
+        tune.setdefault("final_rejected", []).append(
+            f"{cand[0]}: {r.get('error') or 'invalid ' + r.get('validation', '')}"[:200])
+    if invalid is not None:
+        return invalid
+    return chosen, final
 
 
 def main(argv=None) -> int:
@@ -337,64 +433,14 @@ def main(argv=None) -> int:
                              f"{[c[0] for c in every]}")
         chosen = match[0]
     else:
-        ranked = []
-        t_tune = time.time()
-        rounds = a.tune_rounds if a.tune_rounds > 0 else (2 if world == 1 else 1)
-        tune_steps = a.tune_steps if a.tune_steps > 0 else (50 if world == 1 else 20)
-        best_ms = {}
-        # several rounds over the pool in the same order, best time per candidate: a candidate
-        # measured first after an idle gap otherwise pays the clock ramp the others do not
-        for label, impl, opts in pool * rounds:
-            # wall-clock cap on the search (the decision is broadcast from rank 0, so every
-            # rank stops at the same candidate): the best candidate so far runs the final
-            native_ok = any(l in best_ms for l, i, _ in pool if i == "native")
-            spent = time.time() - t_tune
-            over = (native_ok and spent > a.tune_budget_s) or (best_ms and spent > a.tune_cap_s)
-            if job.bcast(over if job.rank == 0 else None):
-                tune.setdefault(label, "skipped (tuning budget)")
-                continue
-            t0 = time.time()
-            r = job.measure(impl, opts, tune_steps, 3, False, a.candidate_timeout,
-                            prewarm_ms=min(a.prewarm_ms, 100.0))
-            if r["ok"]:
-                best_ms[label] = min(r["ms"], best_ms.get(label, float("inf")))
-                tune[label] = round(best_ms[label], 4)
-            elif label not in best_ms:
-                tune[label] = r["error"][:160]
-            job.log(f"tune {label}: {round(r['ms'], 4) if r['ok'] else r['error'][:160]} "
-                    f"({time.time() - t0:.1f} s)")
-        ranked = [(best_ms[label], (label, impl, opts)) for label, impl, opts in pool
-                  if impl == "native" and label in best_ms]
-        if not ranked:
-            # every native path failed on this machine: report the vendor-library slot (our
-            # pytorch implementation, RCCL + hipBLASLt) rather than no number; the result line
-            # names the implementation
-            ranked = [(best_ms[label], (label, impl, opts)) for label, impl, opts in pool
-                      if label in best_ms]
-            tune["native_failed"] = True
-        if not ranked:
+        picked = autotune(job, pool, a, world, tune)
+        if picked is None:
             sys.stderr.write(f"every candidate failed: {json.dumps(tune)}\n")
             return 1
-        ranked.sort(key=lambda x: x[0])
-        chosen = ranked[0][1]
-        fallbacks = [c for _, c in ranked[1:3]]
-    # The winner runs the timed measurement; should it fail there (a flaky transport), the next
-    # fastest candidates are tried before giving up, so one bad path cannot sink the job.
-    final = None
-    for cand in [chosen] + (fallbacks if a.algorithm == "auto" else []):
-        t0 = time.time()
-        final = job.measure(cand[1], cand[2], a.steps, a.warmup, a.validate,
-                            a.candidate_timeout + a.steps * 0.05, prewarm_ms=a.prewarm_ms)
-        job.log(f"final {cand[0]}: {final.get('ms', final.get('error'))} "
-                f"({time.time() - t0:.1f} s)")
-        if final["ok"]:
-            if cand is not chosen:
-                tune["final_fallback_from"] = chosen[0]
-            chosen = cand
-            break
-    if not final["ok"]:
-        sys.stderr.write(f"final measurement failed: {final['error']} "
-                         f"(autotune: {json.dumps(tune)})\n")
+        chosen, fallbacks = picked
+    chosen, final = final_measure(job, chosen, fallbacks, a, tune)
+    if final is None:
+        sys.stderr.write(f"final measurement failed (autotune: {json.dumps(tune)})\n")
         return 1
     ms = final["ms"]
     flop = 2.0 * a.m * a.n * a.k

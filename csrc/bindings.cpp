@@ -153,7 +153,9 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("nranks", &RcclComm::nranks);
 
   py::class_<SymmetricBuffer, std::shared_ptr<SymmetricBuffer>>(m, "SymmetricBuffer")
-      .def(py::init<size_t, int>())
+      .def(py::init<size_t, int, bool>(), py::arg("bytes"), py::arg("device"),
+           py::arg("uncached") = false)
+      .def_property_readonly("uncached", &SymmetricBuffer::uncached)
       .def("ipc_handle", [](const SymmetricBuffer& b) { return py::bytes(b.ipc_handle()); })
       .def("open_peers",
            [](SymmetricBuffer& b, std::vector<py::bytes> hs, int my_rank) {
@@ -172,6 +174,7 @@ PYBIND11_MODULE(_C, m) {
   py::class_<PlanExecutor, std::shared_ptr<PlanExecutor>>(m, "PlanExecutor")
       .def(py::init<int, int, int, const std::vector<int>&>())
       .def("load", &PlanExecutor::load)
+      .def("prepare", &PlanExecutor::prepare)
       .def("set_comm", [](PlanExecutor& p, std::shared_ptr<RcclComm> c) { p.set_comm(c.get()); },
            py::keep_alive<1, 2>())
       .def("run", &PlanExecutor::run)

@@ -57,9 +57,13 @@ ncclDataType_t nccl_dtype(int dt) {
   }
 }
 
-SymmetricBuffer::SymmetricBuffer(size_t bytes, int device) : bytes_(bytes), device_(device) {
+SymmetricBuffer::SymmetricBuffer(size_t bytes, int device, bool uncached)
+    : bytes_(bytes), device_(device), uncached_(uncached) {
   DDLB_HIP(hipSetDevice(device));
-  DDLB_HIP(hipMalloc(&ptr_, bytes ? bytes : 256));
+  if (uncached)
+    DDLB_HIP(hipExtMallocWithFlags(&ptr_, bytes ? bytes : 256, hipDeviceMallocUncached));
+  else
+    DDLB_HIP(hipMalloc(&ptr_, bytes ? bytes : 256));
   DDLB_HIP(hipMemset(ptr_, 0, bytes ? bytes : 256));
   DDLB_HIP(hipDeviceSynchronize());
 }

@@ -50,7 +50,11 @@ ncclDataType_t nccl_dtype(int dt);  // DT_* -> ncclDataType_t
 // same-named buffer on every peer (index = rank; own rank -> local pointer).
 class SymmetricBuffer {
  public:
-  SymmetricBuffer(size_t bytes, int device);
+  // uncached: fine-grained, never cached in any GPU's L2 (hipDeviceMallocUncached). Used for the
+  // cross-process flag words: peers write them over xGMI while this GPU's command processor or a
+  // kernel polls them, so no stale L2 line may ever shadow the HBM copy.
+  SymmetricBuffer(size_t bytes, int device, bool uncached = false);
+  bool uncached() const { return uncached_; }
   ~SymmetricBuffer();
   std::string ipc_handle() const;                       // 64 raw bytes
   void open_peers(const std::vector<std::string>& handles, int my_rank);
@@ -67,6 +71,7 @@ class SymmetricBuffer {
   void* ptr_ = nullptr;
   size_t bytes_ = 0;
   int device_ = 0;
+  bool uncached_ = false;
   std::vector<void*> peers_;
   std::vector<bool> opened_;
 };

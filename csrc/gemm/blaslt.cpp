@@ -52,16 +52,35 @@ bool tune_enabled() {
   const char* v = std::getenv("DDLB_BLAS_TUNE");
   return v == nullptr || std::strcmp(v, "0") != 0;
 }
+// One handle per device; one workspace per (device, stream): two hipBLASLt GEMMs enqueued on
+// different streams may run concurrently, so they must never share scratch memory.
 struct LtDevice {
   hipblasLtHandle_t handle = nullptr;
-  void* workspace = nullptr;
-  size_t ws_bytes = 0;
+  size_t ws_bytes = 0;  // the same cap for every stream's workspace
+  std::unordered_map<hipStream_t, void*> workspace;
 };
 
 constexpr size_t kWorkspace = 64ull << 20;
 std::mutex g_mu;
 std::unordered_map<int, LtDevice> g_dev;
 std::unordered_map<LtKey, LtPlan, LtKeyHash> g_plans;
+
+// Workspace of stream ``s`` (allocated on first use; nullptr + 0 bytes if that fails, which
+// restricts the plan to workspace-free algorithms).
+void* workspace_for(LtDevice* d, hipStream_t s, size_t* bytes) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = d->workspace.find(s);
+  if (it == d->workspace.end()) {
+    void* w = nullptr;
+    if (d->ws_bytes && hipMalloc(&w, d->ws_bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      w = nullptr;
+    }
+    it = d->workspace.emplace(s, w).first;
+  }
+  *bytes = it->second ? d->ws_bytes : 0;
+  return it->second;
+}
 
 bool lt_type(int dt, hipDataType* t) {
   switch (dt) {
@@ -79,13 +98,7 @@ LtDevice* device_state(int dev) {
       d.handle = nullptr;
       return nullptr;
     }
-    if (hipMalloc(&d.workspace, kWorkspace) != hipSuccess) {
-      (void)hipGetLastError();
-      d.workspace = nullptr;
-      d.ws_bytes = 0;
-    } else {
-      d.ws_bytes = kWorkspace;
-    }
+    d.ws_bytes = kWorkspace;
   }
   return &d;
 }
@@ -135,12 +148,15 @@ bool build_plan(LtDevice* d, const LtKey& key, LtPlan* pl) {
   return true;
 }
 
-// Time the heuristic's top candidates on the caller's stream with the real operands and keep
-// the fastest (the top-1 heuristic is not always the fastest kernel for tall-skinny shapes).
-// Runs once per shape, outside graph capture; C is overwritten by the real call that follows.
+// Time the heuristic's top candidates on stream ``s`` with the real operands and keep the
+// fastest (the top-1 heuristic is not always the fastest kernel for tall-skinny shapes). Runs
+// once per shape, outside graph capture, with a host wait on an event: plans call it at bind
+// time (PlanExecutor::prepare), never while enqueueing a run. C is overwritten.
 void autotune(LtDevice* d, LtPlan* pl, const GemmArgs& p, hipStream_t s) {
   pl->tuned = true;
   if (pl->ncand < 2 || !tune_enabled()) return;
+  size_t wsb = 0;
+  void* ws = workspace_for(d, s, &wsb);
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return;
   hipEvent_t e0, e1;
@@ -150,9 +166,10 @@ void autotune(LtDevice* d, LtPlan* pl, const GemmArgs& p, hipStream_t s) {
   float best = 1e30f;
   int best_i = 0;
   for (int i = 0; i < pl->ncand; ++i) {
+    if (pl->cands[i].workspaceSize > wsb) continue;
     auto run = [&]() {
       return hipblasLtMatmul(d->handle, pl->op, &alpha, p.b, pl->la, p.a, pl->lb, &beta, p.c,
-                             pl->lc, p.c, pl->lc, &pl->cands[i].algo, d->workspace,
+                             pl->lc, p.c, pl->lc, &pl->cands[i].algo, ws,
                              pl->cands[i].workspaceSize, s);
     };
     bool ok = true;
@@ -191,10 +208,13 @@ bool blaslt_supports(const GemmArgs& p, int din, int dout) {
   return true;
 }
 
-hipError_t blaslt_gemm(const GemmArgs& p, int din, int dout, hipStream_t s) {
-  if (!blaslt_supports(p, din, dout)) return hipErrorNotSupported;
+namespace {
+// The cached (and, on first use with ``tune``, autotuned) plan of p's shape; nullptr if
+// hipBLASLt cannot run it.
+LtPlan* plan_for(const GemmArgs& p, int din, int dout, hipStream_t s, bool tune, LtDevice** dev_out) {
+  if (!blaslt_supports(p, din, dout)) return nullptr;
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return hipErrorNotSupported;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   const int64_t grp = p.a_grp > 0 ? p.a_grp : p.M;
   LtKey key;
   std::memset(&key, 0, sizeof(key));
@@ -209,7 +229,7 @@ hipError_t blaslt_gemm(const GemmArgs& p, int din, int dout, hipStream_t s) {
   {
     std::lock_guard<std::mutex> lk(g_mu);
     d = device_state(dev);
-    if (d == nullptr) return hipErrorNotSupported;
+    if (d == nullptr) return nullptr;
     auto it = g_plans.find(key);
     if (it == g_plans.end()) {
       LtPlan fresh;
@@ -218,12 +238,33 @@ hipError_t blaslt_gemm(const GemmArgs& p, int din, int dout, hipStream_t s) {
     }
     pl = &it->second;
   }
-  if (!pl->ok) return hipErrorNotSupported;
-  if (!pl->tuned) autotune(d, pl, p, s);
+  if (!pl->ok) return nullptr;
+  if (tune && !pl->tuned) autotune(d, pl, p, s);
+  *dev_out = d;
+  return pl;
+}
+}  // namespace
+
+hipError_t blaslt_prepare(const GemmArgs& p, int din, int dout, hipStream_t s) {
+  LtDevice* d = nullptr;
+  if (plan_for(p, din, dout, s, true, &d) == nullptr) return hipErrorNotSupported;
+  size_t wsb = 0;
+  (void)workspace_for(d, s, &wsb);  // allocated now, not inside a later graph capture
+  return hipSuccess;
+}
+
+hipError_t blaslt_gemm(const GemmArgs& p, int din, int dout, hipStream_t s) {
+  // direct callers (ops.gemm) tune on first use; plans were tuned at bind time (prepare)
+  LtDevice* d = nullptr;
+  LtPlan* pl = plan_for(p, din, dout, s, true, &d);
+  if (pl == nullptr) return hipErrorNotSupported;
+  size_t wsb = 0;
+  void* ws = workspace_for(d, s, &wsb);
+  if (pl->ws > wsb) return hipErrorNotSupported;
   const float alpha = 1.f, beta = 0.f;
   const hipblasStatus_t st =
       hipblasLtMatmul(d->handle, pl->op, &alpha, p.b, pl->la, p.a, pl->lb, &beta, p.c, pl->lc,
-                      p.c, pl->lc, &pl->algo, d->workspace, pl->ws, s);
+                      p.c, pl->lc, &pl->algo, ws, pl->ws, s);
   return st == HIPBLAS_STATUS_SUCCESS ? hipSuccess : hipErrorLaunchFailure;
 }
 

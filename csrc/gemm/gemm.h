@@ -63,5 +63,8 @@ int tile_cols(int tile);
 // hipBLASLt backend (csrc/gemm/blaslt.cpp): plain bf16, f16, f32 GEMMs (algorithm autotuned).
 bool blaslt_supports(const GemmArgs& p, int din, int dout);
 hipError_t blaslt_gemm(const GemmArgs& p, int din, int dout, hipStream_t s);
+// Build (and autotune, with a host wait) the plan of p's shape ahead of time, e.g. when a
+// native plan is bound, so no tuning happens while a run is being enqueued.
+hipError_t blaslt_prepare(const GemmArgs& p, int din, int dout, hipStream_t s);
 
 }  // namespace ddlb

@@ -195,23 +195,36 @@ template <> struct Store4<DT_F32> {
 template <int OUT> constexpr int out_size() { return OUT == DT_F32 ? 4 : 2; }
 
 // ---------------------------------------------------------------- bounded arrival spin
-__device__ __forceinline__ void wait_flag(const GemmArgs& p, int64_t row) {
+// A tile reads the physical A rows map_row(m0) .. map_row(last row of the tile), which can span
+// several shards when the shard height (flag_rows) is not a multiple of the tile height (e.g.
+// m/d = 320 rows with 128- or 256-row tiles): wait for EVERY shard in that range, not only the
+// first row's. The acquire is at system scope: the rows were written by a copy engine or by a
+// peer GPU over xGMI, not by this agent.
+__device__ __forceinline__ void wait_flag(const GemmArgs& p, int64_t row_first, int64_t row_last) {
   if (p.flags == nullptr) return;
-  const int shard = (int)(row / p.flag_rows);
-  unsigned* f = const_cast<unsigned*>(p.flags) + shard;
   if (threadIdx.x == 0) {
-    unsigned spins = 0;
-    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) <
-           p.epoch) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1u << 26)) {  // ~seconds: give up, report, let the grid drain
-        if (p.timeout_word) atomicOr(p.timeout_word, 1u);
-        break;
+    const int s0 = (int)(row_first / p.flag_rows), s1 = (int)(row_last / p.flag_rows);
+    for (int sh = s0; sh <= s1; ++sh) {
+      unsigned* f = const_cast<unsigned*>(p.flags) + sh;
+      unsigned spins = 0;
+      while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < p.epoch) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1u << 26)) {  // ~seconds: give up, report, let the grid drain
+          if (p.timeout_word) atomicOr(p.timeout_word, 1u);
+          break;
+        }
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
   }
   __syncthreads();
+}
+
+// Arrival wait for the tile whose first logical row is m0 and which has (up to) BM rows.
+__device__ __forceinline__ void wait_tile(const GemmArgs& p, int64_t m0, int BM) {
+  if (p.flags == nullptr) return;
+  const int64_t last = (m0 + BM < p.M ? m0 + BM : p.M) - 1;
+  wait_flag(p, map_row(m0, p.a_grp, p.a_gstride), map_row(last, p.a_grp, p.a_gstride));
 }
 
 // ---------------------------------------------------------------- the tiled kernel
@@ -253,7 +266,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_kernel(const GemmArgs p) 
     bptr[i] = (const char*)p.b + gr * p.ldb * esz + chunk * 16;
   }
 
-  wait_flag(p, map_row(m0, p.a_grp, p.a_gstride));
+  wait_tile(p, m0, BM);
 
   auto stage = [&](int buf, int kt) __attribute__((always_inline)) {
     char* base = smem + buf * STAGE;
@@ -849,7 +862,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pp256_kernel(const GemmArgs p) {
     gc = gc < p.N ? gc : p.N - 1;
     bptr[i] = (const char*)p.b + gc * p.ldb * esz + chunk * 16;
   }
-  wait_flag(p, map_row(m0, p.a_grp, p.a_gstride));
+  wait_tile(p, m0, BM);
 
   // part 0: A rows 0-15 + B rows 0-15 of this wave's 32; part 1: the other 16 of each
   auto stage_part = [&](int buf, int kt, int part) __attribute__((always_inline)) {
@@ -1026,7 +1039,7 @@ __global__ __launch_bounds__(512) void gemm_tn_t8_kernel(const GemmArgs p) {
       sB[q][i] = (const char*)p.b + (n0 + lc) * p.ldb * esz + ch;
     }
   }
-  wait_flag(p, m0);
+  wait_tile(p, m0, 256);
   auto stage = [&](const char* const* src, int unit_off, int kt, int buf) __attribute__((always_inline)) {
     kt = kt < nk ? kt : nk - 1;
     char* dst = smem + buf * STAGE + unit_off + wave * 16 * ROWB;
@@ -1216,7 +1229,7 @@ __global__ __launch_bounds__(512) void gemm_tn_t4_kernel(const GemmArgs p) {
       sB[q][i] = (const char*)p.b + (n0 + lc) * p.ldb * esz + ch;
     }
   }
-  wait_flag(p, m0);
+  wait_tile(p, m0, 256);
   auto stage = [&](const char* const* src, int unit_off, int kt, int buf)
                    __attribute__((always_inline)) {
     kt = kt < nk ? kt : nk - 1;
@@ -1849,7 +1862,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_mxfp8_kernel(const GemmAr
     const int chunk = (lane & 7) ^ ((row >> 1) & 7);
     bptr[i] = (const char*)p.b + gr * p.ldb + chunk * 16;
   }
-  wait_flag(p, map_row(m0, p.a_grp, p.a_gstride));
+  wait_tile(p, m0, BM);
   auto stage = [&](int buf, int kt) __attribute__((always_inline)) {
     char* base = smem + buf * STAGE;
     const int64_t koff = (int64_t)kt * ROWB;

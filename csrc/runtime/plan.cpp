@@ -85,8 +85,10 @@ void PlanExecutor::enable_graph(bool on) {
     throw std::runtime_error("plan has epoch-dependent ops (signals / arrival flags): "
                              "it cannot be replayed from a hipGraph");
   graph_on_ = on;
-  if (on && cap_stream_ == nullptr)
+  if (on && cap_stream_ == nullptr) {
     DDLB_HIP(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking));
+    prepare((uintptr_t)cap_stream_);  // hipBLASLt workspaces exist before the capture
+  }
 }
 
 unsigned PlanExecutor::read_timeout() {
@@ -137,29 +139,50 @@ unsigned PlanExecutor::run(uintptr_t main_stream) {
   return epoch_;
 }
 
+GemmArgs PlanExecutor::gemm_args(const int64_t* o) const {
+  GemmArgs g;
+  g.a = (const void*)o[2];
+  g.b = (const void*)o[3];
+  g.c = (void*)o[4];
+  g.lda = o[5]; g.ldb = o[6]; g.ldc = o[7];
+  g.a_grp = o[8]; g.a_gstride = o[9];
+  g.c_grp = o[10]; g.c_gstride = o[11];
+  g.M = (int)o[12]; g.N = (int)o[13]; g.K = (int)o[14];
+  g.flags = (const unsigned*)o[19];
+  g.epoch = epoch_;
+  g.flag_rows = o[20] > 0 ? o[20] : 1;
+  g.nshards = o[21] > 0 ? (int)o[21] : 1;
+  g.first_shard = (int)o[22];
+  g.tile_order = (int)o[23];
+  g.act = (int)o[24];
+  g.a_table = (const uint64_t*)o[25];
+  g.shard_rows = o[26];
+  g.timeout_word = d_timeout_;
+  return g;
+}
+
+void PlanExecutor::prepare(uintptr_t main_stream) {
+  // hipBLASLt GEMMs (mode blas): build and autotune every shape now, on the stream the op will
+  // run on, so enqueueing a run never blocks on a tuning pass (blaslt.cpp autotune).
+  hipStream_t main = (hipStream_t)main_stream;
+  bool any = false;
+  for (size_t i = 0; i < ops_.size(); i += kOpWords) {
+    const int64_t* o = &ops_[i];
+    if (o[0] != OP_GEMM || o[18] != GEMM_MODE_BLAS) continue;
+    const GemmArgs g = gemm_args(o);
+    (void)blaslt_prepare(g, (int)o[15], (int)o[16], S(o[1], main));  // unsupported: MFMA path
+    if (cap_stream_ != nullptr) (void)blaslt_prepare(g, (int)o[15], (int)o[16], cap_stream_);
+    any = true;
+  }
+  if (any) DDLB_HIP(hipDeviceSynchronize());
+}
+
 void PlanExecutor::exec(const int64_t* o, hipStream_t main) {
   hipStream_t s = S(o[1], main);
   switch (o[0]) {
     case OP_NOP: return;
     case OP_GEMM: {
-      GemmArgs g;
-      g.a = (const void*)o[2];
-      g.b = (const void*)o[3];
-      g.c = (void*)o[4];
-      g.lda = o[5]; g.ldb = o[6]; g.ldc = o[7];
-      g.a_grp = o[8]; g.a_gstride = o[9];
-      g.c_grp = o[10]; g.c_gstride = o[11];
-      g.M = (int)o[12]; g.N = (int)o[13]; g.K = (int)o[14];
-      g.flags = (const unsigned*)o[19];
-      g.epoch = epoch_;
-      g.flag_rows = o[20] > 0 ? o[20] : 1;
-      g.nshards = o[21] > 0 ? (int)o[21] : 1;
-      g.first_shard = (int)o[22];
-      g.tile_order = (int)o[23];
-      g.act = (int)o[24];
-      g.a_table = (const uint64_t*)o[25];
-      g.shard_rows = o[26];
-      g.timeout_word = d_timeout_;
+      const GemmArgs g = gemm_args(o);
       DDLB_HIP(gemm_launch(g, (int)o[15], (int)o[16], (int)o[17], (int)o[18], s));
       return;
     }

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../comm/comm.h"
+#include "../gemm/gemm.h"
 
 namespace ddlb {
 
@@ -50,6 +51,9 @@ class PlanExecutor {
   PlanExecutor(int device, int nstreams, int nevents, const std::vector<int>& priorities);
   ~PlanExecutor();
   void load(const std::vector<int64_t>& ops);
+  // Bind-time work that must not happen inside run(): hipBLASLt plan building / autotuning
+  // (host-synchronous) for the plan's blas GEMMs. Call once after load().
+  void prepare(uintptr_t main_stream);
   void set_comm(RcclComm* comm) { comm_ = comm; }
   // Enqueue the whole plan behind `main_stream`; returns the epoch used (1, 2, ...).
   unsigned run(uintptr_t main_stream);
@@ -67,6 +71,7 @@ class PlanExecutor {
 
  private:
   void exec(const int64_t* op, hipStream_t main);
+  GemmArgs gemm_args(const int64_t* op) const;
   void enqueue(hipStream_t main);
   bool any_side_ = false;
   bool graph_on_ = false;

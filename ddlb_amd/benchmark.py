@@ -147,6 +147,9 @@ def run_single(primitive: str, impl_id: str, m: int, n: int, k: int, dtype: str,
                                      barrier_at_each_iteration, num_iterations)
         t = torch.tensor(times, dtype=torch.float64, device=comm.device)
         comm.all_reduce_max(t)
+        # a device-side bounded wait that gave up during warmup / timing means some step ran on
+        # stale data: an error row even when validation is off
+        impl.check_health()
         times = t.cpu().tolist()
         row.update(summarize(times, m, n, k))
         row.update(derived_metrics(primitive, base, str(opts_used.get("size", "")), m, n, k, dtype,

@@ -29,14 +29,15 @@ def _raw_stream(device_index: int) -> int:
 
 
 class SymmetricBuffer:
-    def __init__(self, ctx: "NativeContext", nbytes: int, zero: bool = True):
+    def __init__(self, ctx: "NativeContext", nbytes: int, uncached: bool = False):
         import torch
         import torch.distributed as dist
 
         self.ctx = ctx
         self.nbytes = int(nbytes)
         C = ctx.C
-        self.h = C.SymmetricBuffer(self.nbytes, ctx.device_index)  # zero-filled by hipMemset
+        # zero-filled by hipMemset; ``uncached`` (flag words): fine-grained memory no GPU caches
+        self.h = C.SymmetricBuffer(self.nbytes, ctx.device_index, bool(uncached))
         handles: List = [None] * ctx.world
         mine = bytes(self.h.ipc_handle())
         if ctx.world > 1:
@@ -90,8 +91,8 @@ class NativeContext:
             self._rccl = self.C.RcclComm(obj[0], self.world, self.rank, self.device_index)
         return self._rccl
 
-    def symmetric(self, nbytes: int) -> SymmetricBuffer:
-        buf = SymmetricBuffer(self, nbytes)
+    def symmetric(self, nbytes: int, uncached: bool = False) -> SymmetricBuffer:
+        buf = SymmetricBuffer(self, nbytes, uncached=uncached)
         self._owned.append(buf)
         return buf
 
@@ -146,7 +147,9 @@ class BoundPlan:
                     raise ValueError(f"external {name}: {raw.numel()} B < {spec.nbytes} B needed")
                 self.local[name] = raw
             elif spec.symmetric:
-                self.sym[name] = ctx.symmetric(spec.nbytes)
+                # zero-initialised symmetric buffers are the cross-process flag words: peers
+                # write them over xGMI while this GPU polls, so they live in uncached memory
+                self.sym[name] = ctx.symmetric(spec.nbytes, uncached=spec.zero)
             else:
                 self.local[name] = torch.zeros(max(spec.nbytes, 16), dtype=torch.uint8,
                                                device=dev)
@@ -161,6 +164,7 @@ class BoundPlan:
         self.ex = C.PlanExecutor(ctx.device_index, plan.nstreams, max(plan.nevents, 1),
                                  list(plan.stream_priority))
         self.ex.load(words)
+        self.ex.prepare(_raw_stream(ctx.device_index))  # bind-time hipBLASLt tuning, if any
         if any(op.kind in (OP_ALLGATHER, OP_REDUCE_SCATTER, OP_SEND, OP_RECV) for op in plan.ops):
             self.ex.set_comm(ctx.rccl())
         torch.cuda.synchronize(dev)

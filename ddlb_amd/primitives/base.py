@@ -136,6 +136,10 @@ class Primitive(ABC):
         assert_close(got.to(torch.float32), ref.to(torch.float32), rtol=0,
                      atol=atol_for(self.dtype, self.k))
 
+    def check_health(self) -> None:
+        """Raise if a device-side bounded wait gave up during the runs so far (native plans
+        record that in a timeout word; the library-backed implementations have none)."""
+
     def close(self) -> None:
         """Release implementation resources (streams, plans, process groups)."""
 

@@ -55,8 +55,11 @@ class NativeTPColumnwise(TPColumnwise):
         self.bound.run()
         return self.out
 
-    def validate(self, result) -> None:
+    def check_health(self) -> None:
         self.bound.check_health()
+
+    def validate(self, result) -> None:
+        self.check_health()
         super().validate(result)
 
     def close(self) -> None:

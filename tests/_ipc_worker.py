@@ -25,7 +25,8 @@ def main():
     for label, prim, opts in cfgs:
         try:
             cls = NativeTPColumnwise if prim == "col" else NativeTPRowwise
-            impl = cls(m=1536, n=512, k=768, dtype=opts.pop("dtype", "bfloat16"), **opts)
+            impl = cls(m=opts.pop("m", 1536), n=512, k=768, dtype=opts.pop("dtype", "bfloat16"),
+                       **opts)
             for it in range(4):
                 out = impl.run()
                 torch.cuda.synchronize()

@@ -118,3 +118,85 @@ def test_candidate_pools():
     fp8 = bench.candidate_pool("tp_columnwise", "float8_e4m3fn", 1)
     labels = [c[0] for c in fp8]
     assert "gemm (world=1)/hip/mx" in labels and not any("blas" in x for x in labels)
+
+
+class _FakeJob:
+    """Scripted Job: ``script[label]`` = list of results returned by successive measure()
+    calls of that candidate (tuning first, then the final run)."""
+
+    rank = 0
+
+    def __init__(self, pool, script):
+        self.by_opts = {json.dumps(o, sort_keys=True): lbl for lbl, _, o in pool}
+        self.script = {k: list(v) for k, v in script.items()}
+        self.calls = []
+
+    def bcast(self, obj):
+        return obj
+
+    def log(self, msg):
+        pass
+
+    def measure(self, impl, opts, steps, warmup, validate, timeout, prewarm_ms=0.0):
+        label = self.by_opts[json.dumps(opts, sort_keys=True)]
+        self.calls.append((label, validate))
+        return self.script[label].pop(0)
+
+
+def _args(**kw):
+    import argparse
+
+    d = dict(tune_rounds=1, tune_steps=5, validate=True, candidate_timeout=10.0,
+             tune_budget_s=1e9, tune_cap_s=1e9, prewarm_ms=0.0, steps=5, warmup=1)
+    d.update(kw)
+    return argparse.Namespace(**d)
+
+
+def _ok(ms, valid=True, why=""):
+    return {"ok": True, "ms": ms, "valid": valid, "validation": why}
+
+
+def test_autotune_rejects_fast_invalid_candidate():
+    """A candidate that is fastest but computes the wrong numbers never wins: the
+    tuning runs validate, and an invalid result counts as a failure."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    pool = [("fast-wrong", "native", {"x": 1}), ("slow-right", "native", {"x": 2}),
+            ("vendor", "pytorch", {"x": 3})]
+    job = _FakeJob(pool, {"fast-wrong": [_ok(0.5, False, "mismatch")],
+                          "slow-right": [_ok(1.0), _ok(1.1)], "vendor": [_ok(2.0)]})
+    tune = {}
+    chosen, fallbacks = bench.autotune(job, pool, _args(), 2, tune)
+    assert chosen[0] == "slow-right"
+    assert all(v for _, v in job.calls), "tuning must validate"
+    assert "invalid" in tune["fast-wrong"]
+    assert [c[0] for c in fallbacks] == ["vendor"]
+    cand, final = bench.final_measure(job, chosen, fallbacks, _args(), tune)
+    assert cand[0] == "slow-right" and final["valid"] is True
+
+
+def test_final_falls_back_when_winner_does_not_validate():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    pool = [("a", "native", {"x": 1}), ("b", "native", {"x": 2}), ("v", "pytorch", {"x": 3})]
+    job = _FakeJob(pool, {"a": [_ok(0.5), _ok(0.5, False, "bad last step")],
+                          "b": [_ok(0.7), {"ok": False, "error": "timeout after 10s"}],
+                          "v": [_ok(0.9), _ok(0.95)]})
+    tune = {}
+    chosen, fallbacks = bench.autotune(job, pool, _args(), 2, tune)
+    assert chosen[0] == "a" and [c[0] for c in fallbacks] == ["b", "v"]
+    cand, final = bench.final_measure(job, chosen, fallbacks, _args(), tune)
+    assert cand[0] == "v" and final["valid"] is True
+    assert tune["final_fallback_from"] == "a" and len(tune["final_rejected"]) == 2
+
+
+def test_final_reports_invalid_when_nothing_validates():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    pool = [("a", "native", {"x": 1})]
+    job = _FakeJob(pool, {"a": [_ok(0.5, False, "bad")]})
+    cand, final = bench.final_measure(job, pool[0], [], _args(), {})
+    assert cand[0] == "a" and final["valid"] is False

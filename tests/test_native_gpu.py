@@ -115,6 +115,13 @@ def _ipc_cfgs():
                  dict(algorithm="coll_pipeline", backend="ipc", order="AG_after", s=2)))
     cfgs.append(("col/p2p/fused", "col", dict(algorithm="p2p_pipeline", backend="ipc",
                                               fused=True)))
+    # m/d (480 at d=2, 320 at d=3) is not a multiple of the GEMM tile height, so tiles span two
+    # shards: the flag-gated GEMM must wait for every shard a tile reads
+    cfgs.append(("col/p2p/fused/misaligned", "col", dict(algorithm="p2p_pipeline",
+                                                         backend="ipc", fused=True, m=960)))
+    cfgs.append(("col/p2p/fused/misaligned256", "col", dict(algorithm="p2p_pipeline",
+                                                            backend="ipc", fused=True, m=1920,
+                                                            tile="256x256")))
     cfgs.append(("col/p2p/noring", "col", dict(algorithm="p2p_pipeline", backend="ipc",
                                                offset_stream_indexing_by_rank=False)))
     cfgs.append(("col/p2p/fp8", "col", dict(algorithm="p2p_pipeline", backend="ipc",
