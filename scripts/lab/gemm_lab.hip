@@ -1362,6 +1362,16 @@ __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
   const int my_tiles =
       ((int)blockIdx.x < ntiles) ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
   if (my_tiles == 0) return;
+  // stagger experiments (round 2): delay some blocks at the start so the chip-wide C-store
+  // bursts at tile ends are spread in time. 64: odd blocks ~half a tile; 128: odd blocks ~a
+  // sixth; 192: block % 4 phases of ~a quarter tile each
+  if constexpr ((SKIP & 192) == 64) {
+    if (blockIdx.x & 1) for (int i = 0; i < 3; ++i) __builtin_amdgcn_s_sleep(127);
+  } else if constexpr ((SKIP & 192) == 128) {
+    if (blockIdx.x & 1) __builtin_amdgcn_s_sleep(127);
+  } else if constexpr ((SKIP & 192) == 192) {
+    for (int i = 0; i < (int)(blockIdx.x & 3) * 2; ++i) __builtin_amdgcn_s_sleep(100);
+  }
   // LDS-DMA sources: per-lane 32-bit byte offsets inside a tile's A / B panels (row * ld + swizzled
   // chunk) plus wave-uniform panel bases, so the per-tile state is two scalar pointers
   const int drow = lane >> 3, dpc = lane & 7;
@@ -1452,36 +1462,67 @@ __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
               acc[mq * 4 + f][nq * 2 + g], 0, 0, 0);
   };
   int ti = 0;
-  auto store_q = [&](int mq, int nq) __attribute__((always_inline)) {
+  // one fragment row-block (f) of quadrant (mq, nq) of tile sti: 8 bf16 per lane, then zeroed
+  auto store_frag = [&](int mq, int nq, int f, int sti) __attribute__((always_inline)) {
+    const int i = mq * 4 + f;
     if constexpr ((SKIP & 2) != 0) {
-#pragma unroll
-      for (int f = 0; f < 4; ++f) asm volatile("" ::"v"(acc[mq * 4 + f][nq * 2]), "v"(acc[mq * 4 + f][nq * 2 + 1]));
+      asm volatile("" ::"v"(acc[i][nq * 2]), "v"(acc[i][nq * 2 + 1]));
       return;
     }
     int64_t m0, n0;
-    origin(ti, m0, n0);
+    origin(sti, m0, n0);
+    if constexpr ((SKIP & 512) != 0) {  // timing only: every tile of a block stores to one small
+      m0 = (int64_t)(blockIdx.x % 64) * 256;  // C region (L2-resident lines, no HBM write stream)
+      n0 = 0;
+    }
+    char* crow = (char*)p.c + (m0 + wr * 128 + mq * 64 + f * 16 + frow) * p.ldc * 2;
+    const f32x4 v0 = acc[i][nq * 2], v1 = acc[i][nq * 2 + 1];
+    bf16x8 o = {(__bf16)v0.x, (__bf16)v0.y, (__bf16)v0.z, (__bf16)v0.w,
+                (__bf16)v1.x, (__bf16)v1.y, (__bf16)v1.z, (__bf16)v1.w};
+    if constexpr ((SKIP & 32) != 0) {  // timing only: same bytes, one full 128 B line per 8 lanes
+      const int rl = lane >> 3, ch = lane & 7;
+      char* rrow = (char*)p.c + (m0 + wr * 128 + mq * 64 + f * 16 + nq * 8 + rl) * p.ldc * 2;
+      char* dst = rrow + (n0 + wc * 64 + ch * 8) * 2;
+      if constexpr ((SKIP & 16) != 0) __builtin_nontemporal_store(__builtin_bit_cast(i32x4, o), (i32x4*)dst);
+      else *(uint4*)dst = __builtin_bit_cast(uint4, o);
+    } else if constexpr ((SKIP & 16) != 0) {  // non-temporal (streaming) store: C is never re-read
+      __builtin_nontemporal_store(__builtin_bit_cast(i32x4, o),
+                                  (i32x4*)(crow + (n0 + wc * 64 + nq * 32 + fq * 8) * 2));
+    } else {
+      *(uint4*)(crow + (n0 + wc * 64 + nq * 32 + fq * 8) * 2) = __builtin_bit_cast(uint4, o);
+    }
+    acc[i][nq * 2] = f32x4{0.f, 0.f, 0.f, 0.f};
+    acc[i][nq * 2 + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  auto store_q = [&](int mq, int nq, int sti) __attribute__((always_inline)) {
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      const int i = mq * 4 + f;
-      char* crow = (char*)p.c + (m0 + wr * 128 + mq * 64 + f * 16 + frow) * p.ldc * 2;
-      const f32x4 v0 = acc[i][nq * 2], v1 = acc[i][nq * 2 + 1];
-      bf16x8 o = {(__bf16)v0.x, (__bf16)v0.y, (__bf16)v0.z, (__bf16)v0.w,
-                  (__bf16)v1.x, (__bf16)v1.y, (__bf16)v1.z, (__bf16)v1.w};
-      if constexpr ((SKIP & 32) != 0) {  // timing only: same bytes, one full 128 B line per 8 lanes
-        const int rl = lane >> 3, ch = lane & 7;
-        char* rrow = (char*)p.c + (m0 + wr * 128 + mq * 64 + f * 16 + nq * 8 + rl) * p.ldc * 2;
-        char* dst = rrow + (n0 + wc * 64 + ch * 8) * 2;
-        if constexpr ((SKIP & 16) != 0) __builtin_nontemporal_store(__builtin_bit_cast(i32x4, o), (i32x4*)dst);
-        else *(uint4*)dst = __builtin_bit_cast(uint4, o);
-      } else if constexpr ((SKIP & 16) != 0) {  // non-temporal (streaming) store: C is never re-read
-        __builtin_nontemporal_store(__builtin_bit_cast(i32x4, o),
-                                    (i32x4*)(crow + (n0 + wc * 64 + nq * 32 + fq * 8) * 2));
-      } else {
-        *(uint4*)(crow + (n0 + wc * 64 + nq * 32 + fq * 8) * 2) = __builtin_bit_cast(uint4, o);
+    for (int f = 0; f < 4; ++f) store_frag(mq, nq, f, sti);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // MFMAs of quadrants (mq, na) then (mq, nb) — 32 — with the 8 fragment stores of quadrants
+  // (smq, 0) and (smq, 1) of tile sti interleaved, one after every 4 MFMAs (SKIP & 256): spreads
+  // the C-store issue over a compute section instead of bunching it after one
+  auto mm_st = [&](int mq, int na, int nb, int smq, int sti) __attribute__((always_inline)) {
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int nq = half ? nb : na;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if constexpr ((SKIP & 1024) == 0) __builtin_amdgcn_sched_barrier(0);
+        const int kk = c >> 1;
+#pragma unroll
+        for (int ff = 0; ff < 2; ++ff)
+#pragma unroll
+          for (int g = 0; g < 2; ++g) {
+            const int f = (c & 1) * 2 + ff;
+            acc[mq * 4 + f][nq * 2 + g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8, bR[nq][g][kk]), __builtin_bit_cast(bf16x8, aR[f][kk]),
+                acc[mq * 4 + f][nq * 2 + g], 0, 0, 0);
+          }
+        const int si = half * 4 + c;  // store #si: quadrant (smq, si >> 2), fragment si & 3
+        store_frag(smq, si >> 2, si & 3, sti);
       }
-      acc[i][nq * 2] = f32x4{0.f, 0.f, 0.f, 0.f};
-      acc[i][nq * 2 + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -1507,7 +1548,11 @@ __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
   wait_vm<6>();
   T4_BAR();
   if (g1) T4_BAR();
-  // KIND: 0 normal, 1 last K-tile of a tile, 2 first K-tile after a tile's last
+  // KIND: 0 normal, 1 last K-tile of a tile, 2 first K-tile after a tile's last, 3 second
+  // (3 only with interleaved stores, SKIP & 256: Q00/Q01 of the finished tile are stored inside
+  // phase B of its last K-tile, Q11/Q10 inside phase A of the next tile's first K-tile; the
+  // counted waits keep exactly the ops younger than the unit a phase reads in flight)
+  constexpr bool ILS = (SKIP & 256) != 0;
   auto iter = [&](int h, auto kind_tag) __attribute__((always_inline)) {
     constexpr int KIND = decltype(kind_tag)::value;
     const int b = h & 1;
@@ -1518,27 +1563,51 @@ __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
     stage(0, UA0, qa, b ^ 1);
     stage(1, UA1, qa, b ^ 1);
     T4_LGKM0();
-    if (g1) wait_vm<KIND == 2 ? 8 + 4 * NS : 8>();
+    if constexpr (ILS) {
+      if (g1) wait_vm<KIND == 2 || KIND == 3 ? 8 + 2 * NS : 8>();
+    } else {
+      if (g1) wait_vm<KIND == 2 ? 8 + 4 * NS : 8>();
+    }
     T4_BAR();
     __builtin_amdgcn_s_setprio(1);
-    mm(0, 0);
-    mm(0, 1);
+    if constexpr (ILS && KIND == 2) {
+      mm_st(0, 0, 1, 1, ti - 1);
+    } else {
+      mm(0, 0);
+      mm(0, 1);
+    }
     __builtin_amdgcn_s_setprio(0);
-    if constexpr (KIND == 1) { store_q(0, 0); store_q(0, 1); }
-    if (!g1) wait_vm<KIND == 1 ? 8 + 2 * NS : (KIND == 2 ? 8 + 4 * NS : 8)>();
+    if constexpr (!ILS && KIND == 1) { store_q(0, 0, ti); store_q(0, 1, ti); }
+    if constexpr (ILS) {
+      if (!g1) wait_vm<KIND == 2 ? 8 + 4 * NS : (KIND == 3 ? 8 + 2 * NS : 8)>();
+    } else {
+      if (!g1) wait_vm<KIND == 1 ? 8 + 2 * NS : (KIND == 2 ? 8 + 4 * NS : 8)>();
+    }
     T4_BAR();
     loadA(cur, 1);  // phase B
     stage(2, UB0, qb, b);
     stage(3, UB1, qb, b);
     T4_LGKM0();
-    if (g1) wait_vm<KIND == 1 ? 6 + 2 * NS : 6>();
+    if constexpr (ILS) {
+      if (g1) wait_vm<KIND == 2 ? 6 + 2 * NS : 6>();
+    } else {
+      if (g1) wait_vm<KIND == 1 ? 6 + 2 * NS : 6>();
+    }
     T4_BAR();
     __builtin_amdgcn_s_setprio(1);
-    mm(1, 1);
-    mm(1, 0);
+    if constexpr (ILS && KIND == 1) {
+      mm_st(1, 1, 0, 0, ti);
+    } else {
+      mm(1, 1);
+      mm(1, 0);
+    }
     __builtin_amdgcn_s_setprio(0);
-    if constexpr (KIND == 1) { store_q(1, 1); store_q(1, 0); }
-    if (!g1) wait_vm<KIND == 1 ? 6 + 4 * NS : 6>();
+    if constexpr (!ILS && KIND == 1) { store_q(1, 1, ti); store_q(1, 0, ti); }
+    if constexpr (ILS) {
+      if (!g1) wait_vm<KIND == 1 || KIND == 2 ? 6 + 2 * NS : 6>();
+    } else {
+      if (!g1) wait_vm<KIND == 1 ? 6 + 4 * NS : 6>();
+    }
     T4_BAR();
     qa = qb;
     adv(qb);
@@ -1547,9 +1616,14 @@ __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
   for (ti = 0; ti < my_tiles; ++ti) {
     int t = 0;
     if (ti > 0) { iter(h, std::integral_constant<int, 2>{}); ++h; ++t; }
+    if (ILS && ti > 0) { iter(h, std::integral_constant<int, 3>{}); ++h; ++t; }
     for (; t < nk - 1; ++t, ++h) iter(h, std::integral_constant<int, 0>{});
     iter(h, std::integral_constant<int, 1>{});
     ++h;
+  }
+  if constexpr (ILS) {  // the last tile's Q11 / Q10 have no next tile to hide under
+    store_q(1, 1, my_tiles - 1);
+    store_q(1, 0, my_tiles - 1);
   }
   if (!g1) T4_BAR();
 #undef T4_BAR
@@ -1994,6 +2068,14 @@ int main(int argc, char** argv) {
       {"pt4 noDMA", pt4_kernel<false, 1>, 2, 512, 0},
       {"pt4 noMFMA", pt4_kernel<false, 4>, 2, 512, 0},
       {"pt4 nt", pt4_kernel<false, 16>, 2, 512, 0},
+      {"pt4 nt stag2", pt4_kernel<false, 16 | 64>, 2, 512, 0},
+      {"pt4 nt stag6", pt4_kernel<false, 16 | 128>, 2, 512, 0},
+      {"pt4 nt stag4ph", pt4_kernel<false, 16 | 192>, 2, 512, 0},
+      {"pt4 nt noST", pt4_kernel<false, 16 | 2>, 2, 512, 0},
+      {"pt4 nt ils", pt4_kernel<false, 16 | 256>, 2, 512, 0},
+      {"pt4 nt ils free", pt4_kernel<false, 16 | 256 | 1024>, 2, 512, 0},
+      {"pt4 nt smallC", pt4_kernel<false, 16 | 512>, 2, 512, 0},
+      {"pt4 smallC", pt4_kernel<false, 512>, 2, 512, 0},
       {"pt4 fullline", pt4_kernel<false, 32>, 2, 512, 0},
       {"pt4 fullline nt", pt4_kernel<false, 48>, 2, 512, 0},
       {"pt4 noST", pt4_kernel<false, 2>, 2, 512, 0},
