@@ -73,6 +73,16 @@ CANDIDATES = [
     ("coll_pipeline/ipc/push/s4", "native", dict(_COLL_IPC, direction="push")),
     ("default/ipc/kernel/push", "native", dict(_DEF_K, direction="push")),
     ("coll_pipeline/rccl/s8", "native", dict(_COLL4, s=8)),
+    # Stage GEMMs next to CU-resident comm kernels (RCCL's, or our copy kernel): a persistent
+    # 256x256 GEMM pins one workgroup (its whole register file) per CU, so a CU held by the comm
+    # kernel delays that workgroup's tiles until the comm finishes; 128x128 tiles (4x as many,
+    # dispatched dynamically) let the busy CUs simply take fewer of them
+    ("coll_pipeline/rccl/s4/128", "native", dict(_COLL4, tile="128x128")),
+    ("coll_pipeline/rccl/s8/128", "native", dict(_COLL4, s=8, tile="128x128")),
+    ("coll_pipeline/ipc/kernel/s4", "native", dict(_COLL_IPC, multicast_protocol="kernel",
+                                                   copy_blocks=128, tile="128x128")),
+    ("coll_pipeline/ipc/memcpy/s8", "native", dict(_COLL_IPC, s=8)),
+    ("p2p_pipeline/rccl", "native", dict(algorithm="p2p_pipeline", backend="rccl")),
     # the same IPC paths with kernel-side flags (system-scope atomics, spin on a CU) instead of
     # stream memops; a hedge for fabrics where the command processor's polling is slow
     ("p2p_pipeline/ipc/memcpy/ksig", "native", dict(_P2P, signal="kernel")),
@@ -90,6 +100,8 @@ ROW_CANDIDATES = [
     ("row/default/rccl", "native", dict(algorithm="default", backend="rccl")),
     ("row/default/rccl/blas", "native", _blas(dict(algorithm="default", backend="rccl"))),
     ("row/coll_pipeline/rccl/s4", "native", dict(algorithm="coll_pipeline", backend="rccl", s=4)),
+    ("row/coll_pipeline/rccl/s4/128", "native", dict(algorithm="coll_pipeline", backend="rccl",
+                                                     s=4, tile="128x128")),
     ("row/p2p_pipeline/rccl", "native", dict(algorithm="p2p_pipeline", backend="rccl")),
     ("row/default/ipc/kernel", "native", dict(_RK, algorithm="default")),
     ("row/default/ipc/kernel/blas", "native", _blas(dict(_RK, algorithm="default"))),

@@ -141,3 +141,39 @@ def test_invalid_configs():
         build_tp_columnwise(0, 2, 30, 8, 8, DT_F32, DT_F32, AlgoConfig(algorithm="coll_pipeline", s=4))
     with pytest.raises(ValueError):
         build_tp_rowwise(0, 2, 16, 8, 7, DT_F32, DT_F32, AlgoConfig())
+
+
+def _bench_native_cfgs():
+    """(primitive, label, AlgoConfig) of every native candidate bench.py can pick at world > 1."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from ddlb_amd.primitives.native_common import algo_config
+    from ddlb_amd.primitives.registry import resolve
+
+    out = []
+    for prim in ("tp_columnwise", "tp_rowwise"):
+        for label, impl, opts in bench.candidate_pool(prim, "bfloat16", 8):
+            if impl != "native":
+                continue
+            cls, o, _ = resolve(prim, impl, dict(opts))
+            merged = {**cls.DEFAULT_OPTIONS, **o}
+            for key, alias in cls.OPTION_ALIASES.items():
+                merged[key] = alias.get(merged[key], merged[key])
+            out.append((prim, label, algo_config(merged, order=merged.get("order", "AG_before"))))
+    return out
+
+
+@pytest.mark.parametrize("d", [2, 4, 8])
+@pytest.mark.parametrize("prim,label,cfg", _bench_native_cfgs(),
+                         ids=[c[1] for c in _bench_native_cfgs()])
+def test_bench_candidates_simulate(d, prim, label, cfg):
+    """Every native candidate of the N>1 bench pool, at the driver's world sizes (incl. 8, which
+    no GPU box here can run): protocol completes, no race, exact result, several epochs."""
+    s = cfg.s if cfg.algorithm == "coll_pipeline" else 1
+    if prim == "tp_columnwise":
+        _run_col(d, m=4 * d * s, n=8, k=12, cfg=cfg, epochs=2)
+    else:
+        _run_row(d, m=4 * d * s, n=8, k=4 * d, cfg=cfg, epochs=2)
