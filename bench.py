@@ -79,6 +79,10 @@ CANDIDATES = [
     # dispatched dynamically) let the busy CUs simply take fewer of them
     ("coll_pipeline/rccl/s4/128", "native", dict(_COLL4, tile="128x128")),
     ("coll_pipeline/rccl/s8/128", "native", dict(_COLL4, s=8, tile="128x128")),
+    # the same with RCCL held to 16 channels (16 CUs): more of the chip left to the GEMM while
+    # the gather of the next stage runs (RCCL reads the cap at communicator init)
+    ("coll_pipeline/rccl/s4/128/c16", "native", dict(_COLL4, tile="128x128",
+                                                      _env={"NCCL_MAX_NCHANNELS": "16"})),
     ("coll_pipeline/ipc/kernel/s4", "native", dict(_COLL_IPC, multicast_protocol="kernel",
                                                    copy_blocks=128, tile="128x128")),
     ("coll_pipeline/ipc/memcpy/s8", "native", dict(_COLL_IPC, s=8)),
@@ -269,6 +273,8 @@ class Job:
         out = os.path.join(self.tmp, f"ddlb_bench_{os.getpid()}_{self.counter}.json")
         env = dict(os.environ)
         env["DDLB_CHILD_INIT_METHOD"] = f"tcp://127.0.0.1:{port}"
+        opts = dict(opts)
+        env.update(opts.pop("_env", {}))  # per-candidate runtime settings (e.g. RCCL channels)
         cmd = [sys.executable, os.path.abspath(__file__), "--child", "--child-out", out,
                "--child-impl", impl, "--child-opts", json.dumps(opts), "--steps", str(steps),
                "--warmup", str(warmup), "--primitive", self.a.primitive,
