@@ -29,7 +29,8 @@ __device__ __forceinline__ void wait_vm() {
 // Each wave streams `iters` 1-KiB LDS-DMA pieces from src (wrapping inside `span` bytes, offset
 // per block so blocks do not share lines unless span is small) into its own 8 KiB LDS ring,
 // keeping INFLIGHT pieces outstanding. STORE: each piece is instead a 1-KiB global store.
-template <int INFLIGHT, bool STORE>
+// BUF: the same through a buffer resource (wave-uniform descriptor + 32-bit per-lane offset)
+template <int INFLIGHT, bool STORE, bool BUF = false>
 __global__ __launch_bounds__(512) void dma_kernel(const char* src, char* dst, int64_t span,
                                                   int iters, unsigned long long* cyc) {
   __shared__ __attribute__((aligned(1024))) char smem[8 * 8192];
@@ -42,7 +43,18 @@ __global__ __launch_bounds__(512) void dma_kernel(const char* src, char* dst, in
     // L2-resident mode: waves start at different 1 KiB pieces of the span (no hot spot)
     // (span is a power of two: a mask, not a 64-bit modulo, which would bound the loop itself)
     const int64_t o = (off + ((int64_t)blockIdx.x * 8 + wave) * 37 * 1024) & (span - 1);
-    if constexpr (STORE) {
+    if constexpr (BUF) {
+      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+          STORE ? (void*)dst : (void*)src, 0, 0x7FFFFFF0, 0x00020000);
+      if constexpr (STORE) {
+        typedef __attribute__((ext_vector_type(4))) int i32x4;
+        const i32x4 v = {i, 0, 0, lane};
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, (unsigned)o + lane * 16, 0, 0);
+      } else {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void*)(ring + (i & 7) * 1024), 16,
+                                                 (unsigned)o + lane * 16, 0, 0, 0);
+      }
+    } else if constexpr (STORE) {
       uint4 v = {(unsigned)i, 0u, 0u, (unsigned)lane};
       *(uint4*)(dst + o + lane * 16) = v;
     } else {
@@ -57,17 +69,17 @@ __global__ __launch_bounds__(512) void dma_kernel(const char* src, char* dst, in
   if (lane == 0 && wave == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
-template <int INFLIGHT, bool STORE>
+template <int INFLIGHT, bool STORE, bool BUF = false>
 void run(const char* tag, const char* src, char* dst, int64_t span, int nblk, int iters,
          unsigned long long* cyc) {
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  hipLaunchKernelGGL((dma_kernel<INFLIGHT, STORE>), dim3(nblk), dim3(512), 0, 0, src, dst, span,
+  hipLaunchKernelGGL((dma_kernel<INFLIGHT, STORE, BUF>), dim3(nblk), dim3(512), 0, 0, src, dst, span,
                      iters, cyc);
   CHECK(hipEventRecord(e0));
   for (int r = 0; r < 5; ++r)
-    hipLaunchKernelGGL((dma_kernel<INFLIGHT, STORE>), dim3(nblk), dim3(512), 0, 0, src, dst,
+    hipLaunchKernelGGL((dma_kernel<INFLIGHT, STORE, BUF>), dim3(nblk), dim3(512), 0, 0, src, dst,
                        span, iters, cyc);
   CHECK(hipEventRecord(e1));
   CHECK(hipEventSynchronize(e1));
@@ -110,5 +122,10 @@ int main() {
   run<4, true>("store, L2-resident", src, dst, l2, ncu, iters, cyc);
   run<16, true>("store, L2-resident", src, dst, l2, ncu, iters, cyc);
   run<16, true>("store, HBM-streamed", src, dst, big, ncu, iters / 8, cyc);
+  run<2, false, true>("buffer LDS-DMA, L2-resident", src, dst, l2, ncu, iters, cyc);
+  run<8, false, true>("buffer LDS-DMA, L2-resident", src, dst, l2, ncu, iters, cyc);
+  run<4, true, true>("buffer store, L2-resident", src, dst, l2, ncu, iters, cyc);
+  run<16, true, true>("buffer store, L2-resident", src, dst, l2, ncu, iters, cyc);
+  run<16, true, true>("buffer store, HBM-streamed", src, dst, big, ncu, iters / 8, cyc);
   return 0;
 }
