@@ -1569,14 +1569,14 @@ __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
       if (g1) wait_vm<KIND == 2 ? 8 + 4 * NS : 8>();
     }
     T4_BAR();
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr ((SKIP & 2048) == 0) __builtin_amdgcn_s_setprio((SKIP & 4096) ? 0 : 1);
     if constexpr (ILS && KIND == 2) {
       mm_st(0, 0, 1, 1, ti - 1);
     } else {
       mm(0, 0);
       mm(0, 1);
     }
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr ((SKIP & 2048) == 0) __builtin_amdgcn_s_setprio((SKIP & 4096) ? 1 : 0);
     if constexpr (!ILS && KIND == 1) { store_q(0, 0, ti); store_q(0, 1, ti); }
     if constexpr (ILS) {
       if (!g1) wait_vm<KIND == 2 ? 8 + 4 * NS : (KIND == 3 ? 8 + 2 * NS : 8)>();
@@ -1594,14 +1594,14 @@ __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
       if (g1) wait_vm<KIND == 1 ? 6 + 2 * NS : 6>();
     }
     T4_BAR();
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr ((SKIP & 2048) == 0) __builtin_amdgcn_s_setprio((SKIP & 4096) ? 0 : 1);
     if constexpr (ILS && KIND == 1) {
       mm_st(1, 1, 0, 0, ti);
     } else {
       mm(1, 1);
       mm(1, 0);
     }
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr ((SKIP & 2048) == 0) __builtin_amdgcn_s_setprio((SKIP & 4096) ? 1 : 0);
     if constexpr (!ILS && KIND == 1) { store_q(1, 1, ti); store_q(1, 0, ti); }
     if constexpr (ILS) {
       if (!g1) wait_vm<KIND == 1 || KIND == 2 ? 6 + 2 * NS : 6>();
@@ -2073,6 +2073,8 @@ int main(int argc, char** argv) {
       {"pt4 nt stag4ph", pt4_kernel<false, 16 | 192>, 2, 512, 0},
       {"pt4 nt noST", pt4_kernel<false, 16 | 2>, 2, 512, 0},
       {"pt4 nt ils", pt4_kernel<false, 16 | 256>, 2, 512, 0},
+      {"pt4 nt noprio", pt4_kernel<false, 16 | 2048>, 2, 512, 0},
+      {"pt4 nt loadprio", pt4_kernel<false, 16 | 4096>, 2, 512, 0},
       {"pt4 nt ils free", pt4_kernel<false, 16 | 256 | 1024>, 2, 512, 0},
       {"pt4 nt smallC", pt4_kernel<false, 16 | 512>, 2, 512, 0},
       {"pt4 smallC", pt4_kernel<false, 512>, 2, 512, 0},
