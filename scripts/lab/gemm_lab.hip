@@ -1415,8 +1415,22 @@ __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
     const char* base = (which < 2 ? baseA : baseB) + (int64_t)c.kt * ROWB;
     const unsigned* off = which < 2 ? offA[which] : offB[which - 2];
     char* dst = smem + buf * STAGE + unit_off + wave * 16 * ROWB;
-    glds16(base + off[0], dst);
-    glds16(base + off[1], dst + 8 * ROWB);
+    if constexpr ((SKIP & 8192) != 0) {
+      // buffer form: wave-uniform descriptor of the tile panel, the per-lane 32-bit offset as
+      // voffset and the K-tile offset as soffset: no per-lane 64-bit address arithmetic
+      const uint64_t u = (uint64_t)(which < 2 ? baseA : baseB);
+      const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u);
+      const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
+      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(((uint64_t)hi << 32) | lo), 0, 0x7FFFFFF0, 0x00020000);
+      const int soff = __builtin_amdgcn_readfirstlane(c.kt * ROWB);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void*)dst, 16, off[0], soff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void*)(dst + 8 * ROWB), 16, off[1], soff,
+                                               0, 0);
+    } else {
+      glds16(base + off[0], dst);
+      glds16(base + off[1], dst + 8 * ROWB);
+    }
   };
   const int frow = lane & 15, fq = lane >> 4, sw = (frow >> 1) & 7;
   const int c0 = ((0 + fq) ^ sw) * 16, c1 = ((4 + fq) ^ sw) * 16;
@@ -2074,6 +2088,7 @@ int main(int argc, char** argv) {
       {"pt4 nt noST", pt4_kernel<false, 16 | 2>, 2, 512, 0},
       {"pt4 nt ils", pt4_kernel<false, 16 | 256>, 2, 512, 0},
       {"pt4 nt noprio", pt4_kernel<false, 16 | 2048>, 2, 512, 0},
+      {"pt4 nt bufdma", pt4_kernel<false, 16 | 8192>, 2, 512, 0},
       {"pt4 nt loadprio", pt4_kernel<false, 16 | 4096>, 2, 512, 0},
       {"pt4 nt ils free", pt4_kernel<false, 16 | 256 | 1024>, 2, 512, 0},
       {"pt4 nt smallC", pt4_kernel<false, 16 | 512>, 2, 512, 0},
