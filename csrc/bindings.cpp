@@ -185,5 +185,7 @@ PYBIND11_MODULE(_C, m) {
       .def("read_timeout", &PlanExecutor::read_timeout)
       .def("enable_graph", &PlanExecutor::enable_graph)
       .def("graph_enabled", &PlanExecutor::graph_enabled)
-      .def("graph_capturable", &PlanExecutor::graph_capturable);
+      .def("graph_capturable", &PlanExecutor::graph_capturable)
+      .def("set_timeline", &PlanExecutor::set_timeline)
+      .def("timeline", &PlanExecutor::timeline);
 }

@@ -33,6 +33,8 @@ PlanExecutor::PlanExecutor(int device, int nstreams, int nevents,
 
 PlanExecutor::~PlanExecutor() {
   hipSetDevice(device_);
+  if (tl_start_) hipEventDestroy(tl_start_);
+  for (auto e : tl_ops_) if (e) hipEventDestroy(e);
   if (graph_exec_) hipGraphExecDestroy(graph_exec_);
   if (graph_) hipGraphDestroy(graph_);
   if (cap_stream_) hipStreamDestroy(cap_stream_);
@@ -65,6 +67,7 @@ void PlanExecutor::load(const std::vector<int64_t>& ops) {
     }
   }
   ops_ = ops;
+  if (timeline_on_) set_timeline(true);  // one timing event per (new) op
   any_side_ = false;
   for (size_t i = 1; i < used_.size(); ++i) any_side_ = any_side_ || used_[i];
   if (graph_exec_) { hipGraphExecDestroy(graph_exec_); graph_exec_ = nullptr; }
@@ -81,6 +84,7 @@ bool PlanExecutor::graph_capturable() const {
 }
 
 void PlanExecutor::enable_graph(bool on) {
+  if (on && timeline_on_) throw std::runtime_error("hipGraph replay: turn the plan timeline off");
   if (on && !graph_capturable())
     throw std::runtime_error("plan has epoch-dependent ops (signals / arrival flags): "
                              "it cannot be replayed from a hipGraph");
@@ -97,14 +101,42 @@ unsigned PlanExecutor::read_timeout() {
   return v;
 }
 
+void PlanExecutor::set_timeline(bool on) {
+  if (on && graph_on_) throw std::runtime_error("plan timeline: not available with hipGraph replay");
+  DDLB_HIP(hipSetDevice(device_));
+  if (on && tl_start_ == nullptr) DDLB_HIP(hipEventCreate(&tl_start_));
+  const size_t n = ops_.size() / kOpWords;
+  while (on && tl_ops_.size() < n) {
+    hipEvent_t e = nullptr;
+    DDLB_HIP(hipEventCreate(&e));
+    tl_ops_.push_back(e);
+  }
+  timeline_on_ = on;
+}
+
+std::vector<float> PlanExecutor::timeline() {
+  if (!timeline_on_) throw std::runtime_error("plan timeline: call set_timeline(true) and run()");
+  const size_t n = ops_.size() / kOpWords;
+  std::vector<float> out(n, 0.f);
+  for (size_t i = 0; i < n; ++i) {
+    DDLB_HIP(hipEventSynchronize(tl_ops_[i]));
+    DDLB_HIP(hipEventElapsedTime(&out[i], tl_start_, tl_ops_[i]));
+  }
+  return out;
+}
+
 void PlanExecutor::enqueue(hipStream_t main) {
+  if (timeline_on_) DDLB_HIP(hipEventRecord(tl_start_, main));
   if (any_side_) {
     // fork: every used side stream waits for everything already queued on `main`
     DDLB_HIP(hipEventRecord(fork_join_[0], main));
     for (size_t i = 1; i < streams_.size(); ++i)
       if (used_[i]) DDLB_HIP(hipStreamWaitEvent(streams_[i], fork_join_[0], 0));
   }
-  for (size_t i = 0; i < ops_.size(); i += kOpWords) exec(&ops_[i], main);
+  for (size_t i = 0; i < ops_.size(); i += kOpWords) {
+    exec(&ops_[i], main);
+    if (timeline_on_) DDLB_HIP(hipEventRecord(tl_ops_[i / kOpWords], S(ops_[i + 1], main)));
+  }
   if (any_side_) {  // join
     for (size_t i = 1; i < streams_.size(); ++i)
       if (used_[i]) {

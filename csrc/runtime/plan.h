@@ -68,6 +68,12 @@ class PlanExecutor {
   void enable_graph(bool on);
   bool graph_enabled() const { return graph_on_; }
   bool graph_capturable() const;
+  // Per-op GPU timeline (observability): while on, run() records a timing event on the caller's
+  // stream before the fork and one on each op's stream right after the op. timeline() waits
+  // for the last run and returns, per op, the ms from the fork to the end of that op on its
+  // stream (ops with nothing to enqueue report their stream's previous end). Not with graphs.
+  void set_timeline(bool on);
+  std::vector<float> timeline();
 
  private:
   void exec(const int64_t* op, hipStream_t main);
@@ -88,6 +94,9 @@ class PlanExecutor {
   std::vector<int64_t> ops_;
   std::vector<bool> used_;             // stream i touched by the plan
   RcclComm* comm_ = nullptr;
+  bool timeline_on_ = false;
+  hipEvent_t tl_start_ = nullptr;
+  std::vector<hipEvent_t> tl_ops_;
   unsigned epoch_ = 0;
   unsigned* d_timeout_ = nullptr;
 };

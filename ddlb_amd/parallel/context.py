@@ -200,6 +200,26 @@ class BoundPlan:
             stream = _raw_stream(self.ctx.device_index)
         return self.ex.run(stream)
 
+    def set_timeline(self, on: bool = True) -> None:
+        """Record per-op GPU timing events on the next runs (see :meth:`timeline`)."""
+        self.ex.set_timeline(bool(on))
+
+    def timeline(self) -> List[Dict]:
+        """Per-op timing of the LAST run: ``start_ms`` / ``end_ms`` from the fork on the
+        caller's stream. An op's end is measured (an event on its stream right after it); its
+        start is the end of the previous op on the same stream, so waits show up as the time an
+        op spent blocked behind its dependencies."""
+        ends = self.ex.timeline()
+        last: Dict[int, float] = {}
+        rows = []
+        for i, (op, end) in enumerate(zip(self.plan.ops, ends)):
+            start = last.get(op.stream, 0.0)
+            end = max(float(end), start)
+            last[op.stream] = end
+            rows.append({"index": i, "op": op.name, "stream": op.stream, "start_ms": start,
+                         "end_ms": end})
+        return rows
+
     def check_health(self) -> None:
         code = self.ex.read_timeout()
         if code:

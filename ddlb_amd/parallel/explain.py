@@ -3,6 +3,8 @@
     python -m ddlb_amd.parallel.explain --primitive tp_columnwise -d 8 -m 65536 -n 1024 \
         -k 1024 --algorithm p2p_pipeline --backend ipc --rank 0
     python -m ddlb_amd.parallel.explain ... --simulate   # CPU run of all d ranks (small shapes)
+    torchrun --nproc-per-node 8 -m ddlb_amd.parallel.explain -d 8 -m 65536 -n 1024 -k 1024 \
+        --algorithm coll_pipeline --backend ipc -s 8 --timeline   # per-op GPU timeline per rank
 
 The simulation executes every rank's plan on the CPU with the race / deadlock checker
 (:mod:`ddlb_amd.parallel.sim`) — the same check the test-suite runs for every algorithm.
@@ -12,8 +14,92 @@ from __future__ import annotations
 
 import argparse
 
+from typing import Dict, List
+
 from ddlb_amd.parallel.algorithms import AlgoConfig, build_tp_columnwise, build_tp_rowwise
 from ddlb_amd.parallel.plan import NAME_DT, SIG_KERNEL, SIG_STREAM
+
+# one letter per op kind in the timeline bars
+_GLYPH = {"gemm": "G", "allgather": "A", "reduce_scatter": "R", "send": "S", "recv": "V",
+          "copy": "c", "copy_multi": "c", "reduce": "+", "signal": "!", "wait_signal": "w",
+          "wait": ".", "record": "|", "memset": "0", "group_start": "(", "group_end": ")"}
+
+
+def format_timeline(rows: List[Dict], width: int = 72) -> str:
+    """Text Gantt of :meth:`BoundPlan.timeline` rows: one bar per stream (letters = op kinds,
+    ``.`` = blocked on a dependency), then the ops sorted by start and a busy / overlap summary
+    (busy = time in GEMM / comm / copy / reduce ops, not in waits)."""
+    if not rows:
+        return "(empty plan)"
+    span = max(r["end_ms"] for r in rows) or 1e-9
+    streams = sorted({r["stream"] for r in rows})
+    lines = [f"timeline: {span * 1e3:.1f} us from fork to the last op, {len(rows)} ops"]
+    busy_kinds = {"gemm", "allgather", "reduce_scatter", "send", "recv", "copy", "copy_multi",
+                  "reduce", "memset"}
+    busy_total = 0.0
+    for st in streams:
+        bar = [" "] * width
+        busy = 0.0
+        for r in rows:
+            if r["stream"] != st:
+                continue
+            a = int(r["start_ms"] / span * (width - 1))
+            b = max(a, int(r["end_ms"] / span * (width - 1)))
+            ch = _GLYPH.get(r["op"], "?")
+            for x in range(a, b + 1):
+                if bar[x] in (" ", ".", "|") or ch not in (".", "|"):
+                    bar[x] = ch
+            if r["op"] in busy_kinds:
+                busy += r["end_ms"] - r["start_ms"]
+        busy_total += busy
+        lines.append(f"  s{st:<2d} |{''.join(bar)}| busy {busy * 1e3:8.1f} us")
+    lines.append(f"  sum of busy time over streams / span = {busy_total / span:.2f} "
+                 "(> 1: streams overlap)")
+    lines.append("  idx stream op               start_us    end_us   dur_us")
+    for r in sorted(rows, key=lambda r: (r["start_ms"], r["index"])):
+        if r["end_ms"] - r["start_ms"] < 1e-6 and r["op"] in ("record", "group_start"):
+            continue
+        lines.append(f"  {r['index']:3d} s{r['stream']:<5d} {r['op']:14s} "
+                     f"{r['start_ms'] * 1e3:9.1f} {r['end_ms'] * 1e3:9.1f} "
+                     f"{(r['end_ms'] - r['start_ms']) * 1e3:8.1f}")
+    return "\n".join(lines)
+
+
+def gpu_timeline(a) -> None:
+    """Build the native implementation for this rank (launched under torchrun for d > 1), warm
+    it up, run once with per-op timing events and print this rank's timeline."""
+    import torch
+
+    from ddlb_amd.communicator import Communicator
+    from ddlb_amd.primitives.registry import resolve
+
+    comm = Communicator()
+    comm.ensure_process_group()
+    opts = {"algorithm": a.algorithm, "backend": a.backend, "s": a.s,
+            "multicast_protocol": a.protocol, "signal": a.signal,
+            "offset_stream_indexing_by_rank": not a.no_ring, "fused": a.fused}
+    if a.primitive == "tp_columnwise":
+        opts["order"] = a.order
+    cls, opts, _ = resolve(a.primitive, "native", opts)
+    impl = cls(m=a.m, n=a.n, k=a.k, dtype=a.dtype, **opts)
+    for _ in range(5):
+        impl.run()
+    torch.cuda.synchronize()
+    comm.barrier()
+    impl.bound.set_timeline(True)
+    out = impl.run()
+    torch.cuda.synchronize()
+    rows = impl.bound.timeline()
+    impl.validate(out)
+    text = format_timeline(rows)
+    for r in range(comm.world_size):
+        if r == comm.rank:
+            print(f"[rank {comm.rank}/{comm.world_size}] {a.primitive} {a.algorithm}/{a.backend} "
+                  f"m={a.m} n={a.n} k={a.k} {a.dtype}\n{text}", flush=True)
+        comm.barrier()
+    impl.bound.set_timeline(False)
+    impl.close()
+    comm.destroy()
 
 
 def main(argv=None) -> None:
@@ -34,7 +120,13 @@ def main(argv=None) -> None:
     p.add_argument("--no-ring", action="store_true")
     p.add_argument("--fused", action="store_true")
     p.add_argument("--simulate", action="store_true")
+    p.add_argument("--timeline", action="store_true",
+                   help="run the plan on the GPU (world from the launcher's env, not -d) and "
+                        "print its per-op timeline")
     a = p.parse_args(argv)
+    if a.timeline:
+        gpu_timeline(a)
+        return
     cfg = AlgoConfig(algorithm=a.algorithm, backend=a.backend, order=a.order, s=a.s,
                      ring=not a.no_ring, protocol=a.protocol,
                      signal=SIG_STREAM if a.signal == "stream" else SIG_KERNEL, fused=a.fused)

@@ -288,3 +288,56 @@ def test_rccl_data_plane_world1(comm):
     assert ctx.rccl().async_error() == ""
     bound.close()
     ctx.close()
+
+
+def test_plan_timeline_world1(comm):
+    """Per-op GPU timeline of a hand-built two-stream plan (an RCCL all-gather and a copy on the
+    comm stream, two GEMMs on the caller's stream, one waiting on the comm stream): one entry
+    per op, ends never decrease along a stream, the GEMMs take time, the dependent GEMM starts
+    no earlier than the comm it waits on, and the results are right with the events in place."""
+    from ddlb_amd.parallel.context import NativeContext
+    from ddlb_amd.parallel.explain import format_timeline
+    from ddlb_amd.parallel.plan import DT_BF16, DT_F32, Plan
+
+    M, N, K = 8192, 1024, 1024
+    plan = Plan(0, 1, nstreams=2, stream_priority=[0, 1])
+    a = plan.buffer("a", M * K * 2)
+    bt = plan.buffer("bt", N * K * 2)
+    c0 = plan.buffer("c0", M * N * 4)
+    c1 = plan.buffer("c1", M * N * 4)
+    src = plan.buffer("src", 1 << 22)
+    ag = plan.buffer("ag", 1 << 22)
+    plan.allgather(1, src, ag, (1 << 22) // 4, DT_F32)
+    plan.copy(1, src, ag, 1 << 22)
+    e = plan.event()
+    plan.record(1, e)
+    plan.gemm(0, a, bt, c0, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, din=DT_BF16, dout=DT_F32)
+    plan.wait(0, e)
+    plan.gemm(0, a, bt, c1, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, din=DT_BF16, dout=DT_F32)
+    ctx = NativeContext(comm)
+    bound = ctx.bind(plan)
+    A = torch.randn(M, K, device="cuda").bfloat16()
+    W = torch.randn(N, K, device="cuda").bfloat16()
+    bound.buffer("a").view(torch.bfloat16).view(M, K).copy_(A)
+    bound.buffer("bt").view(torch.bfloat16).view(N, K).copy_(W)
+    bound.run()
+    bound.set_timeline(True)
+    bound.run()
+    torch.cuda.synchronize()
+    rows = bound.timeline()
+    assert len(rows) == len(plan.ops)
+    for st in {r["stream"] for r in rows}:
+        ends = [r["end_ms"] for r in rows if r["stream"] == st]
+        assert ends == sorted(ends)
+    gemms = [r for r in rows if r["op"] == "gemm"]
+    assert len(gemms) == 2 and all(r["end_ms"] - r["start_ms"] > 0.001 for r in gemms)
+    comm_end = max(r["end_ms"] for r in rows if r["stream"] == 1)
+    assert gemms[1]["end_ms"] >= comm_end
+    assert "timeline:" in format_timeline(rows)
+    ref = A.float() @ W.float().T
+    for name in ("c0", "c1"):
+        out = bound.buffer(name).view(torch.float32).view(M, N)
+        torch.testing.assert_close(out, ref, rtol=0, atol=1e-3 * K)
+    bound.set_timeline(False)
+    bound.close()
+    ctx.close()

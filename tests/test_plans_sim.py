@@ -177,3 +177,19 @@ def test_bench_candidates_simulate(d, prim, label, cfg):
         _run_col(d, m=4 * d * s, n=8, k=12, cfg=cfg, epochs=2)
     else:
         _run_row(d, m=4 * d * s, n=8, k=4 * d, cfg=cfg, epochs=2)
+
+
+def test_format_timeline_text():
+    from ddlb_amd.parallel.explain import format_timeline
+
+    rows = [{"index": 0, "op": "wait_signal", "stream": 2, "start_ms": 0.0, "end_ms": 0.01},
+            {"index": 1, "op": "copy", "stream": 2, "start_ms": 0.01, "end_ms": 0.05},
+            {"index": 2, "op": "gemm", "stream": 0, "start_ms": 0.0, "end_ms": 0.04},
+            {"index": 3, "op": "wait", "stream": 0, "start_ms": 0.04, "end_ms": 0.05},
+            {"index": 4, "op": "gemm", "stream": 0, "start_ms": 0.05, "end_ms": 0.08}]
+    text = format_timeline(rows, width=40)
+    assert "80.0 us" in text and "s0" in text and "s2" in text
+    bars = [ln for ln in text.splitlines() if ln.lstrip().startswith("s")]
+    assert "G" in bars[0] and "c" in bars[1] and "w" in bars[1]
+    ratio = float(text.split("busy time over streams / span = ")[1].split()[0])
+    assert abs(ratio - (40 + 30 + 40) / 80) < 0.01
