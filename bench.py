@@ -86,6 +86,13 @@ CANDIDATES = [
     ("coll_pipeline/ipc/kernel/s4", "native", dict(_COLL_IPC, multicast_protocol="kernel",
                                                    copy_blocks=128, tile="128x128")),
     ("coll_pipeline/ipc/memcpy/s8", "native", dict(_COLL_IPC, s=8)),
+    ("coll_pipeline/ipc/kernel/s8", "native", dict(_COLL_IPC, s=8, multicast_protocol="kernel",
+                                                   copy_blocks=128, tile="128x128")),
+    # HIP maps a process's streams onto GPU_MAX_HW_QUEUES in-order hardware queues (4 by
+    # default); the memcpy protocol uses one copy stream per peer (9 streams at d=8), so give it
+    # enough queues that no two of its streams share one (one process per GPU here)
+    ("coll_pipeline/ipc/memcpy/s8/q12", "native", dict(_COLL_IPC, s=8,
+                                                        _env={"GPU_MAX_HW_QUEUES": "12"})),
     ("p2p_pipeline/rccl", "native", dict(algorithm="p2p_pipeline", backend="rccl")),
     # the same IPC paths with kernel-side flags (system-scope atomics, spin on a CU) instead of
     # stream memops; a hedge for fabrics where the command processor's polling is slow

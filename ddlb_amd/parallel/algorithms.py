@@ -25,6 +25,14 @@ Backends: ``rccl`` = RCCL collectives / send-recv on our own communicator and HI
 ``multimem``), synchronised with cross-process flags (READY / ACK epochs).
 
 Stream map: 0 = caller/compute, 1 = RCCL comm (high priority), 2.. = one copy stream per peer.
+
+Enqueue order = intended time order. HIP multiplexes a process's streams onto a few in-order
+hardware queues (``GPU_MAX_HW_QUEUES``, 4 by default; a plan at d = 8 uses up to 9 streams), and
+two streams that share a queue run in enqueue order. The builders therefore emit ops stage by
+stage — the copies of chunk j of every peer, then the GEMM of stage j, then chunk j+1 — never all
+of one peer's chunks before the first GEMM, so a shared queue can only cost overlap, never make
+an early GEMM wait for a late transfer. The stream memops behind signal / wait are themselves
+rocclr blit kernels (``__amd_rocclr_streamOpsWrite`` / ``streamOpsWait``, profiles/r02/sig9*).
 """
 
 from __future__ import annotations
@@ -231,25 +239,35 @@ def build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, dou
         rows = ml // cfg.s
         peers = _peer_order(rank, d, cfg.ring)
         jobs = [(p, [(p * ml + j * rows, rows) for j in range(cfg.s)]) for p in peers]
-        done = _ipc_pull_shards(plan, rank, d, cfg, flags, jobs, lambda r0: arow(r0), k * ein)
-        for j in range(cfg.s):
+
+        def stage_gemm(j: int, done) -> None:  # right after chunk j of every peer is enqueued
             for p in peers:
                 plan.wait(S_MAIN, done[p][j])
             gemm(S_MAIN, arow(j * rows), crow(j * rows), d * rows, a_grp=rows, a_gstride=ml,
                  c_grp=rows, c_gstride=ml)
+
+        _ipc_pull_shards(plan, rank, d, cfg, flags, jobs, lambda r0: arow(r0), k * ein,
+                         on_block=stage_gemm)
         _wait(plan, S_MAIN, [flags.ref("ACK", p) for p in range(d) if p != rank], cfg)
     elif alg == "p2p_pipeline" and be == "ipc":
         order = _shard_order(rank, d, cfg.ring)
         peers = [p for p in order if p != rank]
+        # the own shard's GEMM needs no transfer: enqueue it before the pulls (time order)
+        own_first = (not cfg.fused) and order[0] == rank
         done = _ipc_pull_shards(plan, rank, d, cfg, flags, [(p, [(p * ml, ml)]) for p in peers],
                                 lambda r0: arow(r0), k * ein,
-                                arrive=flags.ref if cfg.fused else None)
+                                arrive=flags.ref if cfg.fused else None,
+                                after_ready=(lambda: gemm(S_MAIN, arow(rank * ml),
+                                                          crow(rank * ml), ml))
+                                if own_first else None)
         if cfg.fused:
             _signal(plan, S_MAIN, [flags.ref("ARRIVE", rank)], cfg)
             gemm(S_MAIN, A, C, m, flags=flags.ref("ARRIVE", 0), flag_rows=ml, nshards=d,
                  first_shard=order[0], tile_order=1)
         else:
             for p in order:
+                if p == rank and own_first:
+                    continue
                 if p != rank:
                     plan.wait(S_MAIN, done[p][0])
                 gemm(S_MAIN, arow(p * ml), crow(p * ml), ml)
@@ -362,21 +380,27 @@ def _col_direct(plan, rank, d, m, n, k, din, dout, ein, eout, cfg, gdt) -> Plan:
 
 
 def _ipc_pull_shards(plan: Plan, rank: int, d: int, cfg: AlgoConfig, flags: _Flags,
-                     jobs, row_ref, row_bytes: int, arrive=None):
+                     jobs, row_ref, row_bytes: int, arrive=None, on_block=None, after_ready=None):
     """Pull row blocks of the symmetric buffer from peers into the same rows locally.
 
-    ``jobs`` = [(peer, [(row0, nrows), ...]), ...] in issue order. Returns
-    ``{peer: [event after block i]}``. Protocol: READY[peer] is waited before the first read of
-    that peer; ACK is sent to the peer after the last block has landed (the peer may then
-    overwrite its shard).
+    ``jobs`` = [(peer, [(row0, nrows), ...]), ...] in issue order, the same number of blocks per
+    peer. Returns ``{peer: [event after block i]}``. Protocol: READY[peer] is waited before the
+    first read of that peer; ACK is sent to the peer after the last block has landed (the peer
+    may then overwrite its shard). Blocks are enqueued block-major (block i of every peer, then
+    ``on_block(i, done)`` — e.g. the GEMM of stage i — then block i+1; see the module docstring
+    on hardware-queue sharing); ``inter_stream_sync`` keeps the peer-major order it needs.
+    ``after_ready()`` is enqueued right after this rank's READY signal, before any pull (e.g.
+    the GEMM of the rank's own shard, which needs no transfer).
     """
     _signal(plan, S_MAIN, [flags.ref("READY", rank, owner=p) for p in range(d) if p != rank], cfg)
+    if after_ready is not None:
+        after_ready()
     done: Dict[int, List[int]] = {}
+    nblk = len(jobs[0][1])
     if cfg.protocol == "kernel":
         # one CU copy kernel per block index, reading every peer (copy_multi, <= 8 segments)
         st = _s_copy(0)
         _wait(plan, st, [flags.ref("READY", p) for p, _ in jobs], cfg)
-        nblk = len(jobs[0][1])
         for b in range(nblk):
             segs = []
             for p, blocks in jobs:
@@ -388,25 +412,53 @@ def _ipc_pull_shards(plan: Plan, rank: int, d: int, cfg: AlgoConfig, flags: _Fla
             plan.record(st, e)
             for p, _ in jobs:
                 done.setdefault(p, []).append(e)
+            if on_block is not None:
+                on_block(b, done)
         if arrive is not None:
             _signal(plan, st, [arrive("ARRIVE", p) for p, _ in jobs], cfg)
         _signal(plan, st, [flags.ref("ACK", rank, owner=p) for p, _ in jobs], cfg)
         return done
-    prev_last = None
-    for idx, (p, blocks) in enumerate(jobs):
-        st = _s_copy(0) if cfg.protocol == "batch_memcpy" else _s_copy(idx)
-        if cfg.inter_stream_sync and prev_last is not None and cfg.protocol != "batch_memcpy":
-            plan.wait(st, prev_last)
-        _wait(plan, st, [flags.ref("READY", p)], cfg)
-        for (r0, nr) in blocks:
-            plan.copy(st, row_ref(r0), row_ref(r0).at(p), nr * row_bytes, method=COPY_ENGINE)
-            e = plan.event()
-            plan.record(st, e)
-            done.setdefault(p, []).append(e)
-        prev_last = done[p][-1]
+
+    def stream_of(idx: int) -> int:
+        return _s_copy(0) if cfg.protocol == "batch_memcpy" else _s_copy(idx)
+
+    def pull(idx: int, p: int, b: int) -> None:
+        r0, nr = jobs[idx][1][b]
+        st = stream_of(idx)
+        plan.copy(st, row_ref(r0), row_ref(r0).at(p), nr * row_bytes, method=COPY_ENGINE)
+        e = plan.event()
+        plan.record(st, e)
+        done.setdefault(p, []).append(e)
+
+    def finish(idx: int, p: int) -> None:
+        st = stream_of(idx)
         if arrive is not None:
             _signal(plan, st, [arrive("ARRIVE", p)], cfg)
         _signal(plan, st, [flags.ref("ACK", rank, owner=p)], cfg)
+
+    if cfg.inter_stream_sync and cfg.protocol != "batch_memcpy":
+        prev_last = None  # peer idx starts after peer idx-1's last block: peer-major issue
+        for idx, (p, _) in enumerate(jobs):
+            if prev_last is not None:
+                plan.wait(stream_of(idx), prev_last)
+            _wait(plan, stream_of(idx), [flags.ref("READY", p)], cfg)
+            for b in range(nblk):
+                pull(idx, p, b)
+            prev_last = done[p][-1]
+            finish(idx, p)
+        if on_block is not None:
+            for b in range(nblk):
+                on_block(b, done)
+        return done
+    for idx, (p, _) in enumerate(jobs):
+        _wait(plan, stream_of(idx), [flags.ref("READY", p)], cfg)
+    for b in range(nblk):
+        for idx, (p, _) in enumerate(jobs):
+            pull(idx, p, b)
+        if on_block is not None:
+            on_block(b, done)
+    for idx, (p, _) in enumerate(jobs):
+        finish(idx, p)
     return done
 
 
