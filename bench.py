@@ -88,9 +88,9 @@ CANDIDATES = [
     ("coll_pipeline/ipc/memcpy/s8", "native", dict(_COLL_IPC, s=8)),
     ("coll_pipeline/ipc/kernel/s8", "native", dict(_COLL_IPC, s=8, multicast_protocol="kernel",
                                                    copy_blocks=128, tile="128x128")),
-    # HIP maps a process's streams onto GPU_MAX_HW_QUEUES in-order hardware queues (4 by
-    # default); the memcpy protocol uses one copy stream per peer (9 streams at d=8), so give it
-    # enough queues that no two of its streams share one (one process per GPU here)
+    # HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default); the
+    # memcpy protocol uses one copy stream per peer (9 streams at d=8): a variant where no two of
+    # its streams share a queue (one process per GPU here, so 12 queues on the device)
     ("coll_pipeline/ipc/memcpy/s8/q12", "native", dict(_COLL_IPC, s=8,
                                                         _env={"GPU_MAX_HW_QUEUES": "12"})),
     ("p2p_pipeline/rccl", "native", dict(algorithm="p2p_pipeline", backend="rccl")),

@@ -26,13 +26,15 @@ Backends: ``rccl`` = RCCL collectives / send-recv on our own communicator and HI
 
 Stream map: 0 = caller/compute, 1 = RCCL comm (high priority), 2.. = one copy stream per peer.
 
-Enqueue order = intended time order. HIP multiplexes a process's streams onto a few in-order
-hardware queues (``GPU_MAX_HW_QUEUES``, 4 by default; a plan at d = 8 uses up to 9 streams), and
-two streams that share a queue run in enqueue order. The builders therefore emit ops stage by
-stage — the copies of chunk j of every peer, then the GEMM of stage j, then chunk j+1 — never all
-of one peer's chunks before the first GEMM, so a shared queue can only cost overlap, never make
-an early GEMM wait for a late transfer. The stream memops behind signal / wait are themselves
-rocclr blit kernels (``__amd_rocclr_streamOpsWrite`` / ``streamOpsWait``, profiles/r02/sig9*).
+Enqueue order = intended time order. HIP multiplexes a process's streams onto a few hardware
+queues (``GPU_MAX_HW_QUEUES``, 4 by default; a plan at d = 8 uses up to 9 streams). Kernels of
+streams sharing a queue were measured to still overlap (profiles/r01/queue_blocking_check.txt),
+but the builders emit ops stage by stage anyway — the copies of chunk j of every peer, then the
+GEMM of stage j, then chunk j+1 — never all of one peer's chunks before the first GEMM: every
+dependency then points backwards in enqueue order, which is what a fully in-order queue needs
+(the world-4 GPU tests run with one queue per process) and what costs nothing otherwise. The
+stream memops behind signal / wait are themselves rocclr blit kernels
+(``__amd_rocclr_streamOpsWrite`` / ``streamOpsWait``, profiles/r02/sig9*).
 """
 
 from __future__ import annotations
