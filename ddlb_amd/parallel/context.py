@@ -66,6 +66,27 @@ class SymmetricBuffer:
         self.release()
 
 
+def check_single_node(world: int) -> None:
+    """HIP IPC symmetric memory (every ``backend=ipc`` plan) maps peers' HBM over xGMI, which
+    only exists between GPUs of one node: refuse a multi-node job with a clear message instead
+    of failing inside hipIpcOpenMemHandle. Hostnames are compared over the control group (no
+    reliance on launcher-specific local-size variables)."""
+    import socket
+
+    import torch.distributed as dist
+
+    if world <= 1:
+        return
+    names: List = [None] * world
+    dist.all_gather_object(names, socket.gethostname())
+    hosts = sorted(set(names))
+    if len(hosts) > 1:
+        raise RuntimeError(
+            f"backend=ipc needs every rank on one node (HIP IPC over xGMI); this job spans "
+            f"{len(hosts)} hosts ({', '.join(hosts[:4])}{', ...' if len(hosts) > 4 else ''}): "
+            "use backend=rccl")
+
+
 class NativeContext:
     def __init__(self, communicator):
         from ddlb_amd.ops import load
@@ -79,6 +100,7 @@ class NativeContext:
         self.device_index = communicator.device.index
         self._rccl = None
         self._owned: List = []
+        self._single_node_checked = False
 
     def rccl(self):
         """Our own RCCL communicator (lazily created, collective over all ranks)."""
@@ -92,6 +114,9 @@ class NativeContext:
         return self._rccl
 
     def symmetric(self, nbytes: int, uncached: bool = False) -> SymmetricBuffer:
+        if not self._single_node_checked:
+            check_single_node(self.world)
+            self._single_node_checked = True
         buf = SymmetricBuffer(self, nbytes, uncached=uncached)
         self._owned.append(buf)
         return buf

@@ -86,3 +86,44 @@ def test_ucc_backends_rejected():
     om.parse({"backend": "cuda", "multicast_protocol": "multimem"})
     cfg = algo_config(om)
     assert cfg.backend == "ipc" and cfg.protocol == "kernel"
+
+
+def _node_check_worker(rank, world, port, q, hosts):
+    import os
+    import socket
+
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from ddlb_amd.parallel.context import check_single_node
+
+    socket.gethostname = lambda: hosts[rank]  # this rank "runs" on hosts[rank]
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        check_single_node(world)
+        q.put((rank, "ok"))
+    except RuntimeError as e:
+        q.put((rank, str(e)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("hosts", [("a", "a"), ("a", "b")])
+def test_ipc_single_node_check(hosts):
+    """backend=ipc plans refuse a job that spans several hosts (HIP IPC / xGMI is per node)."""
+    import multiprocessing as mp
+
+    from conftest import free_port
+
+    ctx = mp.get_context("spawn")
+    q, port = ctx.Queue(), free_port()
+    procs = [ctx.Process(target=_node_check_worker, args=(r, 2, port, q, hosts)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    if hosts[0] == hosts[1]:
+        assert got == {0: "ok", 1: "ok"}
+    else:
+        assert all("one node" in v and "backend=rccl" in v for v in got.values()), got
