@@ -42,8 +42,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-# (label, impl, options), tried in this order; RCCL paths first (most mature transport).
-# "/blas" = the plan's plain GEMM ops on hipBLASLt (gemm_mode=blas), everything else identical.
+# (label, impl, options). "/blas" = the plan's plain GEMM ops on hipBLASLt (gemm_mode=blas),
+# everything else identical.
 def _blas(opts):
     return dict(opts, gemm_mode="blas")
 
@@ -57,46 +57,55 @@ _DEF_K = dict(algorithm="default", backend="ipc", multicast_protocol="kernel", c
 # plain GEMMs), so coll_pipeline has no "/blas" twin.
 # (The flag-gated fused p2p GEMM is left out: its spinning tiles ran 30-100x slower than the
 # unfused pipeline in every multi-rank rehearsal, profiles/r01/s2/; it stays a CLI option.)
+
+
+def _graph(opts):
+    return dict(opts, graph=True)
+
+
+# Ordered by expected strength at d = 8 (the tuning budget may cut the tail of the list).
+# "/graph": the whole plan is captured once and replayed with one hipGraphLaunch per run; the
+# IPC pipelines issue one HIP call per copy / event / signal (~2 us of host time each, ~200 calls
+# per run at d = 8, s = 8: host-bound without the graph, profiles/r02/r2_13_*).
 CANDIDATES = [
     ("coll_pipeline/rccl/s4", "native", _COLL4),
+    ("coll_pipeline/ipc/memcpy/s8/graph", "native", _graph(dict(_COLL_IPC, s=8))),
+    ("coll_pipeline/ipc/kernel/s8/graph", "native", _graph(dict(
+        _COLL_IPC, s=8, multicast_protocol="kernel", copy_blocks=128, tile="128x128"))),
     ("direct/ipc", "native", dict(algorithm="direct", backend="ipc")),
-    ("default/rccl", "native", _DEF),
-    ("default/rccl/blas", "native", _blas(_DEF)),
-    ("p2p_pipeline/ipc/memcpy", "native", _P2P),
-    ("p2p_pipeline/ipc/memcpy/blas", "native", _blas(_P2P)),
-    ("coll_pipeline/ipc/memcpy/s4", "native", _COLL_IPC),
-    ("default/ipc/kernel", "native", _DEF_K),
-    ("default/ipc/kernel/blas", "native", _blas(_DEF_K)),
-    ("p2p_pipeline/ipc/push", "native", dict(_P2P, direction="push")),
-    ("p2p_pipeline/ipc/push/blas", "native", _blas(dict(_P2P, direction="push"))),
-    ("default/ipc/push", "native", dict(_P2P, algorithm="default", direction="push")),
-    ("coll_pipeline/ipc/push/s4", "native", dict(_COLL_IPC, direction="push")),
-    ("default/ipc/kernel/push", "native", dict(_DEF_K, direction="push")),
-    ("coll_pipeline/rccl/s8", "native", dict(_COLL4, s=8)),
-    # Stage GEMMs next to CU-resident comm kernels (RCCL's, or our copy kernel): a persistent
-    # 256x256 GEMM pins one workgroup (its whole register file) per CU, so a CU held by the comm
-    # kernel delays that workgroup's tiles until the comm finishes; 128x128 tiles (4x as many,
-    # dispatched dynamically) let the busy CUs simply take fewer of them
-    ("coll_pipeline/rccl/s4/128", "native", dict(_COLL4, tile="128x128")),
-    ("coll_pipeline/rccl/s8/128", "native", dict(_COLL4, s=8, tile="128x128")),
-    # the same with RCCL held to 16 channels (16 CUs): more of the chip left to the GEMM while
-    # the gather of the next stage runs (RCCL reads the cap at communicator init)
-    ("coll_pipeline/rccl/s4/128/c16", "native", dict(_COLL4, tile="128x128",
-                                                      _env={"NCCL_MAX_NCHANNELS": "16"})),
+    ("coll_pipeline/ipc/memcpy/s4/graph", "native", _graph(_COLL_IPC)),
+    ("coll_pipeline/rccl/s8/graph", "native", _graph(dict(_COLL4, s=8))),
+    # Stage GEMMs next to CU-resident comm kernels (our copy kernel): 128x128 tiles (4x as many,
+    # dispatched dynamically) let the CUs busy with copies simply take fewer of them
     ("coll_pipeline/ipc/kernel/s4", "native", dict(_COLL_IPC, multicast_protocol="kernel",
                                                    copy_blocks=128, tile="128x128")),
-    ("coll_pipeline/ipc/memcpy/s8", "native", dict(_COLL_IPC, s=8)),
-    ("coll_pipeline/ipc/kernel/s8", "native", dict(_COLL_IPC, s=8, multicast_protocol="kernel",
-                                                   copy_blocks=128, tile="128x128")),
+    ("default/rccl", "native", _DEF),
+    ("default/rccl/blas", "native", _blas(_DEF)),
+    ("p2p_pipeline/ipc/memcpy/graph", "native", _graph(_P2P)),
     # HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default); the
     # memcpy protocol uses one copy stream per peer (9 streams at d=8): a variant where no two of
     # its streams share a queue (one process per GPU here, so 12 queues on the device)
     ("coll_pipeline/ipc/memcpy/s8/q12", "native", dict(_COLL_IPC, s=8,
                                                         _env={"GPU_MAX_HW_QUEUES": "12"})),
+    ("coll_pipeline/ipc/memcpy/s8", "native", dict(_COLL_IPC, s=8)),
+    ("default/ipc/kernel", "native", _DEF_K),
+    # the same reasoning for RCCL's CU-resident kernels, and RCCL held to 16 channels (16 CUs)
+    ("coll_pipeline/rccl/s4/128", "native", dict(_COLL4, tile="128x128")),
+    ("coll_pipeline/rccl/s8", "native", dict(_COLL4, s=8)),
+    ("coll_pipeline/rccl/s8/128", "native", dict(_COLL4, s=8, tile="128x128")),
+    ("coll_pipeline/rccl/s4/128/c16", "native", dict(_COLL4, tile="128x128",
+                                                      _env={"NCCL_MAX_NCHANNELS": "16"})),
+    ("coll_pipeline/ipc/kernel/s8", "native", dict(_COLL_IPC, s=8, multicast_protocol="kernel",
+                                                   copy_blocks=128, tile="128x128")),
+    ("coll_pipeline/ipc/memcpy/s4", "native", _COLL_IPC),
+    ("p2p_pipeline/ipc/memcpy", "native", _P2P),
+    ("p2p_pipeline/ipc/push", "native", dict(_P2P, direction="push")),
+    ("default/ipc/push", "native", dict(_P2P, algorithm="default", direction="push")),
+    ("coll_pipeline/ipc/push/s4", "native", dict(_COLL_IPC, direction="push")),
+    ("default/ipc/kernel/push", "native", dict(_DEF_K, direction="push")),
     ("p2p_pipeline/rccl", "native", dict(algorithm="p2p_pipeline", backend="rccl")),
-    # the same IPC paths with kernel-side flags (system-scope atomics, spin on a CU) instead of
-    # stream memops; a hedge for fabrics where the command processor's polling is slow
-    ("p2p_pipeline/ipc/memcpy/ksig", "native", dict(_P2P, signal="kernel")),
+    # kernel-side flags (one spin / store kernel for all flags of an op instead of one rocclr
+    # stream-memop kernel per flag)
     ("default/ipc/kernel/ksig", "native", dict(_DEF_K, signal="kernel")),
     ("pytorch(rccl+hipblaslt)", "pytorch", dict(backend="nccl", empty_cache=False)),
 ]

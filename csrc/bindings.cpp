@@ -187,5 +187,6 @@ PYBIND11_MODULE(_C, m) {
       .def("graph_enabled", &PlanExecutor::graph_enabled)
       .def("graph_capturable", &PlanExecutor::graph_capturable)
       .def("set_timeline", &PlanExecutor::set_timeline)
-      .def("timeline", &PlanExecutor::timeline);
+      .def("timeline", &PlanExecutor::timeline)
+      .def("host_times", &PlanExecutor::host_times);
 }

@@ -44,6 +44,7 @@ struct GemmArgs {
   // Arrival-ordered consumption (p2p pipeline): optional
   const unsigned* flags = nullptr;  // flags[shard] >= epoch once shard's A rows have landed
   unsigned epoch = 0;
+  const unsigned* epoch_ptr = nullptr;  // if set: the epoch is read here (hipGraph replay)
   int64_t flag_rows = 1;            // physical A rows per shard
   unsigned* timeout_word = nullptr; // set to 1 if a spin gave up
   int tile_order = 0, nshards = 1, first_shard = 0;

@@ -204,10 +204,11 @@ __device__ __forceinline__ void wait_flag(const GemmArgs& p, int64_t row_first, 
   if (p.flags == nullptr) return;
   if (threadIdx.x == 0) {
     const int s0 = (int)(row_first / p.flag_rows), s1 = (int)(row_last / p.flag_rows);
+    const unsigned want = p.epoch_ptr ? *p.epoch_ptr : p.epoch;
     for (int sh = s0; sh <= s1; ++sh) {
       unsigned* f = const_cast<unsigned*>(p.flags) + sh;
       unsigned spins = 0;
-      while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < p.epoch) {
+      while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
         __builtin_amdgcn_s_sleep(2);
         if (++spins > (1u << 26)) {  // ~seconds: give up, report, let the grid drain
           if (p.timeout_word) atomicOr(p.timeout_word, 1u);

@@ -21,21 +21,29 @@ struct CopyArgs {            // nseg independent byte copies, 16-byte aligned
   int64_t bytes[kMaxCopySeg] = {};
   int nseg = 0;
 };
+// Signal / wait values: ``value``, or — when ``epoch_ptr`` is set (hipGraph replay, where no
+// host-side value can change between replays) — ``*epoch_ptr + delta`` read on the device.
 struct SignalArgs {          // *ptr[i] = value (system-scope release), i < n
   unsigned* ptr[kMaxSignal] = {};
   unsigned value = 0;
   int n = 0;
+  const unsigned* epoch_ptr = nullptr;
+  int delta = 0;
 };
-struct WaitArgs {            // spin until *ptr[i] >= value for all i (bounded)
+struct WaitArgs {            // spin until *ptr[i] >= value for all i (bounded); value <= 0: no-op
   unsigned* ptr[kMaxSignal] = {};
   unsigned value = 0;
   int n = 0;
   unsigned* timeout_word = nullptr;
+  const unsigned* epoch_ptr = nullptr;
+  int delta = 0;
 };
 
 hipError_t reduce_sum_launch(const ReduceArgs& a, int dtype, hipStream_t s);
 hipError_t copy_launch(const CopyArgs& a, int max_blocks, hipStream_t s);
 hipError_t signal_launch(const SignalArgs& a, hipStream_t s);
 hipError_t wait_launch(const WaitArgs& a, hipStream_t s);
+// *epoch += 1 (one lane): the device-side run counter of a graph-replayed plan.
+hipError_t epoch_bump_launch(unsigned* epoch, hipStream_t s);
 
 }  // namespace ddlb

@@ -178,16 +178,20 @@ __global__ __launch_bounds__(256) void copy_kernel(CopyArgs a) {
 __global__ void signal_kernel(SignalArgs a) {
   const int i = threadIdx.x;
   if (i < a.n) {
+    const unsigned v = a.epoch_ptr ? (unsigned)((int)*a.epoch_ptr + a.delta) : a.value;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
-    __hip_atomic_store(a.ptr[i], a.value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(a.ptr[i], v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
 __global__ void wait_kernel(WaitArgs a) {
   if (threadIdx.x != 0) return;
+  const int want = a.epoch_ptr ? (int)*a.epoch_ptr + a.delta : (int)a.value;
+  if (want <= 0) return;  // nothing to wait for before the first epoch
   for (int i = 0; i < a.n; ++i) {
     unsigned spins = 0;
-    while (__hip_atomic_load(a.ptr[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.value) {
+    while (__hip_atomic_load(a.ptr[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) <
+           (unsigned)want) {
       __builtin_amdgcn_s_sleep(4);
       if (++spins > (1u << 27)) {  // bounded: report and drain instead of hanging the GPU
         if (a.timeout_word) atomicOr(a.timeout_word, 2u);
@@ -196,6 +200,10 @@ __global__ void wait_kernel(WaitArgs a) {
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
+
+__global__ void epoch_bump_kernel(unsigned* epoch) {
+  if (threadIdx.x == 0) *epoch += 1;
 }
 
 int grid_for(int64_t work_items) {
@@ -266,6 +274,11 @@ hipError_t signal_launch(const SignalArgs& a, hipStream_t s) {
 hipError_t wait_launch(const WaitArgs& a, hipStream_t s) {
   if (a.n < 1 || a.n > kMaxSignal) return hipErrorInvalidValue;
   hipLaunchKernelGGL(wait_kernel, dim3(1), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t epoch_bump_launch(unsigned* epoch, hipStream_t s) {
+  hipLaunchKernelGGL(epoch_bump_kernel, dim3(1), dim3(64), 0, s, epoch);
   return hipGetLastError();
 }
 

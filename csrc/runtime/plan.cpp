@@ -1,6 +1,7 @@
 // Plan executor implementation (see plan.h).
 #include "plan.h"
 
+#include <chrono>
 #include <stdexcept>
 
 #include "../gemm/gemm.h"
@@ -25,10 +26,14 @@ PlanExecutor::PlanExecutor(int device, int nstreams, int nevents,
     DDLB_HIP(hipStreamCreateWithPriority(&streams_[(size_t)i], hipStreamNonBlocking, p));
   }
   for (auto& e : fork_join_) DDLB_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  sync_ev_.assign((size_t)nstreams, nullptr);
+  for (auto& e : sync_ev_) DDLB_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  touched_.assign((size_t)nstreams, false);
   events_.assign((size_t)(nevents > 0 ? nevents : 0), nullptr);
   for (auto& e : events_) DDLB_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   DDLB_HIP(hipMalloc(&d_timeout_, 256));
   DDLB_HIP(hipMemset(d_timeout_, 0, 256));
+  d_epoch_ = d_timeout_ + 32;  // its own 128-byte line of the same allocation
 }
 
 PlanExecutor::~PlanExecutor() {
@@ -44,6 +49,7 @@ PlanExecutor::~PlanExecutor() {
       hipStreamDestroy(streams_[i]);
     }
   for (auto e : fork_join_) if (e) hipEventDestroy(e);
+  for (auto e : sync_ev_) if (e) hipEventDestroy(e);
   for (auto e : events_) if (e) hipEventDestroy(e);
   if (d_timeout_) hipFree(d_timeout_);
 }
@@ -75,19 +81,19 @@ void PlanExecutor::load(const std::vector<int64_t>& ops) {
 }
 
 bool PlanExecutor::graph_capturable() const {
-  for (size_t i = 0; i < ops_.size(); i += kOpWords) {
-    const int64_t k = ops_[i];
-    if (k == OP_SIGNAL || k == OP_WAIT_SIGNAL) return false;
-    if (k == OP_GEMM && ops_[i + 19] != 0) return false;
-  }
+  // Every op can be captured: in graph mode the epoch-dependent ops (cross-process signals /
+  // waits, arrival-flag GEMMs) read the run counter from device memory (d_epoch_, bumped by the
+  // first node of every replay) instead of a value baked in at enqueue time.
   return true;
 }
 
 void PlanExecutor::enable_graph(bool on) {
   if (on && timeline_on_) throw std::runtime_error("hipGraph replay: turn the plan timeline off");
-  if (on && !graph_capturable())
-    throw std::runtime_error("plan has epoch-dependent ops (signals / arrival flags): "
-                             "it cannot be replayed from a hipGraph");
+  if (on) {  // the device run counter continues from the host one (see graph_capturable)
+    DDLB_HIP(hipSetDevice(device_));
+    DDLB_HIP(hipDeviceSynchronize());
+    DDLB_HIP(hipMemcpy(d_epoch_, &epoch_, sizeof(unsigned), hipMemcpyHostToDevice));
+  }
   graph_on_ = on;
   if (on && cap_stream_ == nullptr) {
     DDLB_HIP(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking));
@@ -125,17 +131,40 @@ std::vector<float> PlanExecutor::timeline() {
   return out;
 }
 
+void PlanExecutor::join_others(int64_t stream, hipStream_t main) {
+  hipStream_t s = S(stream, main);
+  for (size_t j = 0; j < streams_.size(); ++j) {
+    if ((int64_t)j == stream || !touched_[j]) continue;
+    DDLB_HIP(hipEventRecord(sync_ev_[j], S((int64_t)j, main)));
+    DDLB_HIP(hipStreamWaitEvent(s, sync_ev_[j], 0));
+  }
+}
+
 void PlanExecutor::enqueue(hipStream_t main) {
+  std::fill(touched_.begin(), touched_.end(), false);
   if (timeline_on_) DDLB_HIP(hipEventRecord(tl_start_, main));
+  if (graph_on_) DDLB_HIP(epoch_bump_launch(d_epoch_, main));  // first node of every replay
   if (any_side_) {
     // fork: every used side stream waits for everything already queued on `main`
     DDLB_HIP(hipEventRecord(fork_join_[0], main));
     for (size_t i = 1; i < streams_.size(); ++i)
       if (used_[i]) DDLB_HIP(hipStreamWaitEvent(streams_[i], fork_join_[0], 0));
   }
+  if (timeline_on_) host_us_.assign(ops_.size() / kOpWords, 0.f);
   for (size_t i = 0; i < ops_.size(); i += kOpWords) {
+    const int64_t* o = &ops_[i];
+    if (graph_on_ && (o[0] == OP_WAIT_SIGNAL || (o[0] == OP_GEMM && o[19] != 0)))
+      join_others(o[1], main);
+    touched_[(size_t)o[1]] = true;
+    if (!timeline_on_) {
+      exec(&ops_[i], main);
+      continue;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
     exec(&ops_[i], main);
-    if (timeline_on_) DDLB_HIP(hipEventRecord(tl_ops_[i / kOpWords], S(ops_[i + 1], main)));
+    const auto t1 = std::chrono::steady_clock::now();
+    host_us_[i / kOpWords] = std::chrono::duration<float, std::micro>(t1 - t0).count();
+    DDLB_HIP(hipEventRecord(tl_ops_[i / kOpWords], S(ops_[i + 1], main)));
   }
   if (any_side_) {  // join
     for (size_t i = 1; i < streams_.size(); ++i)
@@ -190,6 +219,7 @@ GemmArgs PlanExecutor::gemm_args(const int64_t* o) const {
   g.a_table = (const uint64_t*)o[25];
   g.shard_rows = o[26];
   g.timeout_word = d_timeout_;
+  g.epoch_ptr = graph_on_ ? d_epoch_ : nullptr;
   return g;
 }
 
@@ -272,12 +302,16 @@ void PlanExecutor::exec(const int64_t* o, hipStream_t main) {
       const int n = (int)o[2];
       if (n < 1 || n > kMaxSignal || 5 + n > kOpWords) throw std::runtime_error("plan: bad signal");
       const unsigned value = (unsigned)((int64_t)epoch_ + o[4]);
-      if (o[3] == 1) {
+      if (o[3] == 1 && !graph_on_) {
         for (int i = 0; i < n; ++i) DDLB_HIP(hipStreamWriteValue32(s, (void*)o[5 + i], value, 0));
       } else {
-        SignalArgs a;
+        SignalArgs a;  // graph mode: always the kernel, reading the device run counter
         a.n = n;
         a.value = value;
+        if (graph_on_) {
+          a.epoch_ptr = d_epoch_;
+          a.delta = (int)o[4];
+        }
         for (int i = 0; i < n; ++i) a.ptr[i] = (unsigned*)o[5 + i];
         DDLB_HIP(signal_launch(a, s));
       }
@@ -287,16 +321,20 @@ void PlanExecutor::exec(const int64_t* o, hipStream_t main) {
       const int n = (int)o[2];
       if (n < 1 || n > kMaxSignal || 5 + n > kOpWords) throw std::runtime_error("plan: bad wait");
       const int64_t v = (int64_t)epoch_ + o[4];
-      if (v <= 0) return;  // nothing to wait for before the first epoch
-      if (o[3] == 1) {
+      if (v <= 0 && !graph_on_) return;  // nothing to wait for before the first epoch
+      if (o[3] == 1 && !graph_on_) {
         for (int i = 0; i < n; ++i)
           DDLB_HIP(hipStreamWaitValue32(s, (void*)o[5 + i], (unsigned)v, hipStreamWaitValueGte,
                                         0xffffffffu));
       } else {
         WaitArgs a;
         a.n = n;
-        a.value = (unsigned)v;
+        a.value = v > 0 ? (unsigned)v : 0u;
         a.timeout_word = d_timeout_;
+        if (graph_on_) {
+          a.epoch_ptr = d_epoch_;
+          a.delta = (int)o[4];
+        }
         for (int i = 0; i < n; ++i) a.ptr[i] = (unsigned*)o[5 + i];
         DDLB_HIP(wait_launch(a, s));
       }

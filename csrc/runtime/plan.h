@@ -63,8 +63,8 @@ class PlanExecutor {
   unsigned read_timeout();  // synchronous; 0 = healthy
   uintptr_t stream(int i) const { return (uintptr_t)streams_.at(i); }
   // hipGraph mode: the plan is captured once (on a private stream) and replayed with one
-  // hipGraphLaunch behind the caller's stream. Only for plans without epoch-dependent ops
-  // (cross-process signals / arrival-flag GEMMs read the epoch at enqueue time).
+  // hipGraphLaunch behind the caller's stream (host cost of a run: one launch instead of one
+  // HIP / RCCL call per op). Epoch-dependent ops read a device-side run counter in this mode.
   void enable_graph(bool on);
   bool graph_enabled() const { return graph_on_; }
   bool graph_capturable() const;
@@ -74,6 +74,8 @@ class PlanExecutor {
   // stream (ops with nothing to enqueue report their stream's previous end). Not with graphs.
   void set_timeline(bool on);
   std::vector<float> timeline();
+  // Host-side cost of enqueueing each op in the last run (us), recorded while the timeline is on.
+  std::vector<float> host_times() const { return host_us_; }
 
  private:
   void exec(const int64_t* op, hipStream_t main);
@@ -93,12 +95,20 @@ class PlanExecutor {
   std::vector<hipEvent_t> fork_join_;  // one per stream
   std::vector<int64_t> ops_;
   std::vector<bool> used_;             // stream i touched by the plan
+  // graph mode: before a cross-process wait (or a flag-gated GEMM) join the tails of every other
+  // stream that already has ops, so ANY execution order of the captured graph keeps all ops
+  // enqueued before the wait ahead of it (what makes the plan deadlock-free in one queue)
+  std::vector<hipEvent_t> sync_ev_;
+  std::vector<bool> touched_;
+  void join_others(int64_t stream, hipStream_t main);
   RcclComm* comm_ = nullptr;
   bool timeline_on_ = false;
   hipEvent_t tl_start_ = nullptr;
   std::vector<hipEvent_t> tl_ops_;
+  std::vector<float> host_us_;
   unsigned epoch_ = 0;
   unsigned* d_timeout_ = nullptr;
+  unsigned* d_epoch_ = nullptr;  // device copy of epoch_ (graph mode), inside d_timeout_'s block
 };
 
 }  // namespace ddlb

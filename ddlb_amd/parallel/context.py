@@ -11,11 +11,21 @@
 
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional
 
 from ddlb_amd.parallel.plan import (OP_ALLGATHER, OP_RECV, OP_REDUCE_SCATTER, OP_SEND, DT_SIZE,
                                     Plan, Ref)
 from ddlb_amd.parallel.sim import TORCH_DT
+
+
+def graph_replay_supported() -> bool:
+    """hipGraph replay segfaulted in this image's HIP runtime with GPU_MAX_HW_QUEUES = 1 or 2
+    (a 9-stream plan replays fine with the default 4; profiles/r02/r2_17_*)."""
+    try:
+        return int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) >= 4
+    except ValueError:
+        return True
 
 
 def _raw_stream(device_index: int) -> int:
@@ -217,7 +227,13 @@ class BoundPlan:
         return raw[loc.off:loc.off + n].view(TORCH_DT[loc.dtype]).view(loc.rows, loc.cols)
 
     def enable_graph(self, on: bool = True) -> None:
-        """Replay the whole plan from one captured hipGraph (plans without signals only)."""
+        """Replay the whole plan from one captured hipGraph: one launch per run instead of one
+        HIP / RCCL call per op (signal plans read a device-side run counter in this mode)."""
+        if on and not graph_replay_supported():
+            raise RuntimeError(
+                "hipGraph replay needs at least 4 hardware queues per process: with "
+                f"GPU_MAX_HW_QUEUES={os.environ.get('GPU_MAX_HW_QUEUES')} the HIP runtime of this "
+                "image crashes in hipGraphLaunch (profiles/r02/r2_17_*)")
         self.ex.enable_graph(on)
 
     def run(self, stream: Optional[int] = None) -> int:
@@ -235,6 +251,7 @@ class BoundPlan:
         start is the end of the previous op on the same stream, so waits show up as the time an
         op spent blocked behind its dependencies."""
         ends = self.ex.timeline()
+        host = self.ex.host_times()
         last: Dict[int, float] = {}
         rows = []
         for i, (op, end) in enumerate(zip(self.plan.ops, ends)):
@@ -242,7 +259,7 @@ class BoundPlan:
             end = max(float(end), start)
             last[op.stream] = end
             rows.append({"index": i, "op": op.name, "stream": op.stream, "start_ms": start,
-                         "end_ms": end})
+                         "end_ms": end, "host_us": float(host[i]) if i < len(host) else 0.0})
         return rows
 
     def check_health(self) -> None:

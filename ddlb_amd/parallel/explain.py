@@ -55,6 +55,13 @@ def format_timeline(rows: List[Dict], width: int = 72) -> str:
         lines.append(f"  s{st:<2d} |{''.join(bar)}| busy {busy * 1e3:8.1f} us")
     lines.append(f"  sum of busy time over streams / span = {busy_total / span:.2f} "
                  "(> 1: streams overlap)")
+    if any("host_us" in r for r in rows):
+        per_kind: Dict[str, float] = {}
+        for r in rows:
+            per_kind[r["op"]] = per_kind.get(r["op"], 0.0) + r.get("host_us", 0.0)
+        total = sum(per_kind.values())
+        top = ", ".join(f"{k} {v:.0f}" for k, v in sorted(per_kind.items(), key=lambda x: -x[1])[:6])
+        lines.append(f"  host enqueue {total:.0f} us: {top}")
     lines.append("  idx stream op               start_us    end_us   dur_us")
     for r in sorted(rows, key=lambda r: (r["start_ms"], r["index"])):
         if r["end_ms"] - r["start_ms"] < 1e-6 and r["op"] in ("record", "group_start"):
@@ -80,12 +87,36 @@ def gpu_timeline(a) -> None:
             "offset_stream_indexing_by_rank": not a.no_ring, "fused": a.fused}
     if a.primitive == "tp_columnwise":
         opts["order"] = a.order
+    if a.graph:
+        opts["graph"] = True
     cls, opts, _ = resolve(a.primitive, "native", opts)
     impl = cls(m=a.m, n=a.n, k=a.k, dtype=a.dtype, **opts)
     for _ in range(5):
         impl.run()
     torch.cuda.synchronize()
     comm.barrier()
+    # host cost of enqueueing one run (every HIP / RCCL call of the plan), GPU kept busy
+    import time
+
+    host = []
+    for _ in range(20):
+        t0 = time.perf_counter()
+        impl.run()
+        host.append((time.perf_counter() - t0) * 1e6)
+    torch.cuda.synchronize()
+    comm.barrier()
+    host.sort()
+    if a.graph:  # one hipGraphLaunch per run: no per-op timeline inside a replayed graph
+        out = impl.run()
+        torch.cuda.synchronize()
+        impl.validate(out)
+        if comm.rank == 0:
+            print(f"[rank 0/{comm.world_size}] {a.primitive} {a.algorithm}/{a.backend} graph "
+                  f"replay: {len(impl.plan.ops)} plan ops, host enqueue per run "
+                  f"{host[len(host) // 2]:.0f} us (median of 20)", flush=True)
+        impl.close()
+        comm.destroy()
+        return
     impl.bound.set_timeline(True)
     out = impl.run()
     torch.cuda.synchronize()
@@ -95,7 +126,9 @@ def gpu_timeline(a) -> None:
     for r in range(comm.world_size):
         if r == comm.rank:
             print(f"[rank {comm.rank}/{comm.world_size}] {a.primitive} {a.algorithm}/{a.backend} "
-                  f"m={a.m} n={a.n} k={a.k} {a.dtype}\n{text}", flush=True)
+                  f"m={a.m} n={a.n} k={a.k} {a.dtype}: {len(impl.plan.ops)} plan ops, host "
+                  f"enqueue per run {host[len(host) // 2]:.0f} us (median of 20)\n{text}",
+                  flush=True)
         comm.barrier()
     impl.bound.set_timeline(False)
     impl.close()
@@ -116,10 +149,14 @@ def main(argv=None) -> None:
     p.add_argument("--order", default="AG_before")
     p.add_argument("-s", type=int, default=2)
     p.add_argument("--protocol", default="memcpy")
-    p.add_argument("--signal", default="stream", choices=["stream", "kernel"])
+    p.add_argument("--signal", "--signal-method", dest="signal", default="stream",
+                   choices=["stream", "kernel"])  # (torchrun's parser claims "--signal...")
     p.add_argument("--no-ring", action="store_true")
     p.add_argument("--fused", action="store_true")
     p.add_argument("--simulate", action="store_true")
+    p.add_argument("--graph", action="store_true",
+                   help="with --timeline: capture the plan in a hipGraph and report the host "
+                        "cost of a replayed run instead of the per-op timeline")
     p.add_argument("--timeline", action="store_true",
                    help="run the plan on the GPU (world from the launcher's env, not -d) and "
                         "print its per-op timeline")

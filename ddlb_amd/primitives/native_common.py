@@ -111,7 +111,9 @@ def maybe_enable_graph(bound, option) -> bool:
     if option is True or option == "true":
         bound.enable_graph(True)
         return True
-    if option == "auto" and bound.ex.graph_capturable():
+    from ddlb_amd.parallel.context import graph_replay_supported
+
+    if option == "auto" and bound.ex.graph_capturable() and graph_replay_supported():
         bound.enable_graph(True)
         return True
     return False

@@ -22,7 +22,12 @@ def main():
     comm.ensure_process_group()
     cfgs = json.loads(os.environ["DDLB_TEST_CFGS"])
     res = {}
+    only = os.environ.get("DDLB_TEST_ONLY", "")
     for label, prim, opts in cfgs:
+        if only and only not in label:
+            continue
+        if os.environ.get("DDLB_TEST_PROGRESS"):
+            print(f"[rank {comm.rank}] {label}", file=sys.stderr, flush=True)
         try:
             cls = NativeTPColumnwise if prim == "col" else NativeTPRowwise
             impl = cls(m=opts.pop("m", 1536), n=512, k=768, dtype=opts.pop("dtype", "bfloat16"),

@@ -136,6 +136,20 @@ def _ipc_cfgs():
             cfgs.append((f"col/{alg}/ipc/push/{proto}", "col",
                          dict(algorithm=alg, backend="ipc", multicast_protocol=proto, s=2,
                               direction="push")))
+    # hipGraph replay of signal plans (device-side run counter for the epoch values)
+    for label, prim, opts in (
+            ("col/coll/memcpy/graph", "col", dict(algorithm="coll_pipeline", s=2)),
+            ("col/coll/kernel/graph", "col", dict(algorithm="coll_pipeline", s=2,
+                                                  multicast_protocol="kernel")),
+            ("col/p2p/memcpy/graph", "col", dict(algorithm="p2p_pipeline")),
+            ("col/p2p/fused/graph", "col", dict(algorithm="p2p_pipeline", fused=True)),
+            ("col/direct/graph", "col", dict(algorithm="direct")),
+            ("col/coll/push/graph", "col", dict(algorithm="coll_pipeline", s=2, direction="push")),
+            ("row/default/kernel/graph", "row", dict(algorithm="default",
+                                                     multicast_protocol="kernel")),
+            ("row/coll/graph", "row", dict(algorithm="coll_pipeline", s=2)),
+            ("row/p2p/graph", "row", dict(algorithm="p2p_pipeline"))):
+        cfgs.append((label, prim, dict(opts, backend="ipc", graph=True)))
     for alg in ("default", "coll_pipeline", "p2p_pipeline"):  # bench.py's "/blas" candidates
         cfgs.append((f"col/{alg}/ipc/blas", "col", dict(algorithm=alg, backend="ipc", s=2,
                                                         gemm_mode="blas")))
@@ -155,7 +169,8 @@ def test_ipc_shared_gpu(world):
         # d=4 protocols testable here. The flag-gated fused GEMM spins tiles of every co-resident
         # process and is covered at world 2-3.
         extra["GPU_MAX_HW_QUEUES"] = "1"
-        cfgs = [c for c in cfgs if not c[2].get("fused")]
+        # (hipGraph replay needs >= 4 HW queues in this HIP runtime: graph configs run at 2-3)
+        cfgs = [c for c in cfgs if not c[2].get("fused") and not c[2].get("graph")]
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world),
@@ -206,7 +221,10 @@ def test_graph_replay_world1(comm, prim):
     impl.close()
 
 
-def test_graph_refused_for_signal_plans():
+def test_signal_plans_are_graph_capturable():
+    """Cross-process signal / wait plans can be captured: in graph mode their epoch-dependent
+    values come from a device-side run counter (the replay itself is exercised by the IPC
+    configurations with graph=True in test_ipc_shared_gpu)."""
     from ddlb_amd.parallel.algorithms import AlgoConfig, build_tp_columnwise
     from ddlb_amd.parallel.plan import DT_BF16
     from ddlb_amd.ops import load
@@ -216,9 +234,11 @@ def test_graph_refused_for_signal_plans():
                                   AlgoConfig(algorithm="p2p_pipeline", backend="ipc"))
     ex = C.PlanExecutor(0, plan.nstreams, max(plan.nevents, 1), list(plan.stream_priority))
     ex.load(plan.encode(lambda ref: 4096))
-    assert not ex.graph_capturable()
+    assert ex.graph_capturable()
+    ex.enable_graph(True)
+    assert ex.graph_enabled()
     with pytest.raises(RuntimeError):
-        ex.enable_graph(True)
+        ex.set_timeline(True)  # per-op events are not available inside a replayed graph
 
 
 @pytest.mark.parametrize("nseg,max_blocks", [(1, 64), (3, 64), (7, 128), (8, 5), (5, 0)])
