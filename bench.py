@@ -127,6 +127,10 @@ ROW_CANDIDATES = [
     ("row/default/ipc/kernel/blas", "native", _blas(dict(_RK, algorithm="default"))),
     ("row/coll_pipeline/ipc/kernel/s4", "native", dict(_RK, algorithm="coll_pipeline", s=4)),
     ("row/p2p_pipeline/ipc/memcpy", "native", dict(algorithm="p2p_pipeline", backend="ipc")),
+    ("row/coll_pipeline/ipc/kernel/s4/graph", "native", _graph(dict(_RK, algorithm="coll_pipeline",
+                                                                    s=4))),
+    ("row/p2p_pipeline/ipc/memcpy/graph", "native", _graph(dict(algorithm="p2p_pipeline",
+                                                                 backend="ipc"))),
     ("row/pytorch(rccl+hipblaslt)", "pytorch", dict(backend="nccl", empty_cache=False)),
 ]
 ROW_WORLD1 = [
