@@ -74,7 +74,6 @@ CANDIDATES = [
         _COLL_IPC, s=8, multicast_protocol="kernel", copy_blocks=128, tile="128x128"))),
     ("direct/ipc", "native", dict(algorithm="direct", backend="ipc")),
     ("coll_pipeline/ipc/memcpy/s4/graph", "native", _graph(_COLL_IPC)),
-    ("coll_pipeline/rccl/s8/graph", "native", _graph(dict(_COLL4, s=8))),
     # Stage GEMMs next to CU-resident comm kernels (our copy kernel): 128x128 tiles (4x as many,
     # dispatched dynamically) let the CUs busy with copies simply take fewer of them
     ("coll_pipeline/ipc/kernel/s4", "native", dict(_COLL_IPC, multicast_protocol="kernel",

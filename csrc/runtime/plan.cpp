@@ -81,14 +81,25 @@ void PlanExecutor::load(const std::vector<int64_t>& ops) {
 }
 
 bool PlanExecutor::graph_capturable() const {
-  // Every op can be captured: in graph mode the epoch-dependent ops (cross-process signals /
-  // waits, arrival-flag GEMMs) read the run counter from device memory (d_epoch_, bumped by the
-  // first node of every replay) instead of a value baked in at enqueue time.
+  // In graph mode the epoch-dependent ops (cross-process signals / waits, arrival-flag GEMMs)
+  // read the run counter from device memory (d_epoch_, bumped by the first node of every
+  // replay) instead of a value baked in at enqueue time, so they capture. RCCL calls do not:
+  // replaying a captured RCCL collective crashed the process on this image (torch's RCCL 2.26,
+  // profiles/r02/r2_19*); RCCL plans issue few calls per run anyway.
+  for (size_t i = 0; i < ops_.size(); i += kOpWords) {
+    const int64_t k = ops_[i];
+    if (k == OP_ALLGATHER || k == OP_REDUCE_SCATTER || k == OP_SEND || k == OP_RECV ||
+        k == OP_GROUP_START || k == OP_GROUP_END)
+      return false;
+  }
   return true;
 }
 
 void PlanExecutor::enable_graph(bool on) {
   if (on && timeline_on_) throw std::runtime_error("hipGraph replay: turn the plan timeline off");
+  if (on && !graph_capturable())
+    throw std::runtime_error("hipGraph replay: plans with RCCL calls are not captured (see "
+                             "graph_capturable)");
   if (on) {  // the device run counter continues from the host one (see graph_capturable)
     DDLB_HIP(hipSetDevice(device_));
     DDLB_HIP(hipDeviceSynchronize());
