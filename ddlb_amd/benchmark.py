@@ -197,6 +197,14 @@ def _gpu_arch(comm) -> str:
         return "unknown"
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
 def _benchmark_worker_entry(result_queue, init_method: str, kwargs: Dict[str, Any]) -> None:
     """Spawned child: fresh HIP context, own process group, one row back to the parent."""
     os.environ["DDLB_CHILD_INIT_METHOD"] = init_method
@@ -259,10 +267,32 @@ class PrimitiveBenchmarkRunner:
                     profile_iterations=self.profile_iterations,
                     validate_every_iteration=self.validate_every_iteration)
 
+    _store = None  # parent-level TCPStore (world > 1): rank 0 publishes each child's port
+
     def _next_init_method(self) -> str:
+        """Rendezvous of the next child process group. Rank 0 binds a currently free port and,
+        when there are several ranks, publishes it through a small TCPStore the parent
+        processes share (created once at the base port; no GPU involved), so every rank's
+        child dials the same, actually free port (a fixed port sequence collided with ephemeral
+        ports of earlier children's sockets: EADDRINUSE)."""
         idx = PrimitiveBenchmarkRunner._child_counter
         PrimitiveBenchmarkRunner._child_counter += 1
-        port = get_master_port() + 1 + (idx % 997)
+        rank, world = get_rank(), get_world_size()
+        port = _free_port() if rank == 0 else 0
+        if world > 1:
+            import datetime
+
+            from torch.distributed import TCPStore
+
+            if PrimitiveBenchmarkRunner._store is None:
+                PrimitiveBenchmarkRunner._store = TCPStore(
+                    get_master_addr(), get_master_port(), world, rank == 0,
+                    timeout=datetime.timedelta(seconds=self.child_timeout_s))
+            key = f"ddlb_child_port_{idx}"
+            if rank == 0:
+                PrimitiveBenchmarkRunner._store.set(key, str(port))
+            else:
+                port = int(PrimitiveBenchmarkRunner._store.get(key).decode())
         return f"tcp://{get_master_addr()}:{port}"
 
     def _done_keys(self) -> set:
