@@ -65,6 +65,7 @@ class AlgoConfig:
     tile: int = 0                       # GEMM tile (0 = auto)
     mode: int = 0                       # GEMM mode (0 auto, 2 MX-fp8)
     copy_blocks: int = 64               # CU budget of the kernel copy protocol
+    copy_streams: int = 1               # memcpy pulls: copy streams (copy engines) per peer
     fused: bool = False                 # p2p columnwise: one flag-gated GEMM launch
     act: int = 0                        # columnwise: fused GEMM epilogue activation (ACT_*)
     direction: str = "pull"             # columnwise ipc: pull peers' shards | push mine to peers
@@ -86,8 +87,8 @@ class PlanIO:
     out: TensorLoc
 
 
-def _nstreams(d: int) -> int:
-    return 2 + max(d - 1, 1)
+def _nstreams(d: int, per_peer: int = 1) -> int:
+    return 2 + max(d - 1, 1) * max(per_peer, 1)
 
 
 def _peer_order(rank: int, d: int, ring: bool) -> List[int]:
@@ -172,7 +173,8 @@ def build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, dou
     check_columnwise(d, m, n, k, cfg)
     ein, eout = DT_SIZE[din], DT_SIZE[dout]
     ml = m // d
-    plan = Plan(rank, d, nstreams=_nstreams(d), stream_priority=[0, 1] + [1] * max(d - 1, 1))
+    ns = _nstreams(d, cfg.copy_streams)
+    plan = Plan(rank, d, nstreams=ns, stream_priority=[0, 1] + [1] * (ns - 2))
     plan.meta.update(primitive="tp_columnwise", algorithm=cfg.algorithm, backend=cfg.backend,
                      order=cfg.order)
     Bt = plan.buffer("Bt", n * k * ein)
@@ -421,13 +423,27 @@ def _ipc_pull_shards(plan: Plan, rank: int, d: int, cfg: AlgoConfig, flags: _Fla
         _signal(plan, st, [flags.ref("ACK", rank, owner=p) for p, _ in jobs], cfg)
         return done
 
-    def stream_of(idx: int) -> int:
-        return _s_copy(0) if cfg.protocol == "batch_memcpy" else _s_copy(idx)
+    split = max(cfg.copy_streams, 1) if cfg.protocol == "memcpy" else 1
+
+    def stream_of(idx: int, part: int = 0) -> int:
+        return _s_copy(0) if cfg.protocol == "batch_memcpy" else _s_copy(idx * split + part)
 
     def pull(idx: int, p: int, b: int) -> None:
+        """Block b of peer p; with copy_streams > 1 its rows are split over that many streams
+        (one copy engine each) and joined on the peer's first stream."""
         r0, nr = jobs[idx][1][b]
         st = stream_of(idx)
-        plan.copy(st, row_ref(r0), row_ref(r0).at(p), nr * row_bytes, method=COPY_ENGINE)
+        if split > 1:
+            cuts = [r0 + (nr * j) // split for j in range(split + 1)]
+            for j in range(split):  # every part's copy first, then the join on part 0
+                a0, a1 = cuts[j], cuts[j + 1]
+                if a1 > a0:
+                    plan.copy(stream_of(idx, j), row_ref(a0), row_ref(a0).at(p),
+                              (a1 - a0) * row_bytes, method=COPY_ENGINE)
+            for j in range(1, split):
+                plan.edge(stream_of(idx, j), st)
+        else:
+            plan.copy(st, row_ref(r0), row_ref(r0).at(p), nr * row_bytes, method=COPY_ENGINE)
         e = plan.event()
         plan.record(st, e)
         done.setdefault(p, []).append(e)
@@ -453,7 +469,8 @@ def _ipc_pull_shards(plan: Plan, rank: int, d: int, cfg: AlgoConfig, flags: _Fla
                 on_block(b, done)
         return done
     for idx, (p, _) in enumerate(jobs):
-        _wait(plan, stream_of(idx), [flags.ref("READY", p)], cfg)
+        for part in range(split):
+            _wait(plan, stream_of(idx, part), [flags.ref("READY", p)], cfg)
     for b in range(nblk):
         for idx, (p, _) in enumerate(jobs):
             pull(idx, p, b)

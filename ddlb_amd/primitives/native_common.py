@@ -22,9 +22,11 @@ inter_stream_synchronization       serialise the per-peer transfers
 Native-only: ``signal`` (``stream`` = hipStreamWrite/WaitValue32 memops, ``kernel`` = tiny spin
 kernels), ``tile`` (GEMM tile or ``auto``), ``gemm_mode`` (``auto`` | ``mx`` for block-scaled fp8 |
 ``blas`` = hipBLASLt for the plain GEMM ops of the plan, fused ones stay on the MFMA kernels),
-``copy_blocks`` (CU budget of the kernel protocol), ``fused`` (p2p: one arrival-flag-gated GEMM),
-``graph`` (capture the plan once and replay it as one hipGraph launch; ``auto`` = whenever the
-plan has no cross-process signals), ``direction`` (columnwise ipc: ``pull`` peers' shards, or
+``copy_blocks`` (CU budget of the kernel protocol), ``copy_streams`` (memcpy pulls: copy streams,
+i.e. copy engines, per peer — a hedge for links faster than one engine), ``fused`` (p2p: one
+arrival-flag-gated GEMM), ``graph`` (capture the plan once and replay it as one hipGraph launch;
+signal plans read a device-side run counter; not for plans with RCCL calls; ``auto`` = whenever
+capturable and the process has >= 4 HW queues), ``direction`` (columnwise ipc: ``pull`` peers' shards, or
 ``push`` my shard into every peer's gather buffer with posted xGMI writes).
 """
 
@@ -45,6 +47,7 @@ COMMON_DEFAULTS = {
     "tile": "auto",
     "gemm_mode": "auto",
     "copy_blocks": 64,
+    "copy_streams": 1,
     "fused": False,
     "graph": False,
     "direction": "pull",
@@ -62,6 +65,7 @@ COMMON_ALLOWED = {
              "t8", "pt8", "t4", "pt4"],
     "gemm_mode": ["auto", "mx", "generic", "blas"],
     "copy_blocks": (1, 4096),
+    "copy_streams": (1, 4),
     "fused": [True, False],
     "graph": [True, False, "auto"],
     "direction": ["pull", "push"],
@@ -95,6 +99,7 @@ def algo_config(options, order: str = "AG_before") -> AlgoConfig:
         signal=SIG_STREAM if options["signal"] == "stream" else SIG_KERNEL,
         tile=TILE_CODE[options["tile"]], mode=MODE_CODE[options["gemm_mode"]],
         copy_blocks=int(options["copy_blocks"]), fused=bool(options["fused"]),
+        copy_streams=int(options.get("copy_streams", 1)),
         direction=options.get("direction", "pull"))
 
 

@@ -193,3 +193,14 @@ def test_format_timeline_text():
     assert "G" in bars[0] and "c" in bars[1] and "w" in bars[1]
     ratio = float(text.split("busy time over streams / span = ")[1].split()[0])
     assert abs(ratio - (40 + 30 + 40) / 80) < 0.01
+
+
+@pytest.mark.parametrize("d", [2, 3, 4])
+@pytest.mark.parametrize("alg", ["default", "coll_pipeline", "p2p_pipeline"])
+@pytest.mark.parametrize("streams", [2, 3])
+def test_columnwise_copy_streams(d, alg, streams):
+    """memcpy pulls split over several copy streams (engines) per peer, joined per block."""
+    cfg = AlgoConfig(algorithm=alg, backend="ipc", s=2, copy_streams=streams)
+    plan, _ = build_tp_columnwise(0, d, 16 * d, 8, 12, DT_F32, DT_F32, cfg)
+    assert plan.nstreams == 2 + (d - 1) * streams
+    _run_col(d, m=16 * d, n=8, k=12, cfg=cfg)
