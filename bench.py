@@ -75,9 +75,9 @@ CANDIDATES = [
     ("direct/ipc", "native", dict(algorithm="direct", backend="ipc")),
     ("coll_pipeline/ipc/memcpy/s4/graph", "native", _graph(_COLL_IPC)),
     # each peer's chunks split over 2 copy streams (2 copy engines per link): a hedge for links
-    # faster than one engine, which is what bounds the few-GPU runs (one link per peer)
-    ("coll_pipeline/ipc/memcpy/s8/cs2/graph", "native", _graph(dict(_COLL_IPC, s=8,
-                                                                    copy_streams=2))),
+    # faster than one engine, which is what bounds the few-GPU runs (one link per peer); not
+    # graph-captured (hipGraph replay of split copies segfaulted, profiles/r02/r2_22_*)
+    ("coll_pipeline/ipc/memcpy/s8/cs2", "native", dict(_COLL_IPC, s=8, copy_streams=2)),
     # Stage GEMMs next to CU-resident comm kernels (our copy kernel): 128x128 tiles (4x as many,
     # dispatched dynamically) let the CUs busy with copies simply take fewer of them
     ("coll_pipeline/ipc/kernel/s4", "native", dict(_COLL_IPC, multicast_protocol="kernel",
@@ -85,7 +85,7 @@ CANDIDATES = [
     ("default/rccl", "native", _DEF),
     ("default/rccl/blas", "native", _blas(_DEF)),
     ("p2p_pipeline/ipc/memcpy/graph", "native", _graph(_P2P)),
-    ("p2p_pipeline/ipc/memcpy/cs2/graph", "native", _graph(dict(_P2P, copy_streams=2))),
+    ("p2p_pipeline/ipc/memcpy/cs2", "native", dict(_P2P, copy_streams=2)),
     # HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default); the
     # memcpy protocol uses one copy stream per peer (9 streams at d=8): a variant where no two of
     # its streams share a queue (one process per GPU here, so 12 queues on the device)

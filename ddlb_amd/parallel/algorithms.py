@@ -176,7 +176,7 @@ def build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, dou
     ns = _nstreams(d, cfg.copy_streams)
     plan = Plan(rank, d, nstreams=ns, stream_priority=[0, 1] + [1] * (ns - 2))
     plan.meta.update(primitive="tp_columnwise", algorithm=cfg.algorithm, backend=cfg.backend,
-                     order=cfg.order)
+                     order=cfg.order, copy_streams=cfg.copy_streams if cfg.protocol == "memcpy" else 1)
     Bt = plan.buffer("Bt", n * k * ein)
     A = (plan.buffer("A_full", m * k * ein, symmetric=(cfg.backend == "ipc"))
          if cfg.algorithm != "direct" else None)

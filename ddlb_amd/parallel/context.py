@@ -234,6 +234,11 @@ class BoundPlan:
                 "hipGraph replay needs at least 4 hardware queues per process: with "
                 f"GPU_MAX_HW_QUEUES={os.environ.get('GPU_MAX_HW_QUEUES')} the HIP runtime of this "
                 "image crashes in hipGraphLaunch (profiles/r02/r2_17_*)")
+        if on and self.plan.meta.get("copy_streams", 1) > 1:
+            raise RuntimeError(
+                "hipGraph replay: plans with copy_streams > 1 (one peer's pulls split over several "
+                "copy streams) segfaulted in this HIP runtime (profiles/r02/r2_22_cs2_graph.txt); "
+                "use graph=False")
         self.ex.enable_graph(on)
 
     def run(self, stream: Optional[int] = None) -> int:

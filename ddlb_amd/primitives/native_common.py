@@ -118,7 +118,8 @@ def maybe_enable_graph(bound, option) -> bool:
         return True
     from ddlb_amd.parallel.context import graph_replay_supported
 
-    if option == "auto" and bound.ex.graph_capturable() and graph_replay_supported():
+    if (option == "auto" and bound.ex.graph_capturable() and graph_replay_supported()
+            and bound.plan.meta.get("copy_streams", 1) <= 1):
         bound.enable_graph(True)
         return True
     return False

@@ -153,9 +153,6 @@ def _ipc_cfgs():
     for alg in ("default", "coll_pipeline", "p2p_pipeline"):  # pulls split over 2 copy streams
         cfgs.append((f"col/{alg}/memcpy/cs2", "col", dict(algorithm=alg, backend="ipc", s=2,
                                                           copy_streams=2)))
-    cfgs.append(("col/coll/memcpy/cs2/graph", "col", dict(algorithm="coll_pipeline",
-                                                          backend="ipc", s=2, copy_streams=2,
-                                                          graph=True)))
     for alg in ("default", "coll_pipeline", "p2p_pipeline"):  # bench.py's "/blas" candidates
         cfgs.append((f"col/{alg}/ipc/blas", "col", dict(algorithm=alg, backend="ipc", s=2,
                                                         gemm_mode="blas")))
