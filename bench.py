@@ -55,8 +55,12 @@ _COLL_IPC = dict(algorithm="coll_pipeline", backend="ipc", multicast_protocol="m
 _DEF_K = dict(algorithm="default", backend="ipc", multicast_protocol="kernel", copy_blocks=128)
 # Pipeline stages use grouped-row GEMMs, which stay on the MFMA kernels (hipBLASLt only takes
 # plain GEMMs), so coll_pipeline has no "/blas" twin.
-# (The flag-gated fused p2p GEMM is left out: its spinning tiles ran 30-100x slower than the
-# unfused pipeline in every multi-rank rehearsal, profiles/r01/s2/; it stays a CLI option.)
+# Flag-gated ("fused") GEMMs: ONE GEMM launch whose tiles spin until their rows have landed.
+# With ranks sharing one GPU (the only multi-rank rehearsal available here) the spinning tiles of
+# one rank hold the CUs the other needs and ran 30-100x slower (profiles/r01/s2/); on a real node
+# each rank owns its GPU and the copy engines fill the flags without any CU, so the block-major
+# fused coll_pipeline (no per-stage GEMM tails, one launch) stays in the pool. The whole-shard
+# p2p form stays a CLI option (a tile waits for its entire 1/d shard).
 
 
 def _graph(opts):
@@ -72,7 +76,10 @@ CANDIDATES = [
     ("coll_pipeline/ipc/memcpy/s8/graph", "native", _graph(dict(_COLL_IPC, s=8))),
     ("coll_pipeline/ipc/kernel/s8/graph", "native", _graph(dict(
         _COLL_IPC, s=8, multicast_protocol="kernel", copy_blocks=128, tile="128x128"))),
+    ("coll_pipeline/ipc/memcpy/s8/fused/graph", "native", _graph(dict(_COLL_IPC, s=8,
+                                                                      fused=True))),
     ("direct/ipc", "native", dict(algorithm="direct", backend="ipc")),
+    ("coll_pipeline/ipc/memcpy/s4/fused/graph", "native", _graph(dict(_COLL_IPC, fused=True))),
     ("coll_pipeline/ipc/memcpy/s4/graph", "native", _graph(_COLL_IPC)),
     # each peer's chunks split over 2 copy streams (2 copy engines per link): a hedge for links
     # faster than one engine, which is what bounds the few-GPU runs (one link per peer); not
@@ -92,6 +99,7 @@ CANDIDATES = [
     ("coll_pipeline/ipc/memcpy/s8/q12", "native", dict(_COLL_IPC, s=8,
                                                         _env={"GPU_MAX_HW_QUEUES": "12"})),
     ("coll_pipeline/ipc/memcpy/s8", "native", dict(_COLL_IPC, s=8)),
+    ("coll_pipeline/ipc/memcpy/s8/fused", "native", dict(_COLL_IPC, s=8, fused=True)),
     ("default/ipc/kernel", "native", _DEF_K),
     # the same reasoning for RCCL's CU-resident kernels, and RCCL held to 16 channels (16 CUs)
     ("coll_pipeline/rccl/s4/128", "native", dict(_COLL4, tile="128x128")),

@@ -48,6 +48,10 @@ struct GemmArgs {
   int64_t flag_rows = 1;            // physical A rows per shard
   unsigned* timeout_word = nullptr; // set to 1 if a spin gave up
   int tile_order = 0, nshards = 1, first_shard = 0;
+  // Row blocks per producer (tile_order): shard index = producer * nsub + block; dispatch is
+  // block-major across producers (block 0 of every producer, own first, then block 1, ...),
+  // i.e. the order chunked pulls from all peers arrive in. nsub = 1: plain shard order.
+  int nsub = 1;
   int act = 0;                      // fused epilogue activation: ACT_* below
   // Direct-access A (optional): row block s of shard_rows rows starts at a_table[s] (device
   // array of addresses, e.g. the peers' IPC-mapped shards read straight over xGMI).

@@ -51,22 +51,24 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 }
 
 // Block -> tile. Default: bijective XCD remap over the whole grid. With ``tile_order`` the grid
-// is dispatched shard-major (shard (first_shard + j) % nshards at dispatch position j, so the
-// tiles of the shard that arrives first run first) and XCD-remapped within each shard.
+// is dispatched shard-major (ordered_shard: the shard that arrives first runs first; with nsub > 1
+// row blocks of all producers interleave block-major) and XCD-remapped within each shard.
+__device__ __forceinline__ int tile_index_virtual(const GemmArgs& p, int vid, int nwg);
+// Dispatch position j -> shard: producers rotate fastest (own first), blocks slowest.
+__device__ __forceinline__ int ordered_shard(const GemmArgs& p, int j) {
+  const int np = p.nshards / p.nsub;
+  return ((p.first_shard + j % np) % np) * p.nsub + j / np;
+}
+
 __device__ __forceinline__ int tile_index(const GemmArgs& p, int nwg) {
-  if (!p.tile_order) return xcd_remap((int)blockIdx.x, nwg);
-  const int per = nwg / p.nshards;
-  const int j = (int)blockIdx.x / per, local = (int)blockIdx.x % per;
-  const int shard = (p.first_shard + j) % p.nshards;
-  return shard * per + xcd_remap(local, per);
+  return tile_index_virtual(p, (int)blockIdx.x, nwg);
 }
 
 __device__ __forceinline__ int tile_index_virtual(const GemmArgs& p, int vid, int nwg) {
   if (!p.tile_order) return xcd_remap(vid, nwg);
   const int per = nwg / p.nshards;
   const int j = vid / per, local = vid % per;
-  const int shard = (p.first_shard + j) % p.nshards;
-  return shard * per + xcd_remap(local, per);
+  return ordered_shard(p, j) * per + xcd_remap(local, per);
 }
 
 // Tile id -> (tm, tn). Row-major, except that without a shard order and with more than 4 column

@@ -112,7 +112,8 @@ hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mo
   if (p.tile_order && !fast) p.tile_order = 0;
   if (fast) {
     if (tile == TILE_AUTO) tile = choose_tile(p.M, p.N, p.K, din);
-    if (p.tile_order && (p.nshards <= 0 || p.M % p.nshards != 0 ||
+    if (p.nsub < 1) p.nsub = 1;
+    if (p.tile_order && (p.nshards <= 0 || p.M % p.nshards != 0 || p.nshards % p.nsub != 0 ||
                          (p.M / p.nshards) % tile_rows(tile) != 0))
       p.tile_order = 0;
     hipError_t e = hipErrorInvalidValue;

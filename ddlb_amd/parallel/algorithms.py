@@ -113,7 +113,7 @@ class _Flags:
         self.slots: Dict[str, Tuple[int, int]] = {}
         self.words = 0
         for name, count in (("READY", d), ("ACK", d), ("CHUNK", s * d), ("ACKS", s * d),
-                            ("ARRIVE", d)):
+                            ("ARRIVE", s * d)):  # ARRIVE[p * s + b]: block b of shard p landed
             self.slots[name] = (self.words, count)
             self.words += count
         nbytes = max(256, ((self.words * 4 + 255) // 256) * 256)
@@ -164,6 +164,10 @@ def check_columnwise(d: int, m: int, n: int, k: int, cfg: AlgoConfig) -> None:
                                     cfg.algorithm == "direct" or cfg.fused):
         raise ValueError("direction=push applies to backend=ipc, order=AG_before, "
                          "default / coll_pipeline / p2p_pipeline (not fused)")
+    if cfg.fused and (cfg.backend != "ipc" or cfg.order != "AG_before" or
+                      cfg.algorithm not in ("p2p_pipeline", "coll_pipeline")):
+        raise ValueError("fused=True (one arrival-flag-gated GEMM) applies to backend=ipc, "
+                         "order=AG_before, p2p_pipeline / coll_pipeline")
     if d > 17:
         raise ValueError("at most 17 ranks per node are supported by the flag/reduce ops")
 
@@ -239,6 +243,21 @@ def build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, dou
             plan.record(S_COMM, e)
             plan.wait(S_MAIN, e)
             gemm(S_MAIN, stg, crow(j * rows), d * rows, c_grp=rows, c_gstride=ml)
+    elif alg == "coll_pipeline" and be == "ipc" and cfg.fused:
+        # ONE flag-gated GEMM over all m rows instead of s stage GEMMs: tiles are dispatched
+        # block-major (block 0 of the own shard and of every peer, then block 1, ...), the order
+        # the chunked pulls land in, and each tile spins until its row block's ARRIVE flag is set
+        # by the copy stream that pulled it; no stage boundaries, no per-stage GEMM tail.
+        rows = ml // cfg.s
+        peers = _peer_order(rank, d, cfg.ring)
+        jobs = [(p, [(p * ml + j * rows, rows) for j in range(cfg.s)]) for p in peers]
+        _ipc_pull_shards(plan, rank, d, cfg, flags, jobs, lambda r0: arow(r0), k * ein,
+                         arrive_block=lambda p, b: flags.ref("ARRIVE", p * cfg.s + b))
+        # enqueued after the pulls (every dependency points backwards in enqueue order)
+        _signal(plan, S_MAIN, [flags.ref("ARRIVE", rank * cfg.s + j) for j in range(cfg.s)], cfg)
+        gemm(S_MAIN, A, C, m, flags=flags.ref("ARRIVE", 0), flag_rows=rows, nshards=d * cfg.s,
+             nsub=cfg.s, first_shard=rank, tile_order=1)
+        _wait(plan, S_MAIN, [flags.ref("ACK", p) for p in range(d) if p != rank], cfg)
     elif alg == "coll_pipeline" and be == "ipc":
         rows = ml // cfg.s
         peers = _peer_order(rank, d, cfg.ring)
@@ -384,7 +403,8 @@ def _col_direct(plan, rank, d, m, n, k, din, dout, ein, eout, cfg, gdt) -> Plan:
 
 
 def _ipc_pull_shards(plan: Plan, rank: int, d: int, cfg: AlgoConfig, flags: _Flags,
-                     jobs, row_ref, row_bytes: int, arrive=None, on_block=None, after_ready=None):
+                     jobs, row_ref, row_bytes: int, arrive=None, on_block=None, after_ready=None,
+                     arrive_block=None):
     """Pull row blocks of the symmetric buffer from peers into the same rows locally.
 
     ``jobs`` = [(peer, [(row0, nrows), ...]), ...] in issue order, the same number of blocks per
@@ -394,7 +414,8 @@ def _ipc_pull_shards(plan: Plan, rank: int, d: int, cfg: AlgoConfig, flags: _Fla
     ``on_block(i, done)`` — e.g. the GEMM of stage i — then block i+1; see the module docstring
     on hardware-queue sharing); ``inter_stream_sync`` keeps the peer-major order it needs.
     ``after_ready()`` is enqueued right after this rank's READY signal, before any pull (e.g.
-    the GEMM of the rank's own shard, which needs no transfer).
+    the GEMM of the rank's own shard, which needs no transfer). ``arrive(name, p)`` is signalled
+    after the last block of peer p, ``arrive_block(p, b)`` (a local flag) after each block.
     """
     _signal(plan, S_MAIN, [flags.ref("READY", rank, owner=p) for p in range(d) if p != rank], cfg)
     if after_ready is not None:
@@ -412,6 +433,10 @@ def _ipc_pull_shards(plan: Plan, rank: int, d: int, cfg: AlgoConfig, flags: _Fla
                 segs.append((row_ref(r0), row_ref(r0).at(p), nr * row_bytes))
             for i in range(0, len(segs), 8):
                 plan.copy_multi(st, segs[i:i + 8], max_blocks=cfg.copy_blocks)
+            if arrive_block is not None:
+                _signal(plan, st, [arrive_block(p, b) for p, _ in jobs], cfg)
+            if arrive_block is not None:
+                _signal(plan, st, [arrive_block(p, b) for p, _ in jobs], cfg)
             e = plan.event()
             plan.record(st, e)
             for p, _ in jobs:
@@ -444,6 +469,8 @@ def _ipc_pull_shards(plan: Plan, rank: int, d: int, cfg: AlgoConfig, flags: _Fla
                 plan.edge(stream_of(idx, j), st)
         else:
             plan.copy(st, row_ref(r0), row_ref(r0).at(p), nr * row_bytes, method=COPY_ENGINE)
+        if arrive_block is not None:
+            _signal(plan, st, [arrive_block(p, b)], cfg)
         e = plan.event()
         plan.record(st, e)
         done.setdefault(p, []).append(e)
@@ -603,6 +630,21 @@ def build_tp_rowwise(rank: int, d: int, m: int, n: int, k: int, din: int, dout: 
             gemm(S_MAIN, j * rows, stg, d * rows, a_grp=rows, a_gstride=ml)
             plan.edge(S_MAIN, S_COMM)
             plan.reduce_scatter(S_COMM, stg, OUT + j * rows * n * eout, rows * n, dout)
+    elif alg == "coll_pipeline" and be == "ipc" and cfg.fused:
+        # ONE flag-gated GEMM over all m rows instead of s stage GEMMs: tiles are dispatched
+        # block-major (block 0 of the own shard and of every peer, then block 1, ...), the order
+        # the chunked pulls land in, and each tile spins until its row block's ARRIVE flag is set
+        # by the copy stream that pulled it; no stage boundaries, no per-stage GEMM tail.
+        rows = ml // cfg.s
+        peers = _peer_order(rank, d, cfg.ring)
+        jobs = [(p, [(p * ml + j * rows, rows) for j in range(cfg.s)]) for p in peers]
+        _ipc_pull_shards(plan, rank, d, cfg, flags, jobs, lambda r0: arow(r0), k * ein,
+                         arrive_block=lambda p, b: flags.ref("ARRIVE", p * cfg.s + b))
+        # enqueued after the pulls (every dependency points backwards in enqueue order)
+        _signal(plan, S_MAIN, [flags.ref("ARRIVE", rank * cfg.s + j) for j in range(cfg.s)], cfg)
+        gemm(S_MAIN, A, C, m, flags=flags.ref("ARRIVE", 0), flag_rows=rows, nshards=d * cfg.s,
+             nsub=cfg.s, first_shard=rank, tile_order=1)
+        _wait(plan, S_MAIN, [flags.ref("ACK", p) for p in range(d) if p != rank], cfg)
     elif alg == "coll_pipeline" and be == "ipc":
         rows = ml // cfg.s
         sblk = rows * n * eout

@@ -122,6 +122,15 @@ def _ipc_cfgs():
     cfgs.append(("col/p2p/fused/misaligned256", "col", dict(algorithm="p2p_pipeline",
                                                             backend="ipc", fused=True, m=1920,
                                                             tile="256x256")))
+    # coll_pipeline fused: one GEMM, tiles gated per (peer, block) and dispatched block-major
+    cfgs.append(("col/coll/fused", "col", dict(algorithm="coll_pipeline", backend="ipc", s=2,
+                                               fused=True)))
+    cfgs.append(("col/coll/fused/ksig/batch", "col", dict(algorithm="coll_pipeline",
+                                                          backend="ipc", s=2, fused=True,
+                                                          signal="kernel",
+                                                          multicast_protocol="batch_memcpy")))
+    cfgs.append(("col/coll/fused/256", "col", dict(algorithm="coll_pipeline", backend="ipc",
+                                                   s=2, fused=True, tile="256x256")))
     cfgs.append(("col/p2p/noring", "col", dict(algorithm="p2p_pipeline", backend="ipc",
                                                offset_stream_indexing_by_rank=False)))
     cfgs.append(("col/p2p/fp8", "col", dict(algorithm="p2p_pipeline", backend="ipc",
@@ -143,6 +152,7 @@ def _ipc_cfgs():
                                                   multicast_protocol="kernel")),
             ("col/p2p/memcpy/graph", "col", dict(algorithm="p2p_pipeline")),
             ("col/p2p/fused/graph", "col", dict(algorithm="p2p_pipeline", fused=True)),
+            ("col/coll/fused/graph", "col", dict(algorithm="coll_pipeline", s=2, fused=True)),
             ("col/direct/graph", "col", dict(algorithm="direct")),
             ("col/coll/push/graph", "col", dict(algorithm="coll_pipeline", s=2, direction="push")),
             ("row/default/kernel/graph", "row", dict(algorithm="default",

@@ -7,7 +7,7 @@ import pytest
 import torch
 
 from ddlb_amd.parallel.algorithms import AlgoConfig, build_tp_columnwise, build_tp_rowwise
-from ddlb_amd.parallel.plan import DT_BF16, DT_F32, SIG_KERNEL, SIG_STREAM
+from ddlb_amd.parallel.plan import DT_BF16, DT_F32, OP_GEMM, SIG_KERNEL, SIG_STREAM
 from ddlb_amd.parallel.sim import Simulator, make_buffers, read_tensor, write_tensor
 
 ALGS = ["default", "coll_pipeline", "p2p_pipeline"]
@@ -113,6 +113,29 @@ def test_push_rejected_where_meaningless():
 def test_p2p_fused_plan(fused):
     cfg = AlgoConfig(algorithm="p2p_pipeline", backend="ipc", fused=fused)
     _run_col(4, m=32, n=8, k=8, cfg=cfg)
+
+
+@pytest.mark.parametrize("d", [2, 3, 4])
+@pytest.mark.parametrize("sig", [SIG_STREAM, SIG_KERNEL])
+@pytest.mark.parametrize("protocol", ["memcpy", "batch_memcpy"])
+def test_coll_fused_plan(d, sig, protocol):
+    """coll_pipeline fused: one flag-gated GEMM, ARRIVE per (peer, block), block-major order."""
+    cfg = AlgoConfig(algorithm="coll_pipeline", backend="ipc", fused=True, s=3, signal=sig,
+                     protocol=protocol)
+    _run_col(d, m=6 * d, n=8, k=8, cfg=cfg, epochs=3)
+    plan, _ = build_tp_columnwise(1, d, 6 * d, 8, 8, DT_F32, DT_F32, cfg)
+    g = [op for op in plan.ops if op.kind == OP_GEMM]
+    assert len(g) == 1 and g[0].args["nshards"] == 3 * d and g[0].args["nsub"] == 3
+    assert g[0].args["flag_rows"] == 2 and g[0].args["first_shard"] == 1
+
+
+def test_fused_rejected_where_meaningless():
+    for cfg in (AlgoConfig(algorithm="default", backend="ipc", fused=True),
+                AlgoConfig(algorithm="coll_pipeline", backend="rccl", fused=True),
+                AlgoConfig(algorithm="p2p_pipeline", backend="ipc", order="AG_after",
+                           fused=True)):
+        with pytest.raises(ValueError):
+            build_tp_columnwise(0, 2, 16, 8, 8, DT_F32, DT_F32, cfg)
 
 
 @pytest.mark.parametrize("d", [1, 2, 3, 4])
