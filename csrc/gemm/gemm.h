@@ -52,6 +52,7 @@ struct GemmArgs {
   // block-major across producers (block 0 of every producer, own first, then block 1, ...),
   // i.e. the order chunked pulls from all peers arrive in. nsub = 1: plain shard order.
   int nsub = 1;
+  int reserve_cus = 0;              // flag-gated persistent GEMMs: CUs left free (see launch_pt4)
   int act = 0;                      // fused epilogue activation: ACT_* below
   // Direct-access A (optional): row block s of shard_rows rows starts at a_table[s] (device
   // array of addresses, e.g. the peers' IPC-mapped shards read straight over xGMI).

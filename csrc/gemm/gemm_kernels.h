@@ -202,8 +202,9 @@ template <int OUT> constexpr int out_size() { return OUT == DT_F32 ? 4 : 2; }
 // m/d = 320 rows with 128- or 256-row tiles): wait for EVERY shard in that range, not only the
 // first row's. The acquire is at system scope: the rows were written by a copy engine or by a
 // peer GPU over xGMI, not by this agent.
-__device__ __forceinline__ void wait_flag(const GemmArgs& p, int64_t row_first, int64_t row_last) {
-  if (p.flags == nullptr) return;
+// Thread 0 spins and acquires; the caller orders the other threads after it with a barrier.
+__device__ __forceinline__ void wait_flag_t0(const GemmArgs& p, int64_t row_first,
+                                             int64_t row_last) {
   if (threadIdx.x == 0) {
     const int s0 = (int)(row_first / p.flag_rows), s1 = (int)(row_last / p.flag_rows);
     const unsigned want = p.epoch_ptr ? *p.epoch_ptr : p.epoch;
@@ -220,6 +221,11 @@ __device__ __forceinline__ void wait_flag(const GemmArgs& p, int64_t row_first, 
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
   }
+}
+
+__device__ __forceinline__ void wait_flag(const GemmArgs& p, int64_t row_first, int64_t row_last) {
+  if (p.flags == nullptr) return;
+  wait_flag_t0(p, row_first, row_last);
   __syncthreads();
 }
 
@@ -1381,7 +1387,9 @@ __global__ __launch_bounds__(512) void gemm_tn_t4_kernel(const GemmArgs p) {
 // a tile's panels plus wave-uniform panel bases, so switching tiles costs two scalar pointers and
 // the kernel stays within 256 VGPRs. Plain A rows only (no shard table / grouped A / flags: t4).
 // Measured (scripts/lab, profiles/r01/s2/lab/t8_vs_ring2.txt): flagship 0.1127 vs t4 0.1160 ms.
-template <class Mma, int OUT>
+// GATED: the arrival-flag form (a separate instantiation, so the ungated kernel's code and
+// schedule are exactly those measured without flags).
+template <class Mma, int OUT, bool GATED>
 __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   constexpr int ROWB = 128, UNIT = 128 * ROWB, STAGE = 4 * UNIT;
   constexpr int UA0 = 0, UA1 = UNIT, UB0 = 2 * UNIT, UB1 = 3 * UNIT;
@@ -1530,6 +1538,11 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   } while (0)
 #define T4_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
   const bool g1 = wr == 1;  // wave-uniform (wave came through readfirstlane)
+  if constexpr (GATED) {  // arrival gate of the first tile, before any staging
+    int64_t m0, n0;
+    origin(0, m0, n0);
+    wait_flag(p, m0, m0 + 255);
+  }
   Cur q0{0, 0}, q1{0, 0};
   adv(q1);
   stage(2, UB0, q0, 0);
@@ -1548,6 +1561,17 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     constexpr int KIND = decltype(kind_tag)::value;
     const int b = h & 1;
     const char* cur = smem + b * STAGE;
+    if (GATED && qa.kt == 0) {
+      // Arrival gate: this iteration stages the first A K-tile of tile qa.ti. Thread 0 spins on
+      // the flags of its rows and acquires; one extra barrier, executed by every wave at this
+      // same point (qa is workgroup-uniform), orders all waves' A staging after it. Both wave
+      // groups insert it at the same place, so their one-barrier stagger is unchanged; an extra
+      // barrier only adds ordering (LDS RAW / WAR distances grow).
+      int64_t m0, n0;
+      origin(qa.ti, m0, n0);
+      wait_flag_t0(p, m0, m0 + 255);
+      T4_BAR();
+    }
     loadB(cur, 0);  // phase A
     loadB(cur, 1);
     loadA(cur, 0);
@@ -2077,7 +2101,7 @@ hipError_t launch_t4(const GemmArgs& p, hipStream_t s) {
 // pt4 needs >= 2 K-tiles per tile (its FIRST and LAST K-tile kinds are distinct), plain A rows
 // and 32-bit panel offsets
 bool pt4_ok(const GemmArgs& p, int esz) {
-  return p.M % 256 == 0 && p.N % 256 == 0 && p.flags == nullptr && p.a_table == nullptr &&
+  return p.M % 256 == 0 && p.N % 256 == 0 && p.a_table == nullptr &&
          p.a_grp == p.M && (int64_t)p.K * esz / 128 >= 2 && p.lda * esz <= (1 << 22) &&
          p.ldb * esz <= (1 << 22);
 }
@@ -2086,10 +2110,17 @@ template <class Mma, int OUT>
 hipError_t launch_pt4(const GemmArgs& p, hipStream_t s) {
   const int tiles = (p.M / 256) * (p.N / 256);
   int grid = num_cus();
+  // Flag-gated: leave reserve_cus CUs free. A pt4 workgroup takes a CU's whole register file, so
+  // with every CU holding a (spinning) tile, the copy / signal kernels that set the flags could
+  // not be scheduled; the reserve keeps the gate deadlock-free whoever moves the data.
+  if (p.flags != nullptr && p.reserve_cus > 0) grid -= p.reserve_cus;
   grid = (grid / 8) * 8;  // blockIdx % 8 == XCD group for every virtual tile id
   if (grid > tiles) grid = tiles;
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT>), dim3(grid), dim3(512), 0, s, p);
+  if (p.flags != nullptr)
+    hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, true>), dim3(grid), dim3(512), 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false>), dim3(grid), dim3(512), 0, s, p);
   return hipGetLastError();
 }
 

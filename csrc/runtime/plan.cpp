@@ -227,6 +227,7 @@ GemmArgs PlanExecutor::gemm_args(const int64_t* o) const {
   g.first_shard = (int)o[22];
   g.tile_order = (int)o[23];
   g.nsub = o[27] > 0 ? (int)o[27] : 1;
+  g.reserve_cus = (int)o[28];
   g.act = (int)o[24];
   g.a_table = (const uint64_t*)o[25];
   g.shard_rows = o[26];

@@ -66,7 +66,8 @@ class AlgoConfig:
     mode: int = 0                       # GEMM mode (0 auto, 2 MX-fp8)
     copy_blocks: int = 64               # CU budget of the kernel copy protocol
     copy_streams: int = 1               # memcpy pulls: copy streams (copy engines) per peer
-    fused: bool = False                 # p2p columnwise: one flag-gated GEMM launch
+    fused: bool = False                 # columnwise p2p / coll: one flag-gated GEMM launch
+    reserve_cus: int = 32               # fused: CUs the persistent gated GEMM leaves free
     act: int = 0                        # columnwise: fused GEMM epilogue activation (ACT_*)
     direction: str = "pull"             # columnwise ipc: pull peers' shards | push mine to peers
 
@@ -256,7 +257,7 @@ def build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, dou
         # enqueued after the pulls (every dependency points backwards in enqueue order)
         _signal(plan, S_MAIN, [flags.ref("ARRIVE", rank * cfg.s + j) for j in range(cfg.s)], cfg)
         gemm(S_MAIN, A, C, m, flags=flags.ref("ARRIVE", 0), flag_rows=rows, nshards=d * cfg.s,
-             nsub=cfg.s, first_shard=rank, tile_order=1)
+             nsub=cfg.s, first_shard=rank, tile_order=1, reserve_cus=cfg.reserve_cus)
         _wait(plan, S_MAIN, [flags.ref("ACK", p) for p in range(d) if p != rank], cfg)
     elif alg == "coll_pipeline" and be == "ipc":
         rows = ml // cfg.s
@@ -286,7 +287,7 @@ def build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, dou
         if cfg.fused:
             _signal(plan, S_MAIN, [flags.ref("ARRIVE", rank)], cfg)
             gemm(S_MAIN, A, C, m, flags=flags.ref("ARRIVE", 0), flag_rows=ml, nshards=d,
-                 first_shard=order[0], tile_order=1)
+                 first_shard=order[0], tile_order=1, reserve_cus=cfg.reserve_cus)
         else:
             for p in order:
                 if p == rank and own_first:
@@ -643,7 +644,7 @@ def build_tp_rowwise(rank: int, d: int, m: int, n: int, k: int, din: int, dout: 
         # enqueued after the pulls (every dependency points backwards in enqueue order)
         _signal(plan, S_MAIN, [flags.ref("ARRIVE", rank * cfg.s + j) for j in range(cfg.s)], cfg)
         gemm(S_MAIN, A, C, m, flags=flags.ref("ARRIVE", 0), flag_rows=rows, nshards=d * cfg.s,
-             nsub=cfg.s, first_shard=rank, tile_order=1)
+             nsub=cfg.s, first_shard=rank, tile_order=1, reserve_cus=cfg.reserve_cus)
         _wait(plan, S_MAIN, [flags.ref("ACK", p) for p in range(d) if p != rank], cfg)
     elif alg == "coll_pipeline" and be == "ipc":
         rows = ml // cfg.s

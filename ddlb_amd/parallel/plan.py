@@ -120,14 +120,15 @@ class Plan:
              flags: Optional[Ref] = None, flag_rows: int = 0, nshards: int = 1,
              first_shard: int = 0, tile_order: int = 0, act: int = 0,
              a_shards: Optional[Sequence[Ref]] = None, shard_rows: int = 0,
-             nsub: int = 1) -> Op:
+             nsub: int = 1, reserve_cus: int = 0) -> Op:
         """``a_shards``: A row block s (``shard_rows`` rows each) is read from ``a_shards[s]``
         (a peer's copy for a direct-access GEMM that pulls its operand over xGMI).
         ``flags`` (arrival-gated tiles): shard ``i`` = rows ``[i*flag_rows, (i+1)*flag_rows)`` may
         be read once ``flags[i]`` reaches the run's epoch; with ``tile_order`` the tiles are
         dispatched shard by shard from ``first_shard`` — ``nsub`` > 1 splits each producer's
         shard into that many row blocks (shard = producer * nsub + block) dispatched block-major
-        (block 0 of every producer first), the order chunked pulls land in."""
+        (block 0 of every producer first), the order chunked pulls land in. A persistent
+        flag-gated GEMM leaves ``reserve_cus`` CUs free for the kernels that set the flags."""
         if nsub < 1 or nshards % nsub:
             raise ValueError(f"nsub ({nsub}) must divide nshards ({nshards})")
         a_table = None
@@ -141,7 +142,8 @@ class Plan:
                          flag_rows=flag_rows, nshards=nshards, first_shard=first_shard,
                          tile_order=tile_order, act=act,
                          a_shards=list(a_shards) if a_shards is not None else None,
-                         shard_rows=shard_rows, a_table=a_table, nsub=nsub)
+                         shard_rows=shard_rows, a_table=a_table, nsub=nsub,
+                         reserve_cus=reserve_cus)
 
     def table(self, name: str, refs: Sequence[Ref]) -> Ref:
         """Device array of 64-bit addresses of ``refs`` (written once when the plan is bound)."""
@@ -229,7 +231,7 @@ class Plan:
                             a.get("act", 0)]
                 if a.get("a_table") is not None:
                     w[25], w[26] = resolve(a["a_table"]), a["shard_rows"]
-                w[27] = a.get("nsub", 1)
+                w[27], w[28] = a.get("nsub", 1), a.get("reserve_cus", 0)
             elif k in (OP_RECORD, OP_WAIT):
                 w[2] = a["event"]
             elif k in (OP_ALLGATHER, OP_REDUCE_SCATTER):

@@ -23,8 +23,9 @@ Native-only: ``signal`` (``stream`` = hipStreamWrite/WaitValue32 memops, ``kerne
 kernels), ``tile`` (GEMM tile or ``auto``), ``gemm_mode`` (``auto`` | ``mx`` for block-scaled fp8 |
 ``blas`` = hipBLASLt for the plain GEMM ops of the plan, fused ones stay on the MFMA kernels),
 ``copy_blocks`` (CU budget of the kernel protocol), ``copy_streams`` (memcpy pulls: copy streams,
-i.e. copy engines, per peer — a hedge for links faster than one engine), ``fused`` (p2p: one
-arrival-flag-gated GEMM), ``graph`` (capture the plan once and replay it as one hipGraph launch;
+i.e. copy engines, per peer — a hedge for links faster than one engine), ``fused`` (p2p / coll: one
+arrival-flag-gated GEMM; ``reserve_cus`` = CUs its persistent form leaves free for the
+kernels that set the flags), ``graph`` (capture the plan once and replay it as one hipGraph launch;
 signal plans read a device-side run counter; not for plans with RCCL calls; ``auto`` = whenever
 capturable and the process has >= 4 HW queues), ``direction`` (columnwise ipc: ``pull`` peers' shards, or
 ``push`` my shard into every peer's gather buffer with posted xGMI writes).
@@ -49,6 +50,7 @@ COMMON_DEFAULTS = {
     "copy_blocks": 64,
     "copy_streams": 1,
     "fused": False,
+    "reserve_cus": 32,
     "graph": False,
     "direction": "pull",
 }
@@ -67,6 +69,7 @@ COMMON_ALLOWED = {
     "copy_blocks": (1, 4096),
     "copy_streams": (1, 4),
     "fused": [True, False],
+    "reserve_cus": (0, 1024),
     "graph": [True, False, "auto"],
     "direction": ["pull", "push"],
 }
@@ -99,6 +102,7 @@ def algo_config(options, order: str = "AG_before") -> AlgoConfig:
         signal=SIG_STREAM if options["signal"] == "stream" else SIG_KERNEL,
         tile=TILE_CODE[options["tile"]], mode=MODE_CODE[options["gemm_mode"]],
         copy_blocks=int(options["copy_blocks"]), fused=bool(options["fused"]),
+        reserve_cus=int(options.get("reserve_cus", 32)),
         copy_streams=int(options.get("copy_streams", 1)),
         direction=options.get("direction", "pull"))
 

@@ -131,6 +131,9 @@ def _ipc_cfgs():
                                                           multicast_protocol="batch_memcpy")))
     cfgs.append(("col/coll/fused/256", "col", dict(algorithm="coll_pipeline", backend="ipc",
                                                    s=2, fused=True, tile="256x256")))
+    for alg in ("coll_pipeline", "p2p_pipeline"):  # the persistent gated GEMM (pt4 + reserve)
+        cfgs.append((f"col/{alg}/fused/pt4", "col", dict(algorithm=alg, backend="ipc", s=2,
+                                                         fused=True, tile="pt4")))
     cfgs.append(("col/p2p/noring", "col", dict(algorithm="p2p_pipeline", backend="ipc",
                                                offset_stream_indexing_by_rank=False)))
     cfgs.append(("col/p2p/fp8", "col", dict(algorithm="p2p_pipeline", backend="ipc",
@@ -377,5 +380,58 @@ def test_plan_timeline_world1(comm):
         out = bound.buffer(name).view(torch.float32).view(M, N)
         torch.testing.assert_close(out, ref, rtol=0, atol=1e-3 * K)
     bound.set_timeline(False)
+    bound.close()
+    ctx.close()
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_flag_gated_persistent_gemm_world1(comm, graph):
+    """The persistent pt4 GEMM gated by arrival flags, in one process: a side stream, held back
+    by two unrelated GEMMs, copies the A row blocks in (block-major over 2 "producers" x 4
+    blocks) and signals each block's flag; the gated GEMM, enqueued after it on the caller's
+    stream, must wait for every block (A is NaN-filled before each run), dispatch block-major
+    (nsub) and leave ``reserve_cus`` CUs free for the side stream's kernels."""
+    from ddlb_amd.parallel.context import NativeContext
+    from ddlb_amd.parallel.plan import DT_BF16, Plan, SIG_KERNEL, SIG_STREAM
+
+    M, N, K, nprod, nsub = 32768, 1024, 1024, 2, 4
+    rows = M // (nprod * nsub)
+    plan = Plan(0, 1, nstreams=2, stream_priority=[0, 1])
+    src = plan.buffer("src", M * K * 2)
+    a = plan.buffer("a", M * K * 2)
+    bt = plan.buffer("bt", N * K * 2)
+    c = plan.buffer("c", M * N * 2)
+    junk = plan.buffer("junk", M * N * 2)
+    flags = plan.buffer("flags", 256, zero=True)
+    sig = SIG_KERNEL if graph else SIG_STREAM
+    for _ in range(2):  # keep the side stream busy while the gated GEMM starts
+        plan.gemm(1, src, bt, junk, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, din=DT_BF16,
+                  dout=DT_BF16)
+    for b in range(nsub):
+        for p in (1, 0):
+            sh = p * nsub + b
+            off = sh * rows * K * 2
+            plan.copy(1, a + off, src + off, rows * K * 2)
+            plan.signal(1, [flags + 4 * sh], method=sig)
+    plan.gemm(0, a, bt, c, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, din=DT_BF16, dout=DT_BF16,
+              tile=19, flags=flags, flag_rows=rows, nshards=nprod * nsub, nsub=nsub,
+              first_shard=1, tile_order=1, reserve_cus=32)
+    ctx = NativeContext(comm)
+    bound = ctx.bind(plan)
+    if graph:
+        bound.enable_graph(True)
+    A = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+    W = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
+    bound.buffer("src").view(torch.bfloat16).view(M, K).copy_(A)
+    bound.buffer("bt").view(torch.bfloat16).view(N, K).copy_(W)
+    ref = A.float() @ W.float().T
+    out = bound.buffer("c").view(torch.bfloat16).view(M, N)
+    for _ in range(3):
+        bound.buffer("a").view(torch.bfloat16).fill_(float("nan"))
+        out.zero_()
+        bound.run()
+        torch.cuda.synchronize()
+        bound.check_health()
+        torch.testing.assert_close(out.float(), ref, rtol=0, atol=1e-3 * K)
     bound.close()
     ctx.close()
