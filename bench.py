@@ -71,8 +71,15 @@ def _graph(opts):
 # "/graph": the whole plan is captured once and replayed with one hipGraphLaunch per run; the
 # IPC pipelines issue one HIP call per copy / event / signal (~2 us of host time each, ~200 calls
 # per run at d = 8, s = 8: host-bound without the graph, profiles/r02/r2_13_*).
+# In-kernel all-gather ("agk"): ONE launch per run; its first copy_blocks workgroups pull the
+# peers' row blocks over xGMI and flag them, the rest run the persistent GEMM gated on the flags
+# (no copy streams, no host op per block, one kernel to capture).
+_AGK = dict(algorithm="coll_pipeline", backend="ipc", multicast_protocol="kernel", fused=True,
+            s=8, copy_blocks=32)
 CANDIDATES = [
     ("coll_pipeline/rccl/s4", "native", _COLL4),
+    ("coll_pipeline/ipc/agk32/s8/graph", "native", _graph(_AGK)),
+    ("coll_pipeline/ipc/agk64/s8/graph", "native", _graph(dict(_AGK, copy_blocks=64))),
     ("coll_pipeline/ipc/memcpy/s8/graph", "native", _graph(dict(_COLL_IPC, s=8))),
     ("coll_pipeline/ipc/kernel/s8/graph", "native", _graph(dict(
         _COLL_IPC, s=8, multicast_protocol="kernel", copy_blocks=128, tile="128x128"))),
@@ -99,7 +106,8 @@ CANDIDATES = [
     ("coll_pipeline/ipc/memcpy/s8/q12", "native", dict(_COLL_IPC, s=8,
                                                         _env={"GPU_MAX_HW_QUEUES": "12"})),
     ("coll_pipeline/ipc/memcpy/s8", "native", dict(_COLL_IPC, s=8)),
-    ("coll_pipeline/ipc/memcpy/s8/fused", "native", dict(_COLL_IPC, s=8, fused=True)),
+    ("coll_pipeline/ipc/agk32/s4/graph", "native", _graph(dict(_AGK, s=4))),
+    ("coll_pipeline/ipc/agk32/s8", "native", _AGK),
     ("default/ipc/kernel", "native", _DEF_K),
     # the same reasoning for RCCL's CU-resident kernels, and RCCL held to 16 channels (16 CUs)
     ("coll_pipeline/rccl/s4/128", "native", dict(_COLL4, tile="128x128")),

@@ -53,6 +53,15 @@ struct GemmArgs {
   // i.e. the order chunked pulls from all peers arrive in. nsub = 1: plain shard order.
   int nsub = 1;
   int reserve_cus = 0;              // flag-gated persistent GEMMs: CUs left free (see launch_pt4)
+  // In-kernel all-gather (flag-gated pt4 only): workgroups [0, ag_ctas) of the launch pull the
+  // peers' row blocks of A over xGMI into A (the same rows), count each (producer, block)
+  // segment's ag_parts pieces and set its flag when the last lands, and ACK each producer once
+  // all its rows are read; the other workgroups run the gated GEMM. ag_tab (device, 2*np+2
+  // entries, np = nshards / nsub producers): [src A of producer 0..np-1 | address of my ACK word
+  // at producer 0..np-1 | READY words (ready[p] >= epoch: p's rows may be read) | counters
+  // (nshards per-segment, then np per-producer; monotonic across runs)].
+  int ag_ctas = 0, ag_parts = 1, ag_rank = 0;
+  const uint64_t* ag_tab = nullptr;
   int act = 0;                      // fused epilogue activation: ACT_* below
   // Direct-access A (optional): row block s of shard_rows rows starts at a_table[s] (device
   // array of addresses, e.g. the peers' IPC-mapped shards read straight over xGMI).

@@ -229,6 +229,77 @@ __device__ __forceinline__ void wait_flag(const GemmArgs& p, int64_t row_first, 
   __syncthreads();
 }
 
+// ---------------------------------------------------------------- in-kernel all-gather
+// The copy workgroups of a flag-gated pt4 launch (GemmArgs::ag_ctas). Work units are
+// (block, producer, part), block-major and producers in ring order from rank + 1: the order the
+// gated GEMM dispatches its tiles in (ordered_shard). Each unit is a contiguous byte range of
+// the same rows in the producer's A and ours; 8 x 16-byte loads in flight per thread. After a
+// unit every thread releases its stores at agent scope (L2 written back: the GEMM tile reading
+// these rows may sit on another XCD), then thread 0 counts the unit; the last part of a
+// segment publishes its flag, the last unit of a producer ACKs it (system scope, over xGMI).
+template <int ESZ>
+__device__ __forceinline__ void ag_copy_role(const GemmArgs& p) {
+  const unsigned want = p.epoch_ptr ? *p.epoch_ptr : p.epoch;
+  const int np = p.nshards / p.nsub, s = p.nsub, parts = p.ag_parts;
+  const uint64_t* tab = p.ag_tab;
+  const unsigned* ready = (const unsigned*)tab[2 * np];
+  unsigned* count = (unsigned*)tab[2 * np + 1];
+  unsigned* arrive = const_cast<unsigned*>(p.flags);
+  const int64_t seg = p.flag_rows * p.lda * ESZ;
+  const int64_t part = (seg / parts + 15) / 16 * 16;
+  const int per_b = (np - 1) * parts, units = s * per_b;
+  const int tid = threadIdx.x;
+  constexpr int T = 512, U = 8;
+  unsigned seen = 0;
+  for (int u = (int)blockIdx.x; u < units; u += p.ag_ctas) {
+    const int b = u / per_b, r = u % per_b;
+    const int prod = (p.ag_rank + 1 + r / parts) % np, pi = r % parts;
+    if (!((seen >> prod) & 1u)) {  // first unit of this producer: its READY, acquired
+      if (tid == 0) {
+        unsigned spins = 0;
+        while (__hip_atomic_load(ready + prod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) <
+               want) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spins > (1u << 26)) {
+            if (p.timeout_word) atomicOr(p.timeout_word, 4u);
+            break;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
+      }
+      __syncthreads();
+      seen |= 1u << prod;
+    }
+    const int64_t base = (int64_t)(prod * s + b) * seg + (int64_t)pi * part;
+    int64_t nb = seg - (int64_t)pi * part;
+    nb = nb < part ? nb : part;
+    const uint4* src = (const uint4*)((const char*)tab[prod] + base);
+    uint4* dst = (uint4*)((char*)p.a + base);
+    const int64_t nvec = nb > 0 ? nb / 16 : 0;
+    int64_t v = tid;
+    for (; v + (U - 1) * T < nvec; v += U * T) {
+      uint4 x[U];
+#pragma unroll
+      for (int i = 0; i < U; ++i) x[i] = src[v + i * T];
+#pragma unroll
+      for (int i = 0; i < U; ++i) dst[v + i * T] = x[i];
+    }
+    for (; v < nvec; v += T) dst[v] = src[v];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    if (tid == 0) {
+      const int sh = prod * s + b;
+      if (__hip_atomic_fetch_add(count + sh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 ==
+          want * (unsigned)parts)
+        __hip_atomic_store(arrive + sh, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      if (__hip_atomic_fetch_add(count + np * s + prod, 1u, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT) + 1 == want * (unsigned)(s * parts))
+        __hip_atomic_store((unsigned*)tab[np + prod], want, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 // Arrival wait for the tile whose first logical row is m0 and which has (up to) BM rows.
 __device__ __forceinline__ void wait_tile(const GemmArgs& p, int64_t m0, int BM) {
   if (p.flags == nullptr) return;
@@ -1403,8 +1474,18 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   const int tiles_n = p.N / 256, ntiles = (p.M / 256) * tiles_n;
   const int esz = Mma::kElem;
   const int nk = p.K * esz / ROWB;
-  const int my_tiles =
-      ((int)blockIdx.x < ntiles) ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  int bid = (int)blockIdx.x, nblk = (int)gridDim.x;
+  if constexpr (GATED) {
+    if (p.ag_ctas > 0) {  // in-kernel all-gather: the first ag_ctas workgroups copy
+      if (bid < p.ag_ctas) {
+        ag_copy_role<Mma::kElem>(p);
+        return;
+      }
+      bid -= p.ag_ctas;
+      nblk -= p.ag_ctas;
+    }
+  }
+  const int my_tiles = (bid < ntiles) ? (ntiles - 1 - bid) / nblk + 1 : 0;
   if (my_tiles == 0) return;
 
   const int drow = lane >> 3, dpc = lane & 7;
@@ -1425,7 +1506,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   const char* baseB = nullptr;
   int src_tile = -1;
   auto origin = [&](int ti, int64_t& m0, int64_t& n0) __attribute__((always_inline)) {
-    const int wg = tile_index_virtual(p, (int)blockIdx.x + ti * (int)gridDim.x, ntiles);
+    const int wg = tile_index_virtual(p, bid + ti * nblk, ntiles);
     int tm_, tn_;
     tile_mn(p, wg, p.M / 256, tiles_n, tm_, tn_);
     m0 = (int64_t)tm_ * 256;
@@ -2114,11 +2195,15 @@ hipError_t launch_pt4(const GemmArgs& p, hipStream_t s) {
   // with every CU holding a (spinning) tile, the copy / signal kernels that set the flags could
   // not be scheduled; the reserve keeps the gate deadlock-free whoever moves the data.
   if (p.flags != nullptr && p.reserve_cus > 0) grid -= p.reserve_cus;
+  GemmArgs q = p;
+  q.ag_ctas = p.flags != nullptr && p.ag_ctas > 0 ? (p.ag_ctas + 7) / 8 * 8 : 0;
+  grid -= q.ag_ctas;
   grid = (grid / 8) * 8;  // blockIdx % 8 == XCD group for every virtual tile id
   if (grid > tiles) grid = tiles;
   if (grid < 1) grid = 1;
   if (p.flags != nullptr)
-    hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, true>), dim3(grid), dim3(512), 0, s, p);
+    hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, true>), dim3(grid + q.ag_ctas), dim3(512), 0,
+                       s, q);
   else
     hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false>), dim3(grid), dim3(512), 0, s, p);
   return hipGetLastError();

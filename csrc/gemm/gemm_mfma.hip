@@ -103,6 +103,19 @@ hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mo
       tile = TILE_128x128;
     if (mode == GEMM_MODE_GENERIC || !gemm_fast_path_ok(p, din, dout)) return hipErrorNotSupported;
   }
+  if (p.ag_ctas > 0) {
+    // in-kernel all-gather: only the gated persistent pt4 kernel carries the copy workgroups;
+    // anything else would skip the copies, so refuse rather than fall back
+    const int esz = dtype_size(din);
+    if (p.flags == nullptr || p.a_table != nullptr || mode == GEMM_MODE_GENERIC ||
+        !gemm_fast_path_ok(p, din, dout) || p.M % 256 || p.N % 256 || p.a_grp != p.M ||
+        (int64_t)p.K * esz / 128 < 2 || p.lda * esz > (1 << 22) || p.ldb * esz > (1 << 22) ||
+        p.nsub < 1 || p.nshards % p.nsub || p.nshards / p.nsub > 32 || p.ag_parts < 1 ||
+        p.ag_tab == nullptr)
+      return hipErrorNotSupported;
+    if (mode == GEMM_MODE_BLAS) mode = GEMM_MODE_AUTO;
+    tile = TILE_PT4;
+  }
   if (mode == GEMM_MODE_BLAS) {
     const hipError_t e = blaslt_gemm(p, din, dout, s);
     if (e != hipErrorNotSupported) return e;

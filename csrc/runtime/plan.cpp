@@ -228,6 +228,10 @@ GemmArgs PlanExecutor::gemm_args(const int64_t* o) const {
   g.tile_order = (int)o[23];
   g.nsub = o[27] > 0 ? (int)o[27] : 1;
   g.reserve_cus = (int)o[28];
+  g.ag_ctas = (int)(o[29] & 0xfffff);
+  g.ag_parts = (int)((o[29] >> 20) & 0xfffff);
+  g.ag_rank = (int)((o[29] >> 40) & 0xffff);
+  g.ag_tab = (const uint64_t*)o[30];
   g.act = (int)o[24];
   g.a_table = (const uint64_t*)o[25];
   g.shard_rows = o[26];

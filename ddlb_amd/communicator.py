@@ -52,8 +52,11 @@ class Communicator:
                 raise RuntimeError(f"local size {self.local_size} exceeds visible GPUs {ndev}")
             torch.cuda.set_device(self.local_rank % ndev)
             self.device = torch.device("cuda", self.local_rank % ndev)
+            # ranks co-resident on this device (> 1 only in shared-GPU rehearsals / tests)
+            self.ranks_per_device = max(1, -(-self.local_size // ndev))
         else:
             self.device = torch.device("cpu")
+            self.ranks_per_device = 1
         self._native = None
         self._initialized = True
 

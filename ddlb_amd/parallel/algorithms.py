@@ -46,6 +46,7 @@ from ddlb_amd.parallel.plan import (COPY_ENGINE, COPY_KERNEL, DT_SIZE, DT_U8,
                                     SIG_STREAM, Plan, Ref)
 
 S_MAIN, S_COMM = 0, 1
+TILE_PT4 = 19  # csrc/gemm/gemm.h Tile::TILE_PT4 (the only kernel carrying in-kernel copies)
 
 
 def _s_copy(i: int) -> int:
@@ -68,6 +69,7 @@ class AlgoConfig:
     copy_streams: int = 1               # memcpy pulls: copy streams (copy engines) per peer
     fused: bool = False                 # columnwise p2p / coll: one flag-gated GEMM launch
     reserve_cus: int = 32               # fused: CUs the persistent gated GEMM leaves free
+    ag_reserve: int = 0                 # in-kernel all-gather: CUs left free besides its copiers
     act: int = 0                        # columnwise: fused GEMM epilogue activation (ACT_*)
     direction: str = "pull"             # columnwise ipc: pull peers' shards | push mine to peers
 
@@ -114,7 +116,8 @@ class _Flags:
         self.slots: Dict[str, Tuple[int, int]] = {}
         self.words = 0
         for name, count in (("READY", d), ("ACK", d), ("CHUNK", s * d), ("ACKS", s * d),
-                            ("ARRIVE", s * d)):  # ARRIVE[p * s + b]: block b of shard p landed
+                            ("ARRIVE", s * d),  # ARRIVE[p * s + b]: block b of shard p landed
+                            ("CNT", s * d + d)):  # in-kernel all-gather counters (monotonic)
             self.slots[name] = (self.words, count)
             self.words += count
         nbytes = max(256, ((self.words * 4 + 255) // 256) * 256)
@@ -145,7 +148,7 @@ def _wait(plan: Plan, stream: int, flags: List[Ref], cfg: AlgoConfig, delta: int
 # =====================================================================================
 #  TP-Columnwise
 # =====================================================================================
-def check_columnwise(d: int, m: int, n: int, k: int, cfg: AlgoConfig) -> None:
+def check_columnwise(d: int, m: int, n: int, k: int, cfg: AlgoConfig, ein: int = 2) -> None:
     if m % d:
         raise ValueError(f"m ({m}) must be divisible by world_size ({d})")
     if cfg.algorithm == "coll_pipeline" and m % (d * cfg.s):
@@ -169,13 +172,18 @@ def check_columnwise(d: int, m: int, n: int, k: int, cfg: AlgoConfig) -> None:
                       cfg.algorithm not in ("p2p_pipeline", "coll_pipeline")):
         raise ValueError("fused=True (one arrival-flag-gated GEMM) applies to backend=ipc, "
                          "order=AG_before, p2p_pipeline / coll_pipeline")
+    if (cfg.fused and cfg.protocol == "kernel" and cfg.algorithm == "coll_pipeline" and d > 1
+            and (m % 256 or n % 256 or k * ein % 128 or k * ein < 256)):
+        raise ValueError("the in-kernel all-gather (coll_pipeline, fused, kernel copies) runs on "
+                         "the persistent 256x256 GEMM: m and n multiples of 256, k rows of "
+                         "whole 128-byte K-tiles")
     if d > 17:
         raise ValueError("at most 17 ranks per node are supported by the flag/reduce ops")
 
 
 def build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, dout: int,
                         cfg: AlgoConfig) -> Tuple[Plan, PlanIO]:
-    check_columnwise(d, m, n, k, cfg)
+    check_columnwise(d, m, n, k, cfg, DT_SIZE[din])
     ein, eout = DT_SIZE[din], DT_SIZE[dout]
     ml = m // d
     ns = _nstreams(d, cfg.copy_streams)
@@ -244,6 +252,26 @@ def build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, dou
             plan.record(S_COMM, e)
             plan.wait(S_MAIN, e)
             gemm(S_MAIN, stg, crow(j * rows), d * rows, c_grp=rows, c_gstride=ml)
+    elif alg == "coll_pipeline" and be == "ipc" and cfg.fused and cfg.protocol == "kernel":
+        # In-kernel all-gather: ONE launch. Its first copy_blocks workgroups pull row block b
+        # of every peer over xGMI (block-major, ring order) and set ARRIVE[p * s + b] when a
+        # block has landed; the other workgroups run the persistent GEMM gated on those flags
+        # (csrc/gemm/gemm_kernels.h ag_copy_role). No copy streams, no host op per block:
+        # READY out, own blocks marked, one kernel, ACKs back.
+        rows = ml // cfg.s
+        _signal(plan, S_MAIN, [flags.ref("READY", rank, owner=p) for p in range(d) if p != rank],
+                cfg)
+        _signal(plan, S_MAIN, [flags.ref("ARRIVE", rank * cfg.s + j) for j in range(cfg.s)], cfg)
+        seg = rows * k * ein
+        ag = dict(ctas=cfg.copy_blocks, parts=max(1, min(seg // (256 << 10), 1024)), rank=rank,
+                  src=[A.at(p) for p in range(d)],
+                  ack=[flags.ref("ACK", rank, owner=p) for p in range(d)],
+                  ready=flags.ref("READY", 0), count=flags.ref("CNT", 0))
+        gdt_ag = dict(gdt, tile=TILE_PT4)
+        plan.gemm(S_MAIN, A, Bt, C, M=m, N=n, K=k, lda=k, ldb=k, ldc=n, **gdt_ag,
+                  flags=flags.ref("ARRIVE", 0), flag_rows=rows, nshards=d * cfg.s, nsub=cfg.s,
+                  first_shard=rank, tile_order=1, reserve_cus=cfg.ag_reserve, ag=ag)
+        _wait(plan, S_MAIN, [flags.ref("ACK", p) for p in range(d) if p != rank], cfg)
     elif alg == "coll_pipeline" and be == "ipc" and cfg.fused:
         # ONE flag-gated GEMM over all m rows instead of s stage GEMMs: tiles are dispatched
         # block-major (block 0 of the own shard and of every peer, then block 1, ...), the order
@@ -631,6 +659,26 @@ def build_tp_rowwise(rank: int, d: int, m: int, n: int, k: int, din: int, dout: 
             gemm(S_MAIN, j * rows, stg, d * rows, a_grp=rows, a_gstride=ml)
             plan.edge(S_MAIN, S_COMM)
             plan.reduce_scatter(S_COMM, stg, OUT + j * rows * n * eout, rows * n, dout)
+    elif alg == "coll_pipeline" and be == "ipc" and cfg.fused and cfg.protocol == "kernel":
+        # In-kernel all-gather: ONE launch. Its first copy_blocks workgroups pull row block b
+        # of every peer over xGMI (block-major, ring order) and set ARRIVE[p * s + b] when a
+        # block has landed; the other workgroups run the persistent GEMM gated on those flags
+        # (csrc/gemm/gemm_kernels.h ag_copy_role). No copy streams, no host op per block:
+        # READY out, own blocks marked, one kernel, ACKs back.
+        rows = ml // cfg.s
+        _signal(plan, S_MAIN, [flags.ref("READY", rank, owner=p) for p in range(d) if p != rank],
+                cfg)
+        _signal(plan, S_MAIN, [flags.ref("ARRIVE", rank * cfg.s + j) for j in range(cfg.s)], cfg)
+        seg = rows * k * ein
+        ag = dict(ctas=cfg.copy_blocks, parts=max(1, min(seg // (256 << 10), 1024)), rank=rank,
+                  src=[A.at(p) for p in range(d)],
+                  ack=[flags.ref("ACK", rank, owner=p) for p in range(d)],
+                  ready=flags.ref("READY", 0), count=flags.ref("CNT", 0))
+        gdt_ag = dict(gdt, tile=TILE_PT4)
+        plan.gemm(S_MAIN, A, Bt, C, M=m, N=n, K=k, lda=k, ldb=k, ldc=n, **gdt_ag,
+                  flags=flags.ref("ARRIVE", 0), flag_rows=rows, nshards=d * cfg.s, nsub=cfg.s,
+                  first_shard=rank, tile_order=1, reserve_cus=cfg.ag_reserve, ag=ag)
+        _wait(plan, S_MAIN, [flags.ref("ACK", p) for p in range(d) if p != rank], cfg)
     elif alg == "coll_pipeline" and be == "ipc" and cfg.fused:
         # ONE flag-gated GEMM over all m rows instead of s stage GEMMs: tiles are dispatched
         # block-major (block 0 of the own shard and of every peer, then block 1, ...), the order

@@ -120,7 +120,7 @@ class Plan:
              flags: Optional[Ref] = None, flag_rows: int = 0, nshards: int = 1,
              first_shard: int = 0, tile_order: int = 0, act: int = 0,
              a_shards: Optional[Sequence[Ref]] = None, shard_rows: int = 0,
-             nsub: int = 1, reserve_cus: int = 0) -> Op:
+             nsub: int = 1, reserve_cus: int = 0, ag: Optional[dict] = None) -> Op:
         """``a_shards``: A row block s (``shard_rows`` rows each) is read from ``a_shards[s]``
         (a peer's copy for a direct-access GEMM that pulls its operand over xGMI).
         ``flags`` (arrival-gated tiles): shard ``i`` = rows ``[i*flag_rows, (i+1)*flag_rows)`` may
@@ -128,9 +128,22 @@ class Plan:
         dispatched shard by shard from ``first_shard`` — ``nsub`` > 1 splits each producer's
         shard into that many row blocks (shard = producer * nsub + block) dispatched block-major
         (block 0 of every producer first), the order chunked pulls land in. A persistent
-        flag-gated GEMM leaves ``reserve_cus`` CUs free for the kernels that set the flags."""
+        flag-gated GEMM leaves ``reserve_cus`` CUs free for the kernels that set the flags.
+        ``ag`` = in-kernel all-gather (``dict(ctas, parts, rank, src, ack, ready, count)``, see
+        csrc/gemm/gemm.h ``ag_ctas``): the launch's first ``ctas`` workgroups pull row block b of
+        every producer p (``src[p]``, same rows) into A, set ``flags[p * nsub + b]`` and ACK p
+        (``ack[p]``) after READY (``ready[p]``); the GEMM tiles gate on those flags."""
         if nsub < 1 or nshards % nsub:
             raise ValueError(f"nsub ({nsub}) must divide nshards ({nshards})")
+        if ag is not None:
+            npro = nshards // nsub
+            if flags is None or len(ag["src"]) != npro or len(ag["ack"]) != npro:
+                raise ValueError("in-kernel all-gather needs flags and one src / ack per producer")
+            if not 1 <= ag["ctas"] < 1 << 20 or not 1 <= ag["parts"] < 1 << 20:
+                raise ValueError("ag ctas / parts out of range")
+            ag = dict(ag, table=self.table(f"__agtab{len(self.buffers)}",
+                                           list(ag["src"]) + list(ag["ack"]) +
+                                           [ag["ready"], ag["count"]]))
         a_table = None
         if a_shards is not None:
             if shard_rows <= 0 or len(a_shards) * shard_rows < M:
@@ -143,7 +156,7 @@ class Plan:
                          tile_order=tile_order, act=act,
                          a_shards=list(a_shards) if a_shards is not None else None,
                          shard_rows=shard_rows, a_table=a_table, nsub=nsub,
-                         reserve_cus=reserve_cus)
+                         reserve_cus=reserve_cus, ag=ag)
 
     def table(self, name: str, refs: Sequence[Ref]) -> Ref:
         """Device array of 64-bit addresses of ``refs`` (written once when the plan is bound)."""
@@ -232,6 +245,10 @@ class Plan:
                 if a.get("a_table") is not None:
                     w[25], w[26] = resolve(a["a_table"]), a["shard_rows"]
                 w[27], w[28] = a.get("nsub", 1), a.get("reserve_cus", 0)
+                g = a.get("ag")
+                if g is not None:
+                    w[29] = g["ctas"] | (g["parts"] << 20) | (g["rank"] << 40)
+                    w[30] = resolve(g["table"])
             elif k in (OP_RECORD, OP_WAIT):
                 w[2] = a["event"]
             elif k in (OP_ALLGATHER, OP_REDUCE_SCATTER):

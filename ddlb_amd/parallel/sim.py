@@ -155,6 +155,8 @@ class Simulator:
     def _exec_local(self, r: int, op, vc: _VC) -> None:
         a, k = op.args, op.kind
         what = f"r{r}.s{op.stream}.{OP_NAMES[k]}"
+        if k == OP_GEMM and a.get("ag") is not None:
+            self._exec_ag(r, op, vc, what)
         if k == OP_GEMM:
             ein, eout = DT_SIZE[a["din"]], DT_SIZE[a["dout"]]
             shards = a.get("a_shards")
@@ -219,6 +221,31 @@ class Simulator:
             pass
         else:
             raise AssertionError(f"not a local op: {OP_NAMES[k]}")
+
+    def _exec_ag(self, r: int, op, vc: _VC, what: str) -> None:
+        """Copy workgroups of an in-kernel all-gather: every peer's row blocks into the same
+        rows of A, each block's ARRIVE flag, then an ACK at the producer."""
+        a = op.args
+        g = a["ag"]
+        npro, nsub = a["nshards"] // a["nsub"], a["nsub"]
+        seg = a["flag_rows"] * a["lda"] * DT_SIZE[a["din"]]
+        val = self.epoch[r]
+        for q in range(npro):
+            if q == g["rank"]:
+                continue
+            for b in range(nsub):
+                off = (q * nsub + b) * seg
+                src, dst = g["src"][q] + off, a["a"] + off
+                self._touch(r, src, seg, False, vc, what + f".ag.src{q}")
+                self._touch(r, dst, seg, True, vc, what + ".ag.dst")
+                self._buf(r, dst)[dst.off:dst.off + seg] = \
+                    self._buf(r, src)[src.off:src.off + seg].clone()
+                f = a["flags"] + 4 * (q * nsub + b)
+                self._buf(r, f)[f.off:f.off + 4].view(torch.int32)[0] = val
+                self.flag_vc[(self._owner(r, f), f.buf, f.off, val)] = vc.copy()
+            f = g["ack"][q]
+            self._buf(r, f)[f.off:f.off + 4].view(torch.int32)[0] = val
+            self.flag_vc[(self._owner(r, f), f.buf, f.off, val)] = vc.copy()
 
     # --------------------------------------------------------------- collectives
     def _exec_collective(self, group: List[Tuple[int, List]], vcs: List[_VC]) -> None:
@@ -373,6 +400,27 @@ class Simulator:
                                 if tgt not in done_rec[r]:
                                     break
                                 vc.join(done_rec[r][tgt])
+                        elif op.kind == OP_GEMM and op.args.get("ag") is not None:
+                            # in-kernel all-gather: the copy workgroups read producer p only
+                            # after READY[p]; the own blocks' flags come from earlier ops. The
+                            # launch is modelled atomically: copies, flags, ACKs, then the GEMM
+                            a = op.args
+                            g = a["ag"]
+                            npro = a["nshards"] // a["nsub"]
+                            gate = [g["ready"] + 4 * q for q in range(npro) if q != g["rank"]]
+                            gate += [a["flags"] + 4 * (g["rank"] * a["nsub"] + b)
+                                     for b in range(a["nsub"])]
+                            ok = True
+                            for f in gate:
+                                val = int(self._buf(r, f)[f.off:f.off + 4].view(torch.int32)[0])
+                                if val < self.epoch[r]:
+                                    ok = False
+                                    break
+                                src = self.flag_vc.get((self._owner(r, f), f.buf, f.off, val))
+                                if src is not None:
+                                    vc.join(src)
+                            if not ok:
+                                break
                         elif op.kind == OP_GEMM and op.args.get("flags") is not None:
                             # flag-gated GEMM: every tile spins on flags[shard] >= epoch before
                             # reading its A rows; atomically modelled as waiting on all shards

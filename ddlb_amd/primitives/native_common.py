@@ -91,9 +91,11 @@ def algo_config(options, order: str = "AG_before") -> AlgoConfig:
         raise BackendUnavailable(
             f"backend '{backend}' needs UCC/UCX, which the MI355X stack does not ship; use "
             "backend=rccl (alias nccl) or backend=ipc (alias cuda)")
-    if options["fused"] and options["multicast_protocol"] == "kernel":
-        raise ValueError("fused=True spins GEMM tiles on arrival flags; it needs copy-engine "
-                         "transfers (multicast_protocol=memcpy|batch_memcpy), not CU copies")
+    if (options["fused"] and options["multicast_protocol"] == "kernel"
+            and options["algorithm"] != "coll_pipeline"):
+        raise ValueError("fused=True with CU copies (multicast_protocol=kernel) is the in-kernel "
+                         "all-gather of algorithm=coll_pipeline; p2p fused needs copy-engine "
+                         "transfers (memcpy | batch_memcpy)")
     return AlgoConfig(
         algorithm=options["algorithm"], backend=backend, order=order, s=int(options["s"]),
         ring=bool(options["offset_stream_indexing_by_rank"]),
@@ -105,6 +107,23 @@ def algo_config(options, order: str = "AG_before") -> AlgoConfig:
         reserve_cus=int(options.get("reserve_cus", 32)),
         copy_streams=int(options.get("copy_streams", 1)),
         direction=options.get("direction", "pull"))
+
+
+def share_cus(cfg: AlgoConfig, communicator) -> AlgoConfig:
+    """Ranks sharing one GPU (rehearsals, tests): a flag-gated persistent GEMM must not take the
+    CUs the co-resident ranks' kernels need to set its flags, so each rank's gated launch is held
+    to its share of the device."""
+    import dataclasses
+
+    import torch
+
+    rpd = getattr(communicator, "ranks_per_device", 1)
+    if rpd <= 1 or not cfg.fused:
+        return cfg
+    cus = torch.cuda.get_device_properties(communicator.device).multi_processor_count
+    spare = cus - cus // rpd
+    return dataclasses.replace(cfg, reserve_cus=max(cfg.reserve_cus, spare + 32),
+                               ag_reserve=max(cfg.ag_reserve, spare + 8))
 
 
 def dtype_codes(dtype_name: str):

@@ -14,7 +14,8 @@ from __future__ import annotations
 
 from ddlb_amd.parallel.algorithms import build_tp_columnwise
 from ddlb_amd.primitives.native_common import (COMMON_ALIASES, COMMON_ALLOWED, COMMON_DEFAULTS,
-                                               algo_config, dtype_codes, maybe_enable_graph)
+                                               algo_config, dtype_codes, maybe_enable_graph,
+                                               share_cus)
 from ddlb_amd.primitives.tp_columnwise.base import TPColumnwise
 
 
@@ -34,7 +35,8 @@ class NativeTPColumnwise(TPColumnwise):
         if not self.communicator.is_gpu:
             raise RuntimeError("the native implementation needs a ROCm GPU (use compute_only / "
                                "pytorch on the CPU)")
-        self.cfg = algo_config(self.options, order=self.options["order"])
+        self.cfg = share_cus(algo_config(self.options, order=self.options["order"]),
+                             self.communicator)
         din, dout = dtype_codes(self.dtype)
         self.plan, self.io = build_tp_columnwise(self.rank, self.world_size, self.m, self.n,
                                                  self.k, din, dout, self.cfg)

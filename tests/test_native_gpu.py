@@ -131,6 +131,14 @@ def _ipc_cfgs():
                                                           multicast_protocol="batch_memcpy")))
     cfgs.append(("col/coll/fused/256", "col", dict(algorithm="coll_pipeline", backend="ipc",
                                                    s=2, fused=True, tile="256x256")))
+    # in-kernel all-gather: copy workgroups inside the gated persistent GEMM launch
+    cfgs.append(("col/coll/agk", "col", dict(algorithm="coll_pipeline", backend="ipc", s=2,
+                                             fused=True, multicast_protocol="kernel",
+                                             copy_blocks=8)))
+    cfgs.append(("col/coll/agk/ksig/fp8", "col", dict(algorithm="coll_pipeline", backend="ipc",
+                                                      s=2, fused=True, signal="kernel",
+                                                      multicast_protocol="kernel", copy_blocks=16,
+                                                      dtype="float8_e4m3fn")))
     for alg in ("coll_pipeline", "p2p_pipeline"):  # the persistent gated GEMM (pt4 + reserve)
         cfgs.append((f"col/{alg}/fused/pt4", "col", dict(algorithm=alg, backend="ipc", s=2,
                                                          fused=True, tile="pt4")))
@@ -156,6 +164,8 @@ def _ipc_cfgs():
             ("col/p2p/memcpy/graph", "col", dict(algorithm="p2p_pipeline")),
             ("col/p2p/fused/graph", "col", dict(algorithm="p2p_pipeline", fused=True)),
             ("col/coll/fused/graph", "col", dict(algorithm="coll_pipeline", s=2, fused=True)),
+            ("col/coll/agk/graph", "col", dict(algorithm="coll_pipeline", s=2, fused=True,
+                                               multicast_protocol="kernel", copy_blocks=8)),
             ("col/direct/graph", "col", dict(algorithm="direct")),
             ("col/coll/push/graph", "col", dict(algorithm="coll_pipeline", s=2, direction="push")),
             ("row/default/kernel/graph", "row", dict(algorithm="default",
@@ -428,6 +438,56 @@ def test_flag_gated_persistent_gemm_world1(comm, graph):
     out = bound.buffer("c").view(torch.bfloat16).view(M, N)
     for _ in range(3):
         bound.buffer("a").view(torch.bfloat16).fill_(float("nan"))
+        out.zero_()
+        bound.run()
+        torch.cuda.synchronize()
+        bound.check_health()
+        torch.testing.assert_close(out.float(), ref, rtol=0, atol=1e-3 * K)
+    bound.close()
+    ctx.close()
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_in_kernel_allgather_world1(comm, graph):
+    """The in-kernel all-gather in one process: a local buffer stands in for the peer's copy of
+    A (same rows), READY is signalled locally, the peer's rows of the gather buffer are NaN
+    before each run; the copy workgroups must pull them, flag each block, ACK, and the gated
+    GEMM tiles must wait for them (C checked against fp32 every run)."""
+    from ddlb_amd.parallel.context import NativeContext
+    from ddlb_amd.parallel.plan import DT_BF16, Plan, SIG_KERNEL, SIG_STREAM
+
+    M, N, K, nsub = 32768, 1024, 1024, 4
+    half, rows = M // 2, M // (2 * nsub)
+    plan = Plan(0, 1, nstreams=1, stream_priority=[0])
+    a = plan.buffer("a", M * K * 2)
+    peer = plan.buffer("peer", M * K * 2)
+    bt = plan.buffer("bt", N * K * 2)
+    c = plan.buffer("c", M * N * 2)
+    fl = plan.buffer("flags", 256, zero=True)
+    READY, ACK, ARRIVE, CNT = fl, fl + 8, fl + 16, fl + 48
+    sig = SIG_KERNEL if graph else SIG_STREAM
+    plan.signal(0, [READY + 4], method=sig)
+    plan.signal(0, [ARRIVE + 4 * j for j in range(nsub)], method=sig)
+    ag = dict(ctas=32, parts=8, rank=0, src=[a, peer], ack=[ACK, ACK + 4], ready=READY,
+              count=CNT)
+    plan.gemm(0, a, bt, c, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, din=DT_BF16, dout=DT_BF16,
+              tile=19, flags=ARRIVE, flag_rows=rows, nshards=2 * nsub, nsub=nsub, first_shard=0,
+              tile_order=1, ag=ag)
+    plan.wait_signal(0, [ACK + 4], method=sig)
+    ctx = NativeContext(comm)
+    bound = ctx.bind(plan)
+    if graph:
+        bound.enable_graph(True)
+    A = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+    W = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
+    av = bound.buffer("a").view(torch.bfloat16).view(M, K)
+    av[:half].copy_(A[:half])
+    bound.buffer("peer").view(torch.bfloat16).view(M, K)[half:].copy_(A[half:])
+    bound.buffer("bt").view(torch.bfloat16).view(N, K).copy_(W)
+    ref = A.float() @ W.float().T
+    out = bound.buffer("c").view(torch.bfloat16).view(M, N)
+    for _ in range(3):
+        av[half:].fill_(float("nan"))
         out.zero_()
         bound.run()
         torch.cuda.synchronize()

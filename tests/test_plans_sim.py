@@ -2,12 +2,14 @@
 protocol (no deadlock, no unordered conflicting access) and numerics vs an fp32 reference."""
 
 import itertools
+import math
 
 import pytest
 import torch
 
 from ddlb_amd.parallel.algorithms import AlgoConfig, build_tp_columnwise, build_tp_rowwise
-from ddlb_amd.parallel.plan import DT_BF16, DT_F32, OP_GEMM, SIG_KERNEL, SIG_STREAM
+from ddlb_amd.parallel.plan import (DT_BF16, DT_F32, OP_COPY, OP_COPY_MULTI, OP_GEMM, OP_SIGNAL,
+                                    SIG_KERNEL, SIG_STREAM)
 from ddlb_amd.parallel.sim import Simulator, make_buffers, read_tensor, write_tensor
 
 ALGS = ["default", "coll_pipeline", "p2p_pipeline"]
@@ -196,7 +198,10 @@ def test_bench_candidates_simulate(d, prim, label, cfg):
     """Every native candidate of the N>1 bench pool, at the driver's world sizes (incl. 8, which
     no GPU box here can run): protocol completes, no race, exact result, several epochs."""
     s = cfg.s if cfg.algorithm == "coll_pipeline" else 1
-    if prim == "tp_columnwise":
+    if prim == "tp_columnwise" and cfg.fused and cfg.protocol == "kernel":
+        # in-kernel all-gather: the persistent 256x256 kernel's shape rules
+        _run_col(d, m=256 * d * s // math.gcd(256, d * s), n=256, k=64, cfg=cfg, epochs=2)
+    elif prim == "tp_columnwise":
         _run_col(d, m=4 * d * s, n=8, k=12, cfg=cfg, epochs=2)
     else:
         _run_row(d, m=4 * d * s, n=8, k=4 * d, cfg=cfg, epochs=2)
@@ -227,3 +232,36 @@ def test_columnwise_copy_streams(d, alg, streams):
     plan, _ = build_tp_columnwise(0, d, 16 * d, 8, 12, DT_F32, DT_F32, cfg)
     assert plan.nstreams == 2 + (d - 1) * streams
     _run_col(d, m=16 * d, n=8, k=12, cfg=cfg)
+
+
+@pytest.mark.parametrize("d", [2, 3, 4])
+@pytest.mark.parametrize("sig", [SIG_STREAM, SIG_KERNEL])
+def test_in_kernel_allgather_plan(d, sig):
+    """coll_pipeline fused with CU copies = ONE launch whose copy workgroups pull every peer's
+    blocks after its READY and ACK it; the GEMM tiles gate on the blocks' ARRIVE flags."""
+    cfg = AlgoConfig(algorithm="coll_pipeline", backend="ipc", fused=True, s=2, signal=sig,
+                     protocol="kernel", copy_blocks=16)
+    _run_col(d, m=256 * d, n=256, k=64, cfg=cfg, epochs=3)
+    plan, _ = build_tp_columnwise(0, d, 256 * d, 256, 64, DT_F32, DT_F32, cfg)
+    g = [op for op in plan.ops if op.kind == OP_GEMM]
+    assert len(g) == 1 and g[0].args["ag"]["ctas"] == 16 and g[0].args["tile"] == 19
+    assert not any(op.kind in (OP_COPY, OP_COPY_MULTI) for op in plan.ops)
+    assert max(op.stream for op in plan.ops) == 0  # everything on the caller's stream
+    with pytest.raises(ValueError):  # the persistent 256x256 kernel carries the copies
+        build_tp_columnwise(0, d, 16 * d, 8, 8, DT_F32, DT_F32, cfg)
+
+
+def test_in_kernel_allgather_ack_protocol_negative():
+    """Without the READY signals the copy workgroups can never start: a deadlock."""
+    from ddlb_amd.parallel.sim import Deadlock
+
+    cfg = AlgoConfig(algorithm="coll_pipeline", backend="ipc", fused=True, s=2,
+                     protocol="kernel", copy_blocks=8)
+    built = [build_tp_columnwise(r, 2, 512, 256, 64, DT_F32, DT_F32, cfg) for r in range(2)]
+    plans = [p for p, _ in built]
+    for p in plans:  # drop READY: the copy workgroups can never start
+        p.ops = [op for op in p.ops if not (op.kind == OP_SIGNAL and any(
+            f.buf == "flags" and f.owner is not None for f in op.args["flags"]))]
+    sim = Simulator(plans, make_buffers(plans))
+    with pytest.raises(Deadlock):
+        sim.run_epoch()
