@@ -448,12 +448,13 @@ def main(argv=None) -> int:
                    help="timed steps per autotune measurement (0 = 50 at world 1, 20 otherwise)")
     p.add_argument("--tune-rounds", type=int, default=0,
                    help="passes over the candidate pool (0 = 2 at world 1, 1 otherwise)")
-    p.add_argument("--candidate-timeout", type=float, default=90.0,
-                   help="per-candidate child timeout (a healthy candidate takes ~5-15 s)")
-    p.add_argument("--tune-budget-s", type=float, default=420.0,
+    p.add_argument("--candidate-timeout", type=float, default=60.0,
+                   help="per-candidate child timeout (a healthy candidate takes ~3-15 s)")
+    p.add_argument("--tune-budget-s", type=float, default=300.0,
                    help="stop trying further candidates after this much autotuning wall time "
-                        "(once a native candidate has succeeded)")
-    p.add_argument("--tune-cap-s", type=float, default=900.0,
+                        "(once a native candidate has succeeded); sized so the whole job, "
+                        "final run and fallbacks included, stays well inside 10 minutes")
+    p.add_argument("--tune-cap-s", type=float, default=420.0,
                    help="hard cap on autotuning wall time (once any candidate has succeeded)")
     p.add_argument("--no-validate", dest="validate", action="store_false", default=True)
     p.add_argument("--prewarm-ms", type=float, default=300.0,

@@ -61,6 +61,7 @@ struct GemmArgs {
   // at producer 0..np-1 | READY words (ready[p] >= epoch: p's rows may be read) | counters
   // (nshards per-segment, then np per-producer; monotonic across runs)].
   int ag_ctas = 0, ag_parts = 1, ag_rank = 0;
+  int ag_mode = 0;                  // AgMode bits below
   const uint64_t* ag_tab = nullptr;
   int act = 0;                      // fused epilogue activation: ACT_* below
   // Direct-access A (optional): row block s of shard_rows rows starts at a_table[s] (device
@@ -69,6 +70,13 @@ struct GemmArgs {
   int64_t shard_rows = 0;
 };
 enum Act : int { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_SILU = 3 };
+// In-kernel all-gather variants (GemmArgs::ag_mode; default 0 = write-through publication, 8
+// loads in flight per lane, system-scope acquire in the GEMM gate).
+enum AgMode : int {
+  AG_LEGACY_PUBLISH = 1,   // plain stores + agent release fence per unit (the first version)
+  AG_AGENT_ACQUIRE = 2,    // the gated tiles acquire at agent scope (flags set by this launch)
+  AG_DEEP_LOADS = 4,       // 16 loads in flight per lane instead of 8
+};
 
 hipError_t gemm_launch(const GemmArgs& p, int din, int dout, int tile, int mode, hipStream_t s);
 bool gemm_fast_path_ok(const GemmArgs& p, int din, int dout);

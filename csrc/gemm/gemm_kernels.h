@@ -219,7 +219,13 @@ __device__ __forceinline__ void wait_flag_t0(const GemmArgs& p, int64_t row_firs
         }
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
+    // system scope: the rows were written by a copy engine or a peer GPU. When only this
+    // launch's own copy workgroups set the flags (in-kernel all-gather, AG_AGENT_ACQUIRE) an
+    // agent-scope acquire covers them (write-through stores, MI355X guide §6 Guideline 16 R1).
+    if (p.ag_mode & AG_AGENT_ACQUIRE)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    else
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   }
 }
 
@@ -233,23 +239,55 @@ __device__ __forceinline__ void wait_flag(const GemmArgs& p, int64_t row_first, 
 // The copy workgroups of a flag-gated pt4 launch (GemmArgs::ag_ctas). Work units are
 // (block, producer, part), block-major and producers in ring order from rank + 1: the order the
 // gated GEMM dispatches its tiles in (ordered_shard). Each unit is a contiguous byte range of
-// the same rows in the producer's A and ours; 8 x 16-byte loads in flight per thread. After a
-// unit every thread releases its stores at agent scope (L2 written back: the GEMM tile reading
-// these rows may sit on another XCD), then thread 0 counts the unit; the last part of a
-// segment publishes its flag, the last unit of a producer ACKs it (system scope, over xGMI).
+// the same rows in the producer's A and ours; U x 16-byte loads in flight per thread.
+// Publication (default, MI355X guide §6 Guideline 16 R1): the payload is stored WRITE-THROUGH
+// (16-byte `sc1` buffer stores), every wave drains its stores (vmcnt(0)), a workgroup barrier,
+// then thread 0 counts the unit with a relaxed agent atomic; the last part of a segment sets its
+// flag (atomic store), the last unit of a producer ACKs it over xGMI. No release fence: an
+// agent-scope release is a `buffer_wbl2` of the whole XCD L2, dirty C tiles of the GEMM
+// workgroups on that XCD included, once per unit. AG_LEGACY_PUBLISH keeps the plain-store +
+// release-fence form for comparison (scripts/bench_agk_world1.py).
+typedef __attribute__((ext_vector_type(4))) unsigned ag_u32x4;
+template <int U, bool WT>
+__device__ __forceinline__ void ag_copy_bytes(const GLB_AS ag_u32x4* src, char* dst, int64_t nvec,
+                                              int tid) {
+  constexpr int T = 512;
+  // wave-uniform descriptor over this unit (a unit is < 1 GiB, checked at launch)
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc((void*)dst, 0, (int)(nvec * 16), 0x00020000);
+  GLB_AS ag_u32x4* d = (GLB_AS ag_u32x4*)dst;
+  auto st = [&](int64_t v, ag_u32x4 x) __attribute__((always_inline)) {
+    if constexpr (WT)
+      __builtin_amdgcn_raw_buffer_store_b128(x, r, (unsigned)(v * 16), 0, 16 /* sc1 */);
+    else
+      d[v] = x;
+  };
+  int64_t v = tid;
+  for (; v + (U - 1) * T < nvec; v += U * T) {
+    ag_u32x4 x[U];
+#pragma unroll
+    for (int i = 0; i < U; ++i) x[i] = src[v + i * T];
+#pragma unroll
+    for (int i = 0; i < U; ++i) st(v + i * T, x[i]);
+  }
+  for (; v < nvec; v += T) st(v, src[v]);
+}
+
 template <int ESZ>
 __device__ __forceinline__ void ag_copy_role(const GemmArgs& p) {
   const unsigned want = p.epoch_ptr ? *p.epoch_ptr : p.epoch;
   const int np = p.nshards / p.nsub, s = p.nsub, parts = p.ag_parts;
   const uint64_t* tab = p.ag_tab;
-  const unsigned* ready = (const unsigned*)tab[2 * np];
-  unsigned* count = (unsigned*)tab[2 * np + 1];
-  unsigned* arrive = const_cast<unsigned*>(p.flags);
+  // every shared word is a GLOBAL (never flat) access
+  const GLB_AS unsigned* ready = (const GLB_AS unsigned*)tab[2 * np];
+  GLB_AS unsigned* count = (GLB_AS unsigned*)tab[2 * np + 1];
+  GLB_AS unsigned* arrive = (GLB_AS unsigned*)p.flags;
   const int64_t seg = p.flag_rows * p.lda * ESZ;
   const int64_t part = (seg / parts + 15) / 16 * 16;
   const int per_b = (np - 1) * parts, units = s * per_b;
   const int tid = threadIdx.x;
-  constexpr int T = 512, U = 8;
+  const bool legacy = (p.ag_mode & AG_LEGACY_PUBLISH) != 0;
+  const bool deep = (p.ag_mode & AG_DEEP_LOADS) != 0;
   unsigned seen = 0;
   for (int u = (int)blockIdx.x; u < units; u += p.ag_ctas) {
     const int b = u / per_b, r = u % per_b;
@@ -273,28 +311,31 @@ __device__ __forceinline__ void ag_copy_role(const GemmArgs& p) {
     const int64_t base = (int64_t)(prod * s + b) * seg + (int64_t)pi * part;
     int64_t nb = seg - (int64_t)pi * part;
     nb = nb < part ? nb : part;
-    const uint4* src = (const uint4*)((const char*)tab[prod] + base);
-    uint4* dst = (uint4*)((char*)p.a + base);
+    const GLB_AS ag_u32x4* src = (const GLB_AS ag_u32x4*)(tab[prod] + base);
+    char* dst = (char*)p.a + base;
     const int64_t nvec = nb > 0 ? nb / 16 : 0;
-    int64_t v = tid;
-    for (; v + (U - 1) * T < nvec; v += U * T) {
-      uint4 x[U];
-#pragma unroll
-      for (int i = 0; i < U; ++i) x[i] = src[v + i * T];
-#pragma unroll
-      for (int i = 0; i < U; ++i) dst[v + i * T] = x[i];
+    if (legacy) {
+      ag_copy_bytes<8, false>(src, dst, nvec, tid);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    } else {
+      if (deep)
+        ag_copy_bytes<16, true>(src, dst, nvec, tid);
+      else
+        ag_copy_bytes<8, true>(src, dst, nvec, tid);
+      // every wave drains its write-through stores (and its peer loads) before the count
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    for (; v < nvec; v += T) dst[v] = src[v];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __syncthreads();
     if (tid == 0) {
       const int sh = prod * s + b;
       if (__hip_atomic_fetch_add(count + sh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 ==
           want * (unsigned)parts)
-        __hip_atomic_store(arrive + sh, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(arrive + sh, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // ACK: every load of the producer's rows by this unit has returned (vmcnt(0) / the
+      // release above), so a relaxed store suffices; it crosses xGMI, hence system scope
       if (__hip_atomic_fetch_add(count + np * s + prod, 1u, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT) + 1 == want * (unsigned)(s * parts))
-        __hip_atomic_store((unsigned*)tab[np + prod], want, __ATOMIC_RELEASE,
+        __hip_atomic_store((GLB_AS unsigned*)tab[np + prod], want, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }

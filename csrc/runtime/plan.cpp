@@ -231,6 +231,7 @@ GemmArgs PlanExecutor::gemm_args(const int64_t* o) const {
   g.ag_ctas = (int)(o[29] & 0xfffff);
   g.ag_parts = (int)((o[29] >> 20) & 0xfffff);
   g.ag_rank = (int)((o[29] >> 40) & 0xffff);
+  g.ag_mode = (int)((o[29] >> 56) & 0x7f);
   g.ag_tab = (const uint64_t*)o[30];
   g.act = (int)o[24];
   g.a_table = (const uint64_t*)o[25];

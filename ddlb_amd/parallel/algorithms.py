@@ -70,6 +70,7 @@ class AlgoConfig:
     fused: bool = False                 # columnwise p2p / coll: one flag-gated GEMM launch
     reserve_cus: int = 32               # fused: CUs the persistent gated GEMM leaves free
     ag_reserve: int = 0                 # in-kernel all-gather: CUs left free besides its copiers
+    ag_mode: int = 0                    # in-kernel all-gather variant (csrc/gemm/gemm.h AgMode)
     act: int = 0                        # columnwise: fused GEMM epilogue activation (ACT_*)
     direction: str = "pull"             # columnwise ipc: pull peers' shards | push mine to peers
 
@@ -266,7 +267,7 @@ def build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, dou
         ag = dict(ctas=cfg.copy_blocks, parts=max(1, min(seg // (256 << 10), 1024)), rank=rank,
                   src=[A.at(p) for p in range(d)],
                   ack=[flags.ref("ACK", rank, owner=p) for p in range(d)],
-                  ready=flags.ref("READY", 0), count=flags.ref("CNT", 0))
+                  ready=flags.ref("READY", 0), count=flags.ref("CNT", 0), mode=cfg.ag_mode)
         gdt_ag = dict(gdt, tile=TILE_PT4)
         plan.gemm(S_MAIN, A, Bt, C, M=m, N=n, K=k, lda=k, ldb=k, ldc=n, **gdt_ag,
                   flags=flags.ref("ARRIVE", 0), flag_rows=rows, nshards=d * cfg.s, nsub=cfg.s,
@@ -610,6 +611,9 @@ def check_rowwise(d: int, m: int, n: int, k: int, cfg: AlgoConfig) -> None:
     if cfg.direction != "pull":
         raise ValueError("direction=push is a tp_columnwise all-gather option (the rowwise "
                          "p2p_pipeline already pushes its partials)")
+    if cfg.fused:
+        raise ValueError("fused=True (flag-gated GEMM over arriving rows) is a tp_columnwise "
+                         "all-gather option")
     if d > 16:
         raise ValueError("at most 16 ranks per node are supported by the reduce op")
 
@@ -659,41 +663,6 @@ def build_tp_rowwise(rank: int, d: int, m: int, n: int, k: int, din: int, dout: 
             gemm(S_MAIN, j * rows, stg, d * rows, a_grp=rows, a_gstride=ml)
             plan.edge(S_MAIN, S_COMM)
             plan.reduce_scatter(S_COMM, stg, OUT + j * rows * n * eout, rows * n, dout)
-    elif alg == "coll_pipeline" and be == "ipc" and cfg.fused and cfg.protocol == "kernel":
-        # In-kernel all-gather: ONE launch. Its first copy_blocks workgroups pull row block b
-        # of every peer over xGMI (block-major, ring order) and set ARRIVE[p * s + b] when a
-        # block has landed; the other workgroups run the persistent GEMM gated on those flags
-        # (csrc/gemm/gemm_kernels.h ag_copy_role). No copy streams, no host op per block:
-        # READY out, own blocks marked, one kernel, ACKs back.
-        rows = ml // cfg.s
-        _signal(plan, S_MAIN, [flags.ref("READY", rank, owner=p) for p in range(d) if p != rank],
-                cfg)
-        _signal(plan, S_MAIN, [flags.ref("ARRIVE", rank * cfg.s + j) for j in range(cfg.s)], cfg)
-        seg = rows * k * ein
-        ag = dict(ctas=cfg.copy_blocks, parts=max(1, min(seg // (256 << 10), 1024)), rank=rank,
-                  src=[A.at(p) for p in range(d)],
-                  ack=[flags.ref("ACK", rank, owner=p) for p in range(d)],
-                  ready=flags.ref("READY", 0), count=flags.ref("CNT", 0))
-        gdt_ag = dict(gdt, tile=TILE_PT4)
-        plan.gemm(S_MAIN, A, Bt, C, M=m, N=n, K=k, lda=k, ldb=k, ldc=n, **gdt_ag,
-                  flags=flags.ref("ARRIVE", 0), flag_rows=rows, nshards=d * cfg.s, nsub=cfg.s,
-                  first_shard=rank, tile_order=1, reserve_cus=cfg.ag_reserve, ag=ag)
-        _wait(plan, S_MAIN, [flags.ref("ACK", p) for p in range(d) if p != rank], cfg)
-    elif alg == "coll_pipeline" and be == "ipc" and cfg.fused:
-        # ONE flag-gated GEMM over all m rows instead of s stage GEMMs: tiles are dispatched
-        # block-major (block 0 of the own shard and of every peer, then block 1, ...), the order
-        # the chunked pulls land in, and each tile spins until its row block's ARRIVE flag is set
-        # by the copy stream that pulled it; no stage boundaries, no per-stage GEMM tail.
-        rows = ml // cfg.s
-        peers = _peer_order(rank, d, cfg.ring)
-        jobs = [(p, [(p * ml + j * rows, rows) for j in range(cfg.s)]) for p in peers]
-        _ipc_pull_shards(plan, rank, d, cfg, flags, jobs, lambda r0: arow(r0), k * ein,
-                         arrive_block=lambda p, b: flags.ref("ARRIVE", p * cfg.s + b))
-        # enqueued after the pulls (every dependency points backwards in enqueue order)
-        _signal(plan, S_MAIN, [flags.ref("ARRIVE", rank * cfg.s + j) for j in range(cfg.s)], cfg)
-        gemm(S_MAIN, A, C, m, flags=flags.ref("ARRIVE", 0), flag_rows=rows, nshards=d * cfg.s,
-             nsub=cfg.s, first_shard=rank, tile_order=1, reserve_cus=cfg.reserve_cus)
-        _wait(plan, S_MAIN, [flags.ref("ACK", p) for p in range(d) if p != rank], cfg)
     elif alg == "coll_pipeline" and be == "ipc":
         rows = ml // cfg.s
         sblk = rows * n * eout

@@ -141,6 +141,8 @@ class Plan:
                 raise ValueError("in-kernel all-gather needs flags and one src / ack per producer")
             if not 1 <= ag["ctas"] < 1 << 20 or not 1 <= ag["parts"] < 1 << 20:
                 raise ValueError("ag ctas / parts out of range")
+            if not 0 <= ag.get("mode", 0) < 8:
+                raise ValueError("ag mode out of range (csrc/gemm/gemm.h AgMode bits)")
             ag = dict(ag, table=self.table(f"__agtab{len(self.buffers)}",
                                            list(ag["src"]) + list(ag["ack"]) +
                                            [ag["ready"], ag["count"]]))
@@ -247,7 +249,8 @@ class Plan:
                 w[27], w[28] = a.get("nsub", 1), a.get("reserve_cus", 0)
                 g = a.get("ag")
                 if g is not None:
-                    w[29] = g["ctas"] | (g["parts"] << 20) | (g["rank"] << 40)
+                    w[29] = (g["ctas"] | (g["parts"] << 20) | (g["rank"] << 40) |
+                             (g.get("mode", 0) << 56))
                     w[30] = resolve(g["table"])
             elif k in (OP_RECORD, OP_WAIT):
                 w[2] = a["event"]

@@ -28,7 +28,9 @@ arrival-flag-gated GEMM; ``reserve_cus`` = CUs its persistent form leaves free f
 kernels that set the flags), ``graph`` (capture the plan once and replay it as one hipGraph launch;
 signal plans read a device-side run counter; not for plans with RCCL calls; ``auto`` = whenever
 capturable and the process has >= 4 HW queues), ``direction`` (columnwise ipc: ``pull`` peers' shards, or
-``push`` my shard into every peer's gather buffer with posted xGMI writes).
+``push`` my shard into every peer's gather buffer with posted xGMI writes), ``ag_mode`` (the in-kernel
+all-gather's copy variant, csrc/gemm/gemm.h ``AgMode`` bits: 1 plain stores + release fence instead
+of write-through stores, 2 agent-scope acquire in the gated tiles, 4 16 loads in flight per lane).
 """
 
 from __future__ import annotations
@@ -53,6 +55,7 @@ COMMON_DEFAULTS = {
     "reserve_cus": 32,
     "graph": False,
     "direction": "pull",
+    "ag_mode": 0,
 }
 COMMON_ALLOWED = {
     "backend": ["rccl", "ipc", *UCC_BACKENDS],
@@ -72,6 +75,7 @@ COMMON_ALLOWED = {
     "reserve_cus": (0, 1024),
     "graph": [True, False, "auto"],
     "direction": ["pull", "push"],
+    "ag_mode": (0, 7),
 }
 COMMON_ALIASES = {
     "backend": {"nccl": "rccl", "cuda": "ipc"},
@@ -106,7 +110,7 @@ def algo_config(options, order: str = "AG_before") -> AlgoConfig:
         copy_blocks=int(options["copy_blocks"]), fused=bool(options["fused"]),
         reserve_cus=int(options.get("reserve_cus", 32)),
         copy_streams=int(options.get("copy_streams", 1)),
-        direction=options.get("direction", "pull"))
+        direction=options.get("direction", "pull"), ag_mode=int(options.get("ag_mode", 0)))
 
 
 def share_cus(cfg: AlgoConfig, communicator) -> AlgoConfig:

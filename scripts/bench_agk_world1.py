@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def build(M, N, K, npro, nsub, ctas, gated=True, unit_kb=256):
+def build(M, N, K, npro, nsub, ctas, gated=True, unit_kb=256, mode=0):
     from ddlb_amd.parallel.plan import DT_BF16, Plan, SIG_KERNEL
 
     rows = M // (npro * nsub)
@@ -34,7 +34,7 @@ def build(M, N, K, npro, nsub, ctas, gated=True, unit_kb=256):
     seg = rows * K * 2
     ag = dict(ctas=ctas, parts=max(1, seg // (unit_kb << 10)), rank=0,
               src=[a] + [peer] * (npro - 1), ack=[ACK + 4 * p for p in range(npro)],
-              ready=READY, count=CNT)
+              ready=READY, count=CNT, mode=mode)
     plan.gemm(0, a, bt, c, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, din=DT_BF16, dout=DT_BF16,
               tile=19, flags=ARRIVE, flag_rows=rows, nshards=npro * nsub, nsub=nsub,
               first_shard=0, tile_order=1, ag=ag)
@@ -54,6 +54,9 @@ def main():
     ap.add_argument("--ctas", default="32,64")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--unit-kb", default="256", help="copy unit sizes (KiB) to try")
+    ap.add_argument("--modes", default="0",
+                    help="ag_mode bit sets to try (csrc/gemm/gemm.h AgMode: 1 legacy plain "
+                         "stores + release fence, 2 agent-scope gate acquire, 4 16 loads/lane)")
     a = ap.parse_args()
     M, N, K = 65536, 1024, 1024
     import socket
@@ -69,11 +72,11 @@ def main():
     W = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
     ref = A.float() @ W.float().T
     own = M // a.np
-    variants = [("pt4 GEMM only", 0, False, 0)] + [
-        (f"agk ctas={c} unit={u}K", int(c), True, int(u)) for c in a.ctas.split(",")
-        for u in a.unit_kb.split(",")]
-    for label, ctas, gated, unit in variants:
-        bound = ctx.bind(build(M, N, K, a.np, a.nsub, ctas, gated, unit or 256))
+    variants = [("pt4 GEMM only", 0, False, 0, 0)] + [
+        (f"agk ctas={c} unit={u}K mode={md}", int(c), True, int(u), int(md))
+        for c in a.ctas.split(",") for u in a.unit_kb.split(",") for md in a.modes.split(",")]
+    for label, ctas, gated, unit, mode in variants:
+        bound = ctx.bind(build(M, N, K, a.np, a.nsub, ctas, gated, unit or 256, mode))
         bound.enable_graph(True)
         av = bound.buffer("a").view(torch.bfloat16).view(M, K)
         av.copy_(A)
@@ -91,10 +94,15 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         bound.check_health()
+        if gated:  # one more run from poisoned peer rows: this run's copies must land
+            av[own:].fill_(float("nan"))
+            bound.run()
+            torch.cuda.synchronize()
+            bound.check_health()
         out = bound.buffer("c").view(torch.bfloat16).view(M, N).float()
         err = (out - ref).abs().max().item()
         ms = e0.elapsed_time(e1) / a.iters
-        print(f"{label:>22}: {ms * 1e3:7.1f} us/run  {2 * M * N * K / ms / 1e9:7.0f} TFLOP/s  "
+        print(f"{label:>34}: {ms * 1e3:7.1f} us/run  {2 * M * N * K / ms / 1e9:7.0f} TFLOP/s  "
               f"copied {(M - own) * K * 2 / 2**20 if gated else 0:.0f} MiB  max|err| {err:.3f}",
               flush=True)
         bound.close()

@@ -447,12 +447,15 @@ def test_flag_gated_persistent_gemm_world1(comm, graph):
     ctx.close()
 
 
+@pytest.mark.parametrize("mode", [0, 1, 6])
 @pytest.mark.parametrize("graph", [False, True])
-def test_in_kernel_allgather_world1(comm, graph):
+def test_in_kernel_allgather_world1(comm, graph, mode):
     """The in-kernel all-gather in one process: a local buffer stands in for the peer's copy of
     A (same rows), READY is signalled locally, the peer's rows of the gather buffer are NaN
     before each run; the copy workgroups must pull them, flag each block, ACK, and the gated
-    GEMM tiles must wait for them (C checked against fp32 every run)."""
+    GEMM tiles must wait for them (C checked against fp32 every run). ``mode``: the copy role's
+    publication variants (csrc/gemm/gemm.h AgMode: 0 write-through stores, 1 plain stores +
+    release fence, 6 write-through + 16 loads per lane + agent-scope gate acquire)."""
     from ddlb_amd.parallel.context import NativeContext
     from ddlb_amd.parallel.plan import DT_BF16, Plan, SIG_KERNEL, SIG_STREAM
 
@@ -469,7 +472,7 @@ def test_in_kernel_allgather_world1(comm, graph):
     plan.signal(0, [READY + 4], method=sig)
     plan.signal(0, [ARRIVE + 4 * j for j in range(nsub)], method=sig)
     ag = dict(ctas=32, parts=8, rank=0, src=[a, peer], ack=[ACK, ACK + 4], ready=READY,
-              count=CNT)
+              count=CNT, mode=mode)
     plan.gemm(0, a, bt, c, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, din=DT_BF16, dout=DT_BF16,
               tile=19, flags=ARRIVE, flag_rows=rows, nshards=2 * nsub, nsub=nsub, first_shard=0,
               tile_order=1, ag=ag)

@@ -111,6 +111,16 @@ def test_push_rejected_where_meaningless():
                                                                      direction="push"))
 
 
+@pytest.mark.parametrize("protocol", ["memcpy", "kernel"])
+def test_rowwise_rejects_fused(protocol):
+    """fused (flag-gated GEMM over arriving A rows) only exists for the columnwise all-gather;
+    the rowwise builder must refuse it up front, not fail while building."""
+    cfg = AlgoConfig(algorithm="coll_pipeline", backend="ipc", s=2, fused=True,
+                     protocol=protocol)
+    with pytest.raises(ValueError, match="tp_columnwise"):
+        build_tp_rowwise(0, 2, 16, 8, 8, DT_F32, DT_F32, cfg)
+
+
 @pytest.mark.parametrize("fused", [True, False])
 def test_p2p_fused_plan(fused):
     cfg = AlgoConfig(algorithm="p2p_pipeline", backend="ipc", fused=fused)
