@@ -30,7 +30,8 @@ signal plans read a device-side run counter; not for plans with RCCL calls; ``au
 capturable and the process has >= 4 HW queues), ``direction`` (columnwise ipc: ``pull`` peers' shards, or
 ``push`` my shard into every peer's gather buffer with posted xGMI writes), ``ag_mode`` (the in-kernel
 all-gather's copy variant, csrc/gemm/gemm.h ``AgMode`` bits: 1 plain stores + release fence instead
-of write-through stores, 2 agent-scope acquire in the gated tiles, 4 16 loads in flight per lane).
+of write-through stores, 2 agent-scope acquire in the gated tiles, 4 16 loads in flight per lane;
+default 6).
 """
 
 from __future__ import annotations
@@ -55,7 +56,7 @@ COMMON_DEFAULTS = {
     "reserve_cus": 32,
     "graph": False,
     "direction": "pull",
-    "ag_mode": 0,
+    "ag_mode": 6,
 }
 COMMON_ALLOWED = {
     "backend": ["rccl", "ipc", *UCC_BACKENDS],
@@ -110,7 +111,7 @@ def algo_config(options, order: str = "AG_before") -> AlgoConfig:
         copy_blocks=int(options["copy_blocks"]), fused=bool(options["fused"]),
         reserve_cus=int(options.get("reserve_cus", 32)),
         copy_streams=int(options.get("copy_streams", 1)),
-        direction=options.get("direction", "pull"), ag_mode=int(options.get("ag_mode", 0)))
+        direction=options.get("direction", "pull"), ag_mode=int(options.get("ag_mode", 6)))
 
 
 def share_cus(cfg: AlgoConfig, communicator) -> AlgoConfig:
