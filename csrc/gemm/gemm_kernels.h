@@ -237,9 +237,10 @@ __device__ __forceinline__ void wait_flag(const GemmArgs& p, int64_t row_first, 
 
 // ---------------------------------------------------------------- in-kernel all-gather
 // The copy workgroups of a flag-gated pt4 launch (GemmArgs::ag_ctas). Work units are
-// (block, producer, part), block-major and producers in ring order from rank + 1: the order the
-// gated GEMM dispatches its tiles in (ordered_shard). Each unit is a contiguous byte range of
-// the same rows in the producer's A and ours; U x 16-byte loads in flight per thread.
+// (block, part, producer), block-major with producers in ring order from rank + 1 innermost: the
+// block order the gated GEMM dispatches its tiles in (ordered_shard), all links busy at once.
+// Each unit is a contiguous byte range of the same rows in the producer's A and ours; U x 16-byte
+// loads in flight per thread.
 // Publication (default, MI355X guide §6 Guideline 16 R1): the payload is stored WRITE-THROUGH
 // (16-byte `sc1` buffer stores), every wave drains its stores (vmcnt(0)), a workgroup barrier,
 // then thread 0 counts the unit with a relaxed agent atomic; the last part of a segment sets its
@@ -290,8 +291,10 @@ __device__ __forceinline__ void ag_copy_role(const GemmArgs& p) {
   const bool deep = (p.ag_mode & AG_DEEP_LOADS) != 0;
   unsigned seen = 0;
   for (int u = (int)blockIdx.x; u < units; u += p.ag_ctas) {
+    // within a block, consecutive units go to different producers: the ag_ctas units in flight
+    // at any time spread over every peer (every xGMI link) instead of ~ag_ctas / parts of them
     const int b = u / per_b, r = u % per_b;
-    const int prod = (p.ag_rank + 1 + r / parts) % np, pi = r % parts;
+    const int prod = (p.ag_rank + 1 + r % (np - 1)) % np, pi = r / (np - 1);
     if (!((seen >> prod) & 1u)) {  // first unit of this producer: its READY, acquired
       if (tid == 0) {
         unsigned spins = 0;

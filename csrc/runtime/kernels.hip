@@ -137,19 +137,19 @@ __global__ __launch_bounds__(256) void reduce_sum_fixed_kernel(ReduceArgs a) {
 
 // Blocks are dealt round-robin to the segments (one segment = one peer = one xGMI link in the
 // IPC all-gathers), so every link carries traffic at once; the blocks of a segment grid-stride
-// over it with 4 x 16 B in flight per lane. (Walking the segments one after another would keep
-// a single link busy at a time: d-1 times the transfer time of a full-mesh exchange.)
+// over it with U x 16 B in flight per lane (8 by default: a peer read over xGMI has several times
+// the latency of local HBM, and bytes in flight per CU are what bound a latency-bound pull).
+// (Walking the segments one after another would keep a single link busy at a time: d-1 times the
+// transfer time of a full-mesh exchange.)
 template <bool NT>  // NT: non-temporal source loads (each source byte is read exactly once)
-__device__ __forceinline__ uint4 copy_ld(const char* p) {
-  if constexpr (NT) {
-    const u32x4 v = __builtin_nontemporal_load((const u32x4*)p);
-    return uint4{v.x, v.y, v.z, v.w};
-  } else {
-    return *(const uint4*)p;
-  }
+__device__ __forceinline__ u32x4 copy_ld(const char* p) {
+  if constexpr (NT)
+    return __builtin_nontemporal_load((const u32x4*)p);
+  else
+    return *(const u32x4*)p;
 }
 
-template <bool NT>
+template <bool NT, int U>
 __global__ __launch_bounds__(256) void copy_kernel(CopyArgs a) {
   const int nseg = a.nseg;
   const int seg = (int)blockIdx.x % nseg;
@@ -161,17 +161,14 @@ __global__ __launch_bounds__(256) void copy_kernel(CopyArgs a) {
   const int64_t bytes = a.bytes[seg];
   const int64_t nvec = bytes / 16;
   int64_t v = t0;
-  for (; v + 3 * stride < nvec; v += 4 * stride) {
-    const uint4 x0 = copy_ld<NT>(src + v * 16);
-    const uint4 x1 = copy_ld<NT>(src + (v + stride) * 16);
-    const uint4 x2 = copy_ld<NT>(src + (v + 2 * stride) * 16);
-    const uint4 x3 = copy_ld<NT>(src + (v + 3 * stride) * 16);
-    *(uint4*)(dst + v * 16) = x0;
-    *(uint4*)(dst + (v + stride) * 16) = x1;
-    *(uint4*)(dst + (v + 2 * stride) * 16) = x2;
-    *(uint4*)(dst + (v + 3 * stride) * 16) = x3;
+  for (; v + (U - 1) * stride < nvec; v += U * stride) {
+    u32x4 x[U];
+#pragma unroll
+    for (int i = 0; i < U; ++i) x[i] = copy_ld<NT>(src + (v + i * stride) * 16);
+#pragma unroll
+    for (int i = 0; i < U; ++i) *(u32x4*)(dst + (v + i * stride) * 16) = x[i];
   }
-  for (; v < nvec; v += stride) *(uint4*)(dst + v * 16) = copy_ld<NT>(src + v * 16);
+  for (; v < nvec; v += stride) *(u32x4*)(dst + v * 16) = copy_ld<NT>(src + v * 16);
   for (int64_t b = nvec * 16 + t0; b < bytes; b += stride) dst[b] = src[b];
 }
 
@@ -259,9 +256,13 @@ hipError_t copy_launch(const CopyArgs& a, int max_blocks, hipStream_t s) {
   g = g < a.nseg ? a.nseg : (g / a.nseg) * a.nseg;
   // Plain loads by default: non-temporal source loads measured slower on HBM (7 x 16 MiB:
   // 52 vs 34 us at 128 blocks, 36 vs 35 at 512; profiles/r01/s3/copy_ab_nt.txt). A/B knob kept.
+  // DDLB_COPY_U=4: the earlier 4 loads in flight per lane (A/B knob).
   static const bool nt = getenv("DDLB_COPY_NT") != nullptr;
-  if (nt) hipLaunchKernelGGL(copy_kernel<true>, dim3(g), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(copy_kernel<false>, dim3(g), dim3(256), 0, s, a);
+  static const bool u4 = getenv("DDLB_COPY_U") != nullptr && atoi(getenv("DDLB_COPY_U")) == 4;
+  if (nt && u4) hipLaunchKernelGGL((copy_kernel<true, 4>), dim3(g), dim3(256), 0, s, a);
+  else if (nt) hipLaunchKernelGGL((copy_kernel<true, 8>), dim3(g), dim3(256), 0, s, a);
+  else if (u4) hipLaunchKernelGGL((copy_kernel<false, 4>), dim3(g), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((copy_kernel<false, 8>), dim3(g), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
