@@ -70,12 +70,14 @@ struct GemmArgs {
   int64_t shard_rows = 0;
 };
 enum Act : int { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_SILU = 3 };
-// In-kernel all-gather variants (GemmArgs::ag_mode; default 0 = write-through publication, 8
-// loads in flight per lane, system-scope acquire in the GEMM gate).
+// In-kernel all-gather variants (GemmArgs::ag_mode bits; 0 = write-through publication, 8 loads
+// in flight per lane, system-scope acquire in the GEMM gate; the plan builders pick the default,
+// ddlb_amd/parallel/algorithms.py AlgoConfig.ag_mode).
 enum AgMode : int {
   AG_LEGACY_PUBLISH = 1,   // plain stores + agent release fence per unit (the first version)
   AG_AGENT_ACQUIRE = 2,    // the gated tiles acquire at agent scope (flags set by this launch)
   AG_DEEP_LOADS = 4,       // 16 loads in flight per lane instead of 8
+  AG_FILL_ROUNDS = 8,      // grow ag_ctas while the GEMM's number of tile rounds stays the same
 };
 
 hipError_t gemm_launch(const GemmArgs& p, int din, int dout, int tile, int mode, hipStream_t s);

@@ -2241,6 +2241,15 @@ hipError_t launch_pt4(const GemmArgs& p, hipStream_t s) {
   if (p.flags != nullptr && p.reserve_cus > 0) grid -= p.reserve_cus;
   GemmArgs q = p;
   q.ag_ctas = p.flags != nullptr && p.ag_ctas > 0 ? (p.ag_ctas + 7) / 8 * 8 : 0;
+  if (q.ag_ctas > 0 && (p.ag_mode & AG_FILL_ROUNDS) && grid - q.ag_ctas >= 8) {
+    // The GEMM takes ceil(tiles / gemm_ctas) rounds of tiles; every copy workgroup that leaves
+    // that count unchanged is free copy bandwidth (flagship: 1024 tiles, 224 GEMM CTAs = 5
+    // rounds, so 208 GEMM + 48 copy CTAs cost the GEMM nothing more than 224 + 32).
+    const int g0 = (grid - q.ag_ctas) / 8 * 8;
+    const int rounds = (tiles + g0 - 1) / g0;
+    const int need = ((tiles + rounds - 1) / rounds + 7) / 8 * 8;
+    if (grid - need > q.ag_ctas) q.ag_ctas = (grid - need) / 8 * 8;
+  }
   grid -= q.ag_ctas;
   grid = (grid / 8) * 8;  // blockIdx % 8 == XCD group for every virtual tile id
   if (grid > tiles) grid = tiles;

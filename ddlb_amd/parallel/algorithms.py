@@ -70,10 +70,11 @@ class AlgoConfig:
     fused: bool = False                 # columnwise p2p / coll: one flag-gated GEMM launch
     reserve_cus: int = 32               # fused: CUs the persistent gated GEMM leaves free
     ag_reserve: int = 0                 # in-kernel all-gather: CUs left free besides its copiers
-    # in-kernel all-gather variant (csrc/gemm/gemm.h AgMode): 6 = write-through publication, 16
+    # in-kernel all-gather variant (csrc/gemm/gemm.h AgMode): 14 = write-through publication, 16
     # loads in flight per lane, agent-scope gate acquire (the fastest at world 1,
-    # profiles/r02/s4/r2s4_2_agk_world1_modes.txt)
-    ag_mode: int = 6
+    # profiles/r02/s4/r2s4_2_agk_world1_modes.txt), copy workgroups grown while the GEMM's tile
+    # rounds stay the same (flagship: 48 instead of 32 at no GEMM cost, r2s4_5_*)
+    ag_mode: int = 14
     act: int = 0                        # columnwise: fused GEMM epilogue activation (ACT_*)
     direction: str = "pull"             # columnwise ipc: pull peers' shards | push mine to peers
 

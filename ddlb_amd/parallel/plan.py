@@ -141,7 +141,7 @@ class Plan:
                 raise ValueError("in-kernel all-gather needs flags and one src / ack per producer")
             if not 1 <= ag["ctas"] < 1 << 20 or not 1 <= ag["parts"] < 1 << 20:
                 raise ValueError("ag ctas / parts out of range")
-            if not 0 <= ag.get("mode", 0) < 8:
+            if not 0 <= ag.get("mode", 0) < 16:
                 raise ValueError("ag mode out of range (csrc/gemm/gemm.h AgMode bits)")
             ag = dict(ag, table=self.table(f"__agtab{len(self.buffers)}",
                                            list(ag["src"]) + list(ag["ack"]) +

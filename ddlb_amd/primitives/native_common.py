@@ -30,8 +30,9 @@ signal plans read a device-side run counter; not for plans with RCCL calls; ``au
 capturable and the process has >= 4 HW queues), ``direction`` (columnwise ipc: ``pull`` peers' shards, or
 ``push`` my shard into every peer's gather buffer with posted xGMI writes), ``ag_mode`` (the in-kernel
 all-gather's copy variant, csrc/gemm/gemm.h ``AgMode`` bits: 1 plain stores + release fence instead
-of write-through stores, 2 agent-scope acquire in the gated tiles, 4 16 loads in flight per lane;
-default 6).
+of write-through stores, 2 agent-scope acquire in the gated tiles, 4 16 loads in flight per lane,
+8 more copy workgroups while the GEMM's tile rounds stay the same;
+default 14).
 """
 
 from __future__ import annotations
@@ -56,7 +57,7 @@ COMMON_DEFAULTS = {
     "reserve_cus": 32,
     "graph": False,
     "direction": "pull",
-    "ag_mode": 6,
+    "ag_mode": 14,
 }
 COMMON_ALLOWED = {
     "backend": ["rccl", "ipc", *UCC_BACKENDS],
@@ -76,7 +77,7 @@ COMMON_ALLOWED = {
     "reserve_cus": (0, 1024),
     "graph": [True, False, "auto"],
     "direction": ["pull", "push"],
-    "ag_mode": (0, 7),
+    "ag_mode": (0, 15),
 }
 COMMON_ALIASES = {
     "backend": {"nccl": "rccl", "cuda": "ipc"},
@@ -111,7 +112,7 @@ def algo_config(options, order: str = "AG_before") -> AlgoConfig:
         copy_blocks=int(options["copy_blocks"]), fused=bool(options["fused"]),
         reserve_cus=int(options.get("reserve_cus", 32)),
         copy_streams=int(options.get("copy_streams", 1)),
-        direction=options.get("direction", "pull"), ag_mode=int(options.get("ag_mode", 6)))
+        direction=options.get("direction", "pull"), ag_mode=int(options.get("ag_mode", 14)))
 
 
 def share_cus(cfg: AlgoConfig, communicator) -> AlgoConfig:

@@ -447,7 +447,7 @@ def test_flag_gated_persistent_gemm_world1(comm, graph):
     ctx.close()
 
 
-@pytest.mark.parametrize("mode", [0, 1, 6])
+@pytest.mark.parametrize("mode", [0, 1, 6, 14])
 @pytest.mark.parametrize("graph", [False, True])
 def test_in_kernel_allgather_world1(comm, graph, mode):
     """The in-kernel all-gather in one process: a local buffer stands in for the peer's copy of
@@ -455,7 +455,8 @@ def test_in_kernel_allgather_world1(comm, graph, mode):
     before each run; the copy workgroups must pull them, flag each block, ACK, and the gated
     GEMM tiles must wait for them (C checked against fp32 every run). ``mode``: the copy role's
     publication variants (csrc/gemm/gemm.h AgMode: 0 write-through stores, 1 plain stores +
-    release fence, 6 write-through + 16 loads per lane + agent-scope gate acquire)."""
+    release fence, 6 write-through + 16 loads per lane + agent-scope gate acquire, 14 = 6 + copy
+    workgroups grown while the GEMM's tile rounds stay the same)."""
     from ddlb_amd.parallel.context import NativeContext
     from ddlb_amd.parallel.plan import DT_BF16, Plan, SIG_KERNEL, SIG_STREAM
 
