@@ -146,6 +146,12 @@ ROW_CANDIDATES = [
     ("row/default/ipc/kernel", "native", dict(_RK, algorithm="default")),
     ("row/default/ipc/kernel/blas", "native", _blas(dict(_RK, algorithm="default"))),
     ("row/coll_pipeline/ipc/kernel/s4", "native", dict(_RK, algorithm="coll_pipeline", s=4)),
+    # direct store: ONE GEMM whose epilogue writes every peer's partial into its receive slot
+    # over xGMI (shard-interleaved tiles: all links at once), then one local d-way reduce
+    ("row/p2p_pipeline/ipc/direct/graph", "native", _graph(dict(algorithm="p2p_pipeline",
+                                                                backend="ipc", fused=True))),
+    ("row/p2p_pipeline/ipc/direct", "native", dict(algorithm="p2p_pipeline", backend="ipc",
+                                                   fused=True)),
     ("row/p2p_pipeline/ipc/memcpy", "native", dict(algorithm="p2p_pipeline", backend="ipc")),
     ("row/coll_pipeline/ipc/kernel/s4/graph", "native", _graph(dict(_RK, algorithm="coll_pipeline",
                                                                     s=4))),

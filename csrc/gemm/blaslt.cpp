@@ -196,7 +196,9 @@ void autotune(LtDevice* d, LtPlan* pl, const GemmArgs& p, hipStream_t s) {
 bool blaslt_supports(const GemmArgs& p, int din, int dout) {
   hipDataType t;
   if (!lt_type(din, &t) || !lt_type(dout, &t)) return false;
-  if (p.flags != nullptr || p.act != ACT_NONE || p.tile_order != 0 || p.a_table) return false;
+  if (p.flags != nullptr || p.act != ACT_NONE || p.tile_order != 0 || p.a_table ||
+      p.c_table)
+    return false;
   if (p.M <= 0 || p.N <= 0 || p.K <= 0) return false;
   // Plain GEMMs only. Grouped-row (pipeline-stage) addressing stays on the MFMA kernels, which
   // read the grouped rows natively in one launch: the equivalent hipBLASLt strided batch with a

@@ -68,6 +68,11 @@ struct GemmArgs {
   // array of addresses, e.g. the peers' IPC-mapped shards read straight over xGMI).
   const uint64_t* a_table = nullptr;
   int64_t shard_rows = 0;
+  // Direct-store C (optional): row block s of c_shard_rows rows is written at c_table[s] (device
+  // array of addresses, e.g. the peers' IPC-mapped receive slots: a reduce-scatter's partials
+  // stored straight over xGMI by the GEMM epilogue). tile_order = 2 interleaves the shards.
+  const uint64_t* c_table = nullptr;
+  int64_t c_shard_rows = 0;
 };
 enum Act : int { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_SILU = 3 };
 // In-kernel all-gather variants (GemmArgs::ag_mode bits; 0 = write-through publication, 8 loads

@@ -44,6 +44,18 @@ __device__ __forceinline__ const char* a_row(const GemmArgs& p, int64_t row, int
   return (const char*)p.a + map_row(row, p.a_grp, p.a_gstride) * p.lda * esz;
 }
 
+// Address of logical C row ``row``: grouped rows, or a per-shard pointer table (direct store:
+// row block s of c_shard_rows rows lives at c_table[s], e.g. a peer's receive slot over xGMI).
+template <int OSZ>
+__device__ __forceinline__ char* c_row(const GemmArgs& p, int64_t row) {
+  if (p.c_table != nullptr) {
+    const unsigned ur = (unsigned)row, us = (unsigned)p.c_shard_rows;
+    const unsigned sh = ur / us;
+    return (char*)p.c_table[sh] + (int64_t)(ur - sh * us) * p.ldc * OSZ;
+  }
+  return (char*)p.c + map_row(row, p.c_grp, p.c_gstride) * p.ldc * OSZ;
+}
+
 // Bijective XCD remap (guide §5, "XCD swizzle must be bijective").
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, idx = bid >> 3;
@@ -66,6 +78,13 @@ __device__ __forceinline__ int tile_index(const GemmArgs& p, int nwg) {
 
 __device__ __forceinline__ int tile_index_virtual(const GemmArgs& p, int vid, int nwg) {
   if (!p.tile_order) return xcd_remap(vid, nwg);
+  if (p.tile_order == 2) {
+    // shards interleaved: consecutive ids (one per XCD) walk different shards, so the tiles in
+    // flight cover every shard at once (a direct-store GEMM keeps every peer's link busy) and,
+    // with nshards dividing 8, each XCD stays on one shard (its A panels in that XCD's L2)
+    const int ns = p.nshards, per = nwg / ns;
+    return (vid % ns) * per + vid / ns;
+  }
   const int per = nwg / p.nshards;
   const int j = vid / per, local = vid % per;
   return ordered_shard(p, j) * per + xcd_remap(local, per);
@@ -507,7 +526,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_kernel(const GemmArgs p) 
   for (int i = 0; i < MR; ++i) {
     const int64_t row = m0 + wm * TM + i * 16 + frow;
     if (row >= p.M) continue;
-    char* crow = (char*)p.c + map_row(row, p.c_grp, p.c_gstride) * p.ldc * OSZ;
+    char* crow = c_row<OSZ>(p, row);
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
       const int64_t col = n0 + wn * TN + j * 16 + fq * 4;
@@ -619,7 +638,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_persist_kernel(const Gemm
 #pragma unroll
     for (int i = 0; i < MR; ++i) {
       const int64_t row = m0 + wm * TM + i * 16 + frow;
-      char* crow = (char*)p.c + map_row(row, p.c_grp, p.c_gstride) * p.ldc * OSZ;
+      char* crow = c_row<OSZ>(p, row);
 #pragma unroll
       for (int j = 0; j < NR; ++j) {
         const int64_t col = n0 + wn * TN + j * 16 + fq * 4;
@@ -911,8 +930,7 @@ __global__ __launch_bounds__(512) void gemm_tn_ring_kernel(const GemmArgs p) {
       if (p.act == ACT_NONE) {
 #pragma unroll
         for (int i = 0; i < MR; ++i) {
-          char* crow = (char*)p.c + map_row(m0 + wm * TM + i * 16 + frow, p.c_grp, p.c_gstride) *
-                                        p.ldc * OSZ;
+          char* crow = c_row<OSZ>(p, m0 + wm * TM + i * 16 + frow);
 #pragma unroll
           for (int jp = 0; jp < NR / 2; ++jp)
             Store8<OUT>::st(crow + (n0 + wn * TN + jp * 32 + fq * 8) * OSZ, acc[i][2 * jp],
@@ -921,8 +939,7 @@ __global__ __launch_bounds__(512) void gemm_tn_ring_kernel(const GemmArgs p) {
       } else {
 #pragma unroll
         for (int i = 0; i < MR; ++i) {
-          char* crow = (char*)p.c + map_row(m0 + wm * TM + i * 16 + frow, p.c_grp, p.c_gstride) *
-                                        p.ldc * OSZ;
+          char* crow = c_row<OSZ>(p, m0 + wm * TM + i * 16 + frow);
 #pragma unroll
           for (int jp = 0; jp < NR / 2; ++jp)
             Store8<OUT>::st(crow + (n0 + wn * TN + jp * 32 + fq * 8) * OSZ,
@@ -1092,7 +1109,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pp256_kernel(const GemmArgs p) {
   for (int i = 0; i < 8; ++i) {
     const int64_t row = m0 + wr * 128 + (i >> 2) * 64 + (i & 3) * 16 + frow;
     if (row >= p.M) continue;
-    char* crow = (char*)p.c + map_row(row, p.c_grp, p.c_gstride) * p.ldc * OSZ;
+    char* crow = c_row<OSZ>(p, row);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int64_t col = n0 + wc * 64 + (j >> 1) * 32 + (j & 1) * 16 + fq * 4;
@@ -1290,7 +1307,7 @@ __global__ __launch_bounds__(512) void gemm_tn_t8_kernel(const GemmArgs p) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int64_t row = m0 + wr * 128 + (i >> 2) * 64 + (i & 3) * 16 + frow;
-    char* crow = (char*)p.c + map_row(row, p.c_grp, p.c_gstride) * p.ldc * OSZ;
+    char* crow = c_row<OSZ>(p, row);
 #pragma unroll
     for (int nq = 0; nq < 2; ++nq) {
       char* dst = crow + (n0 + wc * 64 + nq * 32 + fq * 8) * OSZ;
@@ -1473,7 +1490,7 @@ __global__ __launch_bounds__(512) void gemm_tn_t4_kernel(const GemmArgs p) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int64_t row = m0 + wr * 128 + (i >> 2) * 64 + (i & 3) * 16 + frow;
-    char* crow = (char*)p.c + map_row(row, p.c_grp, p.c_gstride) * p.ldc * OSZ;
+    char* crow = c_row<OSZ>(p, row);
 #pragma unroll
     for (int nq = 0; nq < 2; ++nq) {
       char* dst = crow + (n0 + wc * 64 + nq * 32 + fq * 8) * OSZ;
@@ -1640,7 +1657,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     for (int f = 0; f < 4; ++f) {
       const int i = mq * 4 + f;
       const int64_t row = m0 + wr * 128 + mq * 64 + f * 16 + frow;
-      char* dst = (char*)p.c + map_row(row, p.c_grp, p.c_gstride) * p.ldc * OSZ +
+      char* dst = c_row<OSZ>(p, row) +
                   (n0 + wc * 64 + nq * 32 + fq * 8) * OSZ;
       // one store site (two branch-local stores get merged by the optimizer, which drops the
       // non-temporal hint)
@@ -1897,7 +1914,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt8_kernel(const GemmArgs p) {
     for (int f = 0; f < 4; ++f) {
       const int i = mq * 4 + f;
       const int64_t row = m0 + wr * 128 + mq * 64 + f * 16 + frow;
-      char* dst = (char*)p.c + map_row(row, p.c_grp, p.c_gstride) * p.ldc * OSZ +
+      char* dst = c_row<OSZ>(p, row) +
                   (n0 + wc * 64 + nq * 32 + fq * 8) * OSZ;
       // one store site (two branch-local stores get merged by the optimizer, which drops the
       // non-temporal hint)
@@ -2074,7 +2091,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_mxfp8_kernel(const GemmAr
   for (int i = 0; i < MR; ++i) {
     const int64_t row = m0 + wm * TM + i * 16 + frow;
     if (row >= p.M) continue;
-    char* crow = (char*)p.c + map_row(row, p.c_grp, p.c_gstride) * p.ldc * OSZ;
+    char* crow = c_row<OSZ>(p, row);
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
       const int64_t col = n0 + wn * TN + j * 16 + fq * 4;

@@ -103,6 +103,16 @@ hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mo
       tile = TILE_128x128;
     if (mode == GEMM_MODE_GENERIC || !gemm_fast_path_ok(p, din, dout)) return hipErrorNotSupported;
   }
+  if (p.c_table != nullptr) {
+    // direct-store C: every fast kernel addresses C rows through c_row(); hipBLASLt and the
+    // generic kernel cannot, and an interleaved shard order needs whole tiles per shard
+    if (p.c_shard_rows <= 0 || p.c_grp != p.M || mode == GEMM_MODE_GENERIC ||
+        !gemm_fast_path_ok(p, din, dout))
+      return hipErrorNotSupported;
+    if (mode == GEMM_MODE_BLAS) mode = GEMM_MODE_AUTO;
+  }
+  if (p.tile_order == 2 && (p.nshards <= 0 || p.M % p.nshards != 0))
+    return hipErrorInvalidValue;
   if (p.ag_ctas > 0) {
     // in-kernel all-gather: only the gated persistent pt4 kernel carries the copy workgroups;
     // anything else would skip the copies, so refuse rather than fall back
@@ -113,10 +123,10 @@ hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mo
         p.nsub < 1 || p.nshards % p.nsub || p.nshards / p.nsub > 32 || p.ag_parts < 1 ||
         p.ag_tab == nullptr || p.flag_rows * p.lda * esz / p.ag_parts >= (int64_t(1) << 30))
       return hipErrorNotSupported;  // (a copy unit is addressed by one 32-bit buffer descriptor)
-  } else if (p.ag_mode != 0) {
-    return hipErrorNotSupported;  // agent-scope gate acquire only for flags this launch sets
     if (mode == GEMM_MODE_BLAS) mode = GEMM_MODE_AUTO;
     tile = TILE_PT4;
+  } else if (p.ag_mode != 0) {
+    return hipErrorNotSupported;  // agent-scope gate acquire only for flags this launch sets
   }
   if (mode == GEMM_MODE_BLAS) {
     const hipError_t e = blaslt_gemm(p, din, dout, s);
@@ -131,12 +141,14 @@ hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mo
     if (p.tile_order && (p.nshards <= 0 || p.M % p.nshards != 0 || p.nshards % p.nsub != 0 ||
                          (p.M / p.nshards) % tile_rows(tile) != 0))
       p.tile_order = 0;
+    if (p.tile_order == 2 && p.N % tile_cols(tile) != 0) p.tile_order = 0;  // whole tiles/shard
     hipError_t e = hipErrorInvalidValue;
     if (din == DT_FP8 && mode == GEMM_MODE_MX) e = launch_fast_mx(p, dout, tile, s);
     else e = launch_fast(p, din, dout, tile, s);
     if (e != hipErrorInvalidValue) return e;
   }
-  if (p.flags != nullptr) return hipErrorNotSupported;  // arrival flags need the tiled kernel
+  if (p.flags != nullptr || p.c_table != nullptr)
+    return hipErrorNotSupported;  // arrival flags / direct-store C need the tiled kernels
   return launch_generic(p, din, dout, s);
 }
 

@@ -615,9 +615,10 @@ def check_rowwise(d: int, m: int, n: int, k: int, cfg: AlgoConfig) -> None:
     if cfg.direction != "pull":
         raise ValueError("direction=push is a tp_columnwise all-gather option (the rowwise "
                          "p2p_pipeline already pushes its partials)")
-    if cfg.fused:
-        raise ValueError("fused=True (flag-gated GEMM over arriving rows) is a tp_columnwise "
-                         "all-gather option")
+    if cfg.fused and not (cfg.algorithm == "p2p_pipeline" and cfg.backend == "ipc"):
+        raise ValueError("fused=True for tp_rowwise is the direct-store p2p_pipeline (backend=ipc: "
+                         "the GEMM epilogue writes each peer's partial into its receive slot); the "
+                         "flag-gated GEMM over arriving rows is a tp_columnwise all-gather option")
     if d > 16:
         raise ValueError("at most 16 ranks per node are supported by the reduce op")
 
@@ -680,6 +681,21 @@ def build_tp_rowwise(rank: int, d: int, m: int, n: int, k: int, din: int, dout: 
             srcs = [stg + rank * sblk] + [(stg + rank * sblk).at(p) for p in peers]
             plan.reduce(S_COMM, OUT + j * sblk, srcs, rows * n, dout)
             _signal(plan, S_COMM, [flags.ref("ACKS", j * d + rank, owner=p) for p in peers], cfg)
+    elif alg == "p2p_pipeline" and be == "ipc" and cfg.fused:
+        # Direct-store reduce-scatter: ONE GEMM over all m rows whose epilogue writes row block q
+        # (the partial rank q reduces) straight into q's receive slot for this rank over xGMI
+        # (csrc/gemm/gemm_kernels.h c_row); tile_order=2 interleaves the blocks, so the tiles in
+        # flight store to every peer (every link) at once. No staging buffer, no copy engine,
+        # no HBM round trip of the partials; the comm IS the GEMM's C stream.
+        RECV = plan.buffer("RECV", d * blk, symmetric=True)
+        _wait(plan, S_MAIN, [flags.ref("ACK", p) for p in peers], cfg, delta=-1)
+        slots = [(RECV + rank * blk).at(q) if q != rank else RECV + rank * blk for q in range(d)]
+        gemm(S_MAIN, 0, RECV + rank * blk, m, c_shards=slots, c_shard_rows=ml, nshards=d,
+             tile_order=2)
+        _signal(plan, S_MAIN, [flags.ref("READY", rank, owner=p) for p in peers], cfg)
+        _wait(plan, S_MAIN, [flags.ref("READY", p) for p in peers], cfg)
+        plan.reduce(S_MAIN, OUT, [RECV + q * blk for q in range(d)], ml * n, dout)
+        _signal(plan, S_MAIN, [flags.ref("ACK", rank, owner=p) for p in peers], cfg)
     elif alg == "p2p_pipeline" and be == "ipc":
         PST = plan.buffer("PST", d * blk)
         RECV = plan.buffer("RECV", d * blk, symmetric=True)

@@ -19,7 +19,7 @@ from __future__ import annotations
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
-OP_WORDS = 32
+OP_WORDS = 34
 (OP_NOP, OP_GEMM, OP_RECORD, OP_WAIT, OP_ALLGATHER, OP_REDUCE_SCATTER, OP_SEND, OP_RECV,
  OP_GROUP_START, OP_GROUP_END, OP_COPY, OP_SIGNAL, OP_WAIT_SIGNAL, OP_REDUCE, OP_MEMSET,
  OP_COPY_MULTI) = range(16)
@@ -120,7 +120,8 @@ class Plan:
              flags: Optional[Ref] = None, flag_rows: int = 0, nshards: int = 1,
              first_shard: int = 0, tile_order: int = 0, act: int = 0,
              a_shards: Optional[Sequence[Ref]] = None, shard_rows: int = 0,
-             nsub: int = 1, reserve_cus: int = 0, ag: Optional[dict] = None) -> Op:
+             nsub: int = 1, reserve_cus: int = 0, ag: Optional[dict] = None,
+             c_shards: Optional[Sequence[Ref]] = None, c_shard_rows: int = 0) -> Op:
         """``a_shards``: A row block s (``shard_rows`` rows each) is read from ``a_shards[s]``
         (a peer's copy for a direct-access GEMM that pulls its operand over xGMI).
         ``flags`` (arrival-gated tiles): shard ``i`` = rows ``[i*flag_rows, (i+1)*flag_rows)`` may
@@ -132,7 +133,11 @@ class Plan:
         ``ag`` = in-kernel all-gather (``dict(ctas, parts, rank, src, ack, ready, count)``, see
         csrc/gemm/gemm.h ``ag_ctas``): the launch's first ``ctas`` workgroups pull row block b of
         every producer p (``src[p]``, same rows) into A, set ``flags[p * nsub + b]`` and ACK p
-        (``ack[p]``) after READY (``ready[p]``); the GEMM tiles gate on those flags."""
+        (``ack[p]``) after READY (``ready[p]``); the GEMM tiles gate on those flags.
+        ``c_shards`` (direct-store C): C row block s (``c_shard_rows`` rows) is written at
+        ``c_shards[s]`` — e.g. the peers' receive slots, so the epilogue stores a reduce-scatter's
+        partials straight over xGMI; ``tile_order=2`` interleaves the blocks (every destination's
+        tiles in flight at once)."""
         if nsub < 1 or nshards % nsub:
             raise ValueError(f"nsub ({nsub}) must divide nshards ({nshards})")
         if ag is not None:
@@ -146,6 +151,13 @@ class Plan:
             ag = dict(ag, table=self.table(f"__agtab{len(self.buffers)}",
                                            list(ag["src"]) + list(ag["ack"]) +
                                            [ag["ready"], ag["count"]]))
+        c_table = None
+        if c_shards is not None:
+            if c_shard_rows <= 0 or len(c_shards) * c_shard_rows < M or c_grp not in (0, M):
+                raise ValueError("c_shards must cover the M rows (no grouped C rows)")
+            c_table = self.table(f"__ctab{len(self.buffers)}", c_shards)
+        if tile_order == 2 and (nshards < 1 or M % nshards):
+            raise ValueError("tile_order=2 needs nshards dividing M")
         a_table = None
         if a_shards is not None:
             if shard_rows <= 0 or len(a_shards) * shard_rows < M:
@@ -158,7 +170,9 @@ class Plan:
                          tile_order=tile_order, act=act,
                          a_shards=list(a_shards) if a_shards is not None else None,
                          shard_rows=shard_rows, a_table=a_table, nsub=nsub,
-                         reserve_cus=reserve_cus, ag=ag)
+                         reserve_cus=reserve_cus, ag=ag,
+                         c_shards=list(c_shards) if c_shards is not None else None,
+                         c_shard_rows=c_shard_rows, c_table=c_table)
 
     def table(self, name: str, refs: Sequence[Ref]) -> Ref:
         """Device array of 64-bit addresses of ``refs`` (written once when the plan is bound)."""
@@ -252,6 +266,8 @@ class Plan:
                     w[29] = (g["ctas"] | (g["parts"] << 20) | (g["rank"] << 40) |
                              (g.get("mode", 0) << 56))
                     w[30] = resolve(g["table"])
+                if a.get("c_table") is not None:
+                    w[32], w[33] = resolve(a["c_table"]), a["c_shard_rows"]
             elif k in (OP_RECORD, OP_WAIT):
                 w[2] = a["event"]
             elif k in (OP_ALLGATHER, OP_REDUCE_SCATTER):

@@ -177,17 +177,30 @@ class Simulator:
                                           a["K"], ein):
                     self._touch(r, ref, nb, False, vc, what + ".A")
             self._touch(r, a["b"], ((a["N"] - 1) * a["ldb"] + a["K"]) * ein, False, vc, what + ".B")
-            for ref, nb in self._rows(a["c"], a["M"], a["c_grp"], a["c_gstride"], a["ldc"],
-                                      a["N"], eout):
-                self._touch(r, ref, nb, True, vc, what + ".C")
+            cshards = a.get("c_shards")
+            if cshards is None:
+                for ref, nb in self._rows(a["c"], a["M"], a["c_grp"], a["c_gstride"], a["ldc"],
+                                          a["N"], eout):
+                    self._touch(r, ref, nb, True, vc, what + ".C")
             A = A_shards if A_shards is not None else self._gather_rows(
                 self._buf(r, a["a"]), a["a"].off, a["M"], a["a_grp"], a["a_gstride"], a["lda"],
                 a["K"], a["din"]).float()
             Bt = _view(self._buf(r, a["b"]), a["b"].off, (a["N"] - 1) * a["ldb"] + a["K"],
                        a["din"]).as_strided((a["N"], a["K"]), (a["ldb"], 1)).float()
             Cv = apply_act(A @ Bt.t(), a.get("act", 0))
-            self._scatter_rows(self._buf(r, a["c"]), a["c"].off, a["M"], a["c_grp"], a["c_gstride"],
-                               a["ldc"], a["N"], a["dout"], Cv)
+            if cshards is None:
+                self._scatter_rows(self._buf(r, a["c"]), a["c"].off, a["M"], a["c_grp"],
+                                   a["c_gstride"], a["ldc"], a["N"], a["dout"], Cv)
+            else:  # direct-store C: row block s written at c_shards[s] (maybe a peer's buffer)
+                R = a["c_shard_rows"]
+                for sidx, ref in enumerate(cshards):
+                    rows = min(R, a["M"] - sidx * R)
+                    if rows <= 0:
+                        break
+                    self._touch(r, ref, ((rows - 1) * a["ldc"] + a["N"]) * eout, True, vc,
+                                what + f".C{sidx}")
+                    self._scatter_rows(self._buf(r, ref), ref.off, rows, 0, 0, a["ldc"], a["N"],
+                                       a["dout"], Cv[sidx * R:sidx * R + rows])
         elif k == OP_COPY:
             self._touch(r, a["src"], a["nbytes"], False, vc, what + ".src")
             self._touch(r, a["dst"], a["nbytes"], True, vc, what + ".dst")

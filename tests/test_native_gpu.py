@@ -142,6 +142,12 @@ def _ipc_cfgs():
     for alg in ("coll_pipeline", "p2p_pipeline"):  # the persistent gated GEMM (pt4 + reserve)
         cfgs.append((f"col/{alg}/fused/pt4", "col", dict(algorithm=alg, backend="ipc", s=2,
                                                          fused=True, tile="pt4")))
+    # tp_rowwise direct store: the GEMM epilogue writes each peer's partial into its RECV slot
+    cfgs.append(("row/p2p/direct", "row", dict(algorithm="p2p_pipeline", backend="ipc",
+                                               fused=True)))
+    cfgs.append(("row/p2p/direct/128/ksig", "row", dict(algorithm="p2p_pipeline", backend="ipc",
+                                                        fused=True, tile="128x128",
+                                                        signal="kernel")))
     cfgs.append(("col/p2p/noring", "col", dict(algorithm="p2p_pipeline", backend="ipc",
                                                offset_stream_indexing_by_rank=False)))
     cfgs.append(("col/p2p/fp8", "col", dict(algorithm="p2p_pipeline", backend="ipc",
@@ -171,7 +177,8 @@ def _ipc_cfgs():
             ("row/default/kernel/graph", "row", dict(algorithm="default",
                                                      multicast_protocol="kernel")),
             ("row/coll/graph", "row", dict(algorithm="coll_pipeline", s=2)),
-            ("row/p2p/graph", "row", dict(algorithm="p2p_pipeline"))):
+            ("row/p2p/graph", "row", dict(algorithm="p2p_pipeline")),
+            ("row/p2p/direct/graph", "row", dict(algorithm="p2p_pipeline", fused=True))):
         cfgs.append((label, prim, dict(opts, backend="ipc", graph=True)))
     for alg in ("default", "coll_pipeline", "p2p_pipeline"):  # pulls split over 2 copy streams
         cfgs.append((f"col/{alg}/memcpy/cs2", "col", dict(algorithm=alg, backend="ipc", s=2,
@@ -497,5 +504,40 @@ def test_in_kernel_allgather_world1(comm, graph, mode):
         torch.cuda.synchronize()
         bound.check_health()
         torch.testing.assert_close(out.float(), ref, rtol=0, atol=1e-3 * K)
+    bound.close()
+    ctx.close()
+
+
+@pytest.mark.parametrize("tile,mode", [(0, 0), (18, 0), (4, 0), (0, 3)])
+def test_direct_store_gemm_world1(comm, tile, mode):
+    """Direct-store C (c_shards): row block q of one GEMM lands in its own buffer (the peers'
+    receive slots in the rowwise p2p plan), tiles dispatched shard-interleaved (tile_order=2).
+    Every kernel family that can take it (pt4 auto, t4, 128x128; blas falls back to MFMA)."""
+    from ddlb_amd.parallel.context import NativeContext
+    from ddlb_amd.parallel.plan import DT_BF16, Plan
+
+    M, N, K, d = 4096, 1024, 512, 4
+    rows = M // d
+    plan = Plan(0, 1, nstreams=1, stream_priority=[0])
+    a = plan.buffer("a", M * K * 2)
+    bt = plan.buffer("bt", N * K * 2)
+    slots = [plan.buffer(f"slot{q}", rows * N * 2) for q in range(d)]
+    plan.gemm(0, a, bt, slots[0], M=M, N=N, K=K, lda=K, ldb=K, ldc=N, din=DT_BF16, dout=DT_BF16,
+              tile=tile, mode=mode, c_shards=slots, c_shard_rows=rows, nshards=d, tile_order=2)
+    ctx = NativeContext(comm)
+    bound = ctx.bind(plan)
+    A = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+    W = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
+    bound.buffer("a").view(torch.bfloat16).view(M, K).copy_(A)
+    bound.buffer("bt").view(torch.bfloat16).view(N, K).copy_(W)
+    ref = A.float() @ W.float().T
+    for _ in range(2):
+        for q in range(d):
+            bound.buffer(f"slot{q}").view(torch.bfloat16).fill_(float("nan"))
+        bound.run()
+        torch.cuda.synchronize()
+        for q in range(d):
+            out = bound.buffer(f"slot{q}").view(torch.bfloat16).view(rows, N).float()
+            torch.testing.assert_close(out, ref[q * rows:(q + 1) * rows], rtol=0, atol=1e-3 * K)
     bound.close()
     ctx.close()

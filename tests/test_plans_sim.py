@@ -111,14 +111,29 @@ def test_push_rejected_where_meaningless():
                                                                      direction="push"))
 
 
-@pytest.mark.parametrize("protocol", ["memcpy", "kernel"])
-def test_rowwise_rejects_fused(protocol):
-    """fused (flag-gated GEMM over arriving A rows) only exists for the columnwise all-gather;
-    the rowwise builder must refuse it up front, not fail while building."""
-    cfg = AlgoConfig(algorithm="coll_pipeline", backend="ipc", s=2, fused=True,
-                     protocol=protocol)
-    with pytest.raises(ValueError, match="tp_columnwise"):
+@pytest.mark.parametrize("alg,backend", [("coll_pipeline", "ipc"), ("default", "ipc"),
+                                         ("p2p_pipeline", "rccl")])
+def test_rowwise_rejects_fused(alg, backend):
+    """tp_rowwise fused = the direct-store p2p_pipeline over IPC only; anything else must be
+    refused up front, not fail while building."""
+    cfg = AlgoConfig(algorithm=alg, backend=backend, s=2, fused=True)
+    with pytest.raises(ValueError, match="direct-store"):
         build_tp_rowwise(0, 2, 16, 8, 8, DT_F32, DT_F32, cfg)
+
+
+@pytest.mark.parametrize("d", [1, 2, 3, 4])
+@pytest.mark.parametrize("sig", [SIG_STREAM, SIG_KERNEL])
+def test_rowwise_direct_store_plan(d, sig):
+    """tp_rowwise p2p_pipeline fused: ONE GEMM whose row block q lands in rank q's receive slot
+    (direct store over xGMI), interleaved shard order; READY / reduce / ACK epochs."""
+    cfg = AlgoConfig(algorithm="p2p_pipeline", backend="ipc", fused=True, signal=sig)
+    _run_row(d, m=8 * d, n=8, k=4 * d, cfg=cfg, epochs=4)
+    if d > 1:
+        plan, _ = build_tp_rowwise(1, d, 8 * d, 8, 4 * d, DT_F32, DT_F32, cfg)
+        g = [op for op in plan.ops if op.kind == OP_GEMM]
+        assert len(g) == 1 and g[0].args["tile_order"] == 2 and g[0].args["c_shard_rows"] == 8
+        owners = [ref.owner for ref in g[0].args["c_shards"]]
+        assert owners == [q if q != 1 else None for q in range(d)]
 
 
 @pytest.mark.parametrize("fused", [True, False])
