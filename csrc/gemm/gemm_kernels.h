@@ -46,14 +46,23 @@ __device__ __forceinline__ const char* a_row(const GemmArgs& p, int64_t row, int
 
 // Address of logical C row ``row``: grouped rows, or a per-shard pointer table (direct store:
 // row block s of c_shard_rows rows lives at c_table[s], e.g. a peer's receive slot over xGMI).
-template <int OSZ>
+// DS: 0 = grouped rows only (no table), 1 = table only, 2 = decided at run time. The persistent
+// pt4 kernel (the flagship's) is instantiated per form: the run-time branch in its epilogue cost
+// ~8 % (profiles/r02/s4/r2s4_7_*). Both forms are built as global-address-space pointers: a
+// pointer read from the table is otherwise "generic", and the merged value would turn every
+// epilogue store into a flat store.
+template <int OSZ, int DS = 2>
 __device__ __forceinline__ char* c_row(const GemmArgs& p, int64_t row) {
-  if (p.c_table != nullptr) {
+  if constexpr (DS == 0) return (char*)p.c + map_row(row, p.c_grp, p.c_gstride) * p.ldc * OSZ;
+  GLB_AS char* base;
+  if (DS == 1 || p.c_table != nullptr) {
     const unsigned ur = (unsigned)row, us = (unsigned)p.c_shard_rows;
     const unsigned sh = ur / us;
-    return (char*)p.c_table[sh] + (int64_t)(ur - sh * us) * p.ldc * OSZ;
+    base = (GLB_AS char*)p.c_table[sh] + (int64_t)(ur - sh * us) * p.ldc * OSZ;
+  } else {
+    base = (GLB_AS char*)p.c + map_row(row, p.c_grp, p.c_gstride) * p.ldc * OSZ;
   }
-  return (char*)p.c + map_row(row, p.c_grp, p.c_gstride) * p.ldc * OSZ;
+  return (char*)base;
 }
 
 // Bijective XCD remap (guide §5, "XCD swizzle must be bijective").
@@ -1521,7 +1530,7 @@ __global__ __launch_bounds__(512) void gemm_tn_t4_kernel(const GemmArgs p) {
 // Measured (scripts/lab, profiles/r01/s2/lab/t8_vs_ring2.txt): flagship 0.1127 vs t4 0.1160 ms.
 // GATED: the arrival-flag form (a separate instantiation, so the ungated kernel's code and
 // schedule are exactly those measured without flags).
-template <class Mma, int OUT, bool GATED>
+template <class Mma, int OUT, bool GATED, bool DS = false>
 __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   constexpr int ROWB = 128, UNIT = 128 * ROWB, STAGE = 4 * UNIT;
   constexpr int UA0 = 0, UA1 = UNIT, UB0 = 2 * UNIT, UB1 = 3 * UNIT;
@@ -1657,7 +1666,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     for (int f = 0; f < 4; ++f) {
       const int i = mq * 4 + f;
       const int64_t row = m0 + wr * 128 + mq * 64 + f * 16 + frow;
-      char* dst = c_row<OSZ>(p, row) +
+      char* dst = c_row<OSZ, DS ? 1 : 0>(p, row) +
                   (n0 + wc * 64 + nq * 32 + fq * 8) * OSZ;
       // one store site (two branch-local stores get merged by the optimizer, which drops the
       // non-temporal hint)
@@ -2274,6 +2283,9 @@ hipError_t launch_pt4(const GemmArgs& p, hipStream_t s) {
   if (p.flags != nullptr)
     hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, true>), dim3(grid + q.ag_ctas), dim3(512), 0,
                        s, q);
+  else if (p.c_table != nullptr)
+    hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false, true>), dim3(grid), dim3(512), 0, s,
+                       p);
   else
     hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false>), dim3(grid), dim3(512), 0, s, p);
   return hipGetLastError();

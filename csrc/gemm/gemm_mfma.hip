@@ -107,7 +107,7 @@ hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mo
     // direct-store C: every fast kernel addresses C rows through c_row(); hipBLASLt and the
     // generic kernel cannot, and an interleaved shard order needs whole tiles per shard
     if (p.c_shard_rows <= 0 || p.c_grp != p.M || mode == GEMM_MODE_GENERIC ||
-        !gemm_fast_path_ok(p, din, dout))
+        p.flags != nullptr || p.ag_ctas > 0 || !gemm_fast_path_ok(p, din, dout))
       return hipErrorNotSupported;
     if (mode == GEMM_MODE_BLAS) mode = GEMM_MODE_AUTO;
   }
