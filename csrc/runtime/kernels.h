@@ -45,5 +45,15 @@ hipError_t signal_launch(const SignalArgs& a, hipStream_t s);
 hipError_t wait_launch(const WaitArgs& a, hipStream_t s);
 // *epoch += 1 (one lane): the device-side run counter of a graph-replayed plan.
 hipError_t epoch_bump_launch(unsigned* epoch, hipStream_t s);
+// hipGraph prologue: ++*epoch, then *ptr[i] = new epoch + delta[i] (system-scope release) — the
+// run-counter bump and the plan's leading signals in ONE launch instead of 1 + k.
+constexpr int kMaxPrologue = 32;
+struct BumpSignalArgs {
+  unsigned* epoch = nullptr;
+  unsigned* ptr[kMaxPrologue] = {};
+  int delta[kMaxPrologue] = {};
+  int n = 0;
+};
+hipError_t bump_signal_launch(const BumpSignalArgs& a, hipStream_t s);
 
 }  // namespace ddlb

@@ -199,6 +199,21 @@ __global__ void wait_kernel(WaitArgs a) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 }
 
+__global__ void bump_signal_kernel(BumpSignalArgs a) {
+  __shared__ unsigned e;
+  if (threadIdx.x == 0) {
+    e = *a.epoch + 1;
+    *a.epoch = e;
+  }
+  __syncthreads();
+  const int i = threadIdx.x;
+  if (i < a.n) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+    __hip_atomic_store(a.ptr[i], (unsigned)((int)e + a.delta[i]), __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 __global__ void epoch_bump_kernel(unsigned* epoch) {
   if (threadIdx.x == 0) *epoch += 1;
 }
@@ -275,6 +290,12 @@ hipError_t signal_launch(const SignalArgs& a, hipStream_t s) {
 hipError_t wait_launch(const WaitArgs& a, hipStream_t s) {
   if (a.n < 1 || a.n > kMaxSignal) return hipErrorInvalidValue;
   hipLaunchKernelGGL(wait_kernel, dim3(1), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t bump_signal_launch(const BumpSignalArgs& a, hipStream_t s) {
+  if (a.epoch == nullptr || a.n < 0 || a.n > kMaxPrologue) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bump_signal_kernel, dim3(1), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 

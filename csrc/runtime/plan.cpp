@@ -2,6 +2,7 @@
 #include "plan.h"
 
 #include <chrono>
+#include <cstdlib>
 #include <stdexcept>
 
 #include "../gemm/gemm.h"
@@ -154,7 +155,29 @@ void PlanExecutor::join_others(int64_t stream, hipStream_t main) {
 void PlanExecutor::enqueue(hipStream_t main) {
   std::fill(touched_.begin(), touched_.end(), false);
   if (timeline_on_) DDLB_HIP(hipEventRecord(tl_start_, main));
-  if (graph_on_) DDLB_HIP(epoch_bump_launch(d_epoch_, main));  // first node of every replay
+  size_t first = 0;
+  if (graph_on_) {
+    // first node of every replay: the run-counter bump, fused with the plan's leading signals on
+    // the main stream (READY to the peers, own-shard arrival flags): one launch instead of 1 + k
+    // (each small kernel after a GEMM costs a few us of boundary + L2 write-back)
+    BumpSignalArgs b;
+    b.epoch = d_epoch_;
+    static const bool fuse = getenv("DDLB_GRAPH_PROLOGUE") == nullptr ||
+                             atoi(getenv("DDLB_GRAPH_PROLOGUE")) != 0;  // A/B knob
+    for (; fuse && first < ops_.size(); first += kOpWords) {
+      const int64_t* o = &ops_[first];
+      if (o[0] != OP_SIGNAL || o[1] != 0 || o[2] < 1 || o[2] > kMaxSignal ||
+          b.n + o[2] > kMaxPrologue)
+        break;
+      for (int i = 0; i < (int)o[2]; ++i) {
+        b.ptr[b.n] = (unsigned*)o[5 + i];
+        b.delta[b.n] = (int)o[4];
+        ++b.n;
+      }
+      touched_[0] = true;
+    }
+    DDLB_HIP(bump_signal_launch(b, main));
+  }
   if (any_side_) {
     // fork: every used side stream waits for everything already queued on `main`
     DDLB_HIP(hipEventRecord(fork_join_[0], main));
@@ -162,7 +185,7 @@ void PlanExecutor::enqueue(hipStream_t main) {
       if (used_[i]) DDLB_HIP(hipStreamWaitEvent(streams_[i], fork_join_[0], 0));
   }
   if (timeline_on_) host_us_.assign(ops_.size() / kOpWords, 0.f);
-  for (size_t i = 0; i < ops_.size(); i += kOpWords) {
+  for (size_t i = first; i < ops_.size(); i += kOpWords) {
     const int64_t* o = &ops_[i];
     if (graph_on_ && (o[0] == OP_WAIT_SIGNAL || (o[0] == OP_GEMM && o[19] != 0)))
       join_others(o[1], main);
