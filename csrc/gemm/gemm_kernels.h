@@ -10,6 +10,7 @@
 #include <type_traits>
 
 #include "gemm.h"
+#include "tile_map.h"
 
 namespace ddlb {
 namespace {
@@ -25,13 +26,6 @@ typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
 
 __device__ __forceinline__ void glds16(const void* g, void* lds) {
   __builtin_amdgcn_global_load_lds((const GLB_AS void*)g, (LDS_AS void*)lds, 16, 0, 0);
-}
-
-// Rows and group sizes fit in 32 bits: 32-bit unsigned division is ~10x cheaper than 64-bit.
-__device__ __forceinline__ int64_t map_row(int64_t i, int64_t grp, int64_t gstride) {
-  const unsigned ui = (unsigned)i, ug = (unsigned)grp;
-  const unsigned q = ui / ug;
-  return (int64_t)q * gstride + (int64_t)(ui - q * ug);
 }
 
 // Address of logical A row ``row``: grouped rows, or a per-shard pointer table (direct access).
@@ -65,56 +59,8 @@ __device__ __forceinline__ char* c_row(const GemmArgs& p, int64_t row) {
   return (char*)base;
 }
 
-// Bijective XCD remap (guide §5, "XCD swizzle must be bijective").
-__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
-  const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, idx = bid >> 3;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-}
-
-// Block -> tile. Default: bijective XCD remap over the whole grid. With ``tile_order`` the grid
-// is dispatched shard-major (ordered_shard: the shard that arrives first runs first; with nsub > 1
-// row blocks of all producers interleave block-major) and XCD-remapped within each shard.
-__device__ __forceinline__ int tile_index_virtual(const GemmArgs& p, int vid, int nwg);
-// Dispatch position j -> shard: producers rotate fastest (own first), blocks slowest.
-__device__ __forceinline__ int ordered_shard(const GemmArgs& p, int j) {
-  const int np = p.nshards / p.nsub;
-  return ((p.first_shard + j % np) % np) * p.nsub + j / np;
-}
-
 __device__ __forceinline__ int tile_index(const GemmArgs& p, int nwg) {
   return tile_index_virtual(p, (int)blockIdx.x, nwg);
-}
-
-__device__ __forceinline__ int tile_index_virtual(const GemmArgs& p, int vid, int nwg) {
-  if (!p.tile_order) return xcd_remap(vid, nwg);
-  if (p.tile_order == 2) {
-    // shards interleaved: consecutive ids (one per XCD) walk different shards, so the tiles in
-    // flight cover every shard at once (a direct-store GEMM keeps every peer's link busy) and,
-    // with nshards dividing 8, each XCD stays on one shard (its A panels in that XCD's L2)
-    const int ns = p.nshards, per = nwg / ns;
-    return (vid % ns) * per + vid / ns;
-  }
-  const int per = nwg / p.nshards;
-  const int j = vid / per, local = vid % per;
-  return ordered_shard(p, j) * per + xcd_remap(local, per);
-}
-
-// Tile id -> (tm, tn). Row-major, except that without a shard order and with more than 4 column
-// tiles, ids are rastered in groups of 8 m-blocks (column-major inside a group): the 32 tiles an
-// XCD runs together (consecutive ids after xcd_remap) then cover 8 m-blocks x 4 n-blocks, i.e. 12
-// A / B panels in its L2 instead of 1 + 32 (guide §5, L2 reuse per XCD). Bijective.
-__device__ __forceinline__ void tile_mn(const GemmArgs& p, int wg, int tiles_m, int tiles_n,
-                                        int& tm, int& tn) {
-  constexpr int G = 8;
-  if (p.tile_order || tiles_n <= 4) {
-    tm = wg / tiles_n;
-    tn = wg % tiles_n;
-    return;
-  }
-  const int per = G * tiles_n, grp = wg / per, first = grp * G;
-  const int gs = tiles_m - first < G ? tiles_m - first : G, in = wg - grp * per;
-  tm = first + in % gs;
-  tn = in / gs;
 }
 
 // ---------------------------------------------------------------- MFMA "consume 16 bytes" ops
@@ -319,10 +265,8 @@ __device__ __forceinline__ void ag_copy_role(const GemmArgs& p) {
   const bool deep = (p.ag_mode & AG_DEEP_LOADS) != 0;
   unsigned seen = 0;
   for (int u = (int)blockIdx.x; u < units; u += p.ag_ctas) {
-    // within a block, consecutive units go to different producers: the ag_ctas units in flight
-    // at any time spread over every peer (every xGMI link) instead of ~ag_ctas / parts of them
-    const int b = u / per_b, r = u % per_b;
-    const int prod = (p.ag_rank + 1 + r % (np - 1)) % np, pi = r / (np - 1);
+    int b, prod, pi;  // every peer's units interleaved (tile_map.h)
+    ag_unit(u, np, parts, p.ag_rank, b, prod, pi);
     if (!((seen >> prod) & 1u)) {  // first unit of this producer: its READY, acquired
       if (tid == 0) {
         unsigned spins = 0;
@@ -2267,15 +2211,10 @@ hipError_t launch_pt4(const GemmArgs& p, hipStream_t s) {
   if (p.flags != nullptr && p.reserve_cus > 0) grid -= p.reserve_cus;
   GemmArgs q = p;
   q.ag_ctas = p.flags != nullptr && p.ag_ctas > 0 ? (p.ag_ctas + 7) / 8 * 8 : 0;
-  if (q.ag_ctas > 0 && (p.ag_mode & AG_FILL_ROUNDS) && grid - q.ag_ctas >= 8) {
-    // The GEMM takes ceil(tiles / gemm_ctas) rounds of tiles; every copy workgroup that leaves
-    // that count unchanged is free copy bandwidth (flagship: 1024 tiles, 224 GEMM CTAs = 5
-    // rounds, so 208 GEMM + 48 copy CTAs cost the GEMM nothing more than 224 + 32).
-    const int g0 = (grid - q.ag_ctas) / 8 * 8;
-    const int rounds = (tiles + g0 - 1) / g0;
-    const int need = ((tiles + rounds - 1) / rounds + 7) / 8 * 8;
-    if (grid - need > q.ag_ctas) q.ag_ctas = (grid - need) / 8 * 8;
-  }
+  // The GEMM takes ceil(tiles / gemm_ctas) rounds of tiles; every copy workgroup that leaves that
+  // count unchanged is free copy bandwidth (flagship: 1024 tiles, 224 GEMM CTAs = 5 rounds, so
+  // 208 GEMM + 48 copy CTAs cost the GEMM nothing more than 224 + 32).
+  if (q.ag_ctas > 0 && (p.ag_mode & AG_FILL_ROUNDS)) q.ag_ctas = ag_fill_ctas(grid, q.ag_ctas, tiles);
   grid -= q.ag_ctas;
   grid = (grid / 8) * 8;  // blockIdx % 8 == XCD group for every virtual tile id
   if (grid > tiles) grid = tiles;

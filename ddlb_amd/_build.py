@@ -46,7 +46,8 @@ SOURCES = [  # heaviest translation units first (the parallel build's critical p
     "runtime/plan.cpp",
     "bindings.cpp",
 ]
-HEADERS = ["gemm/gemm.h", "gemm/gemm_kernels.h", "gemm/gemm_entry.h", "runtime/kernels.h",
+HEADERS = ["gemm/gemm.h", "gemm/gemm_kernels.h", "gemm/gemm_entry.h", "gemm/tile_map.h",
+           "runtime/kernels.h",
            "comm/comm.h", "runtime/plan.h"]
 
 
