@@ -139,6 +139,13 @@ def _ipc_cfgs():
                                                       s=2, fused=True, signal="kernel",
                                                       multicast_protocol="kernel", copy_blocks=16,
                                                       dtype="float8_e4m3fn")))
+    cfgs.append(("col/coll/agk/mx", "col", dict(algorithm="coll_pipeline", backend="ipc", s=2,
+                                                fused=True, multicast_protocol="kernel",
+                                                copy_blocks=16, dtype="float8_e4m3fn",
+                                                gemm_mode="mx")))
+    cfgs.append(("row/p2p/direct/mx", "row", dict(algorithm="p2p_pipeline", backend="ipc",
+                                                  fused=True, dtype="float8_e4m3fn",
+                                                  gemm_mode="mx")))
     for alg in ("coll_pipeline", "p2p_pipeline"):  # the persistent gated GEMM (pt4 + reserve)
         cfgs.append((f"col/{alg}/fused/pt4", "col", dict(algorithm=alg, backend="ipc", s=2,
                                                          fused=True, tile="pt4")))
