@@ -31,3 +31,19 @@ def test_tile_maps_host_asan_ubsan(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
     assert "tile maps ok" in r.stdout
+
+
+def test_op_word_layout_matches_native():
+    """The Python plan encoder and the C++ executor agree on the op size (csrc/runtime/plan.h
+    kOpWords); a mismatch would shift every op's fields. Skipped when the extension is not built."""
+    import glob
+    import importlib
+
+    if not glob.glob(os.path.join(ROOT, "ddlb_amd", "_C*.so")):
+        pytest.skip("native extension not built")
+    import torch  # noqa: F401  (shared HIP runtime first)
+
+    from ddlb_amd.parallel.plan import OP_WORDS
+
+    C = importlib.import_module("ddlb_amd._C")
+    assert C.OP_WORDS == OP_WORDS
