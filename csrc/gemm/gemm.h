@@ -59,7 +59,8 @@ struct GemmArgs {
   // all its rows are read; the other workgroups run the gated GEMM. ag_tab (device, 2*np+2
   // entries, np = nshards / nsub producers): [src A of producer 0..np-1 | address of my ACK word
   // at producer 0..np-1 | READY words (ready[p] >= epoch: p's rows may be read) | counters
-  // (nshards per-segment, then np per-producer; monotonic across runs)].
+  // (nshards per-segment, then np per-producer; monotonic across runs) | with AG_WAIT_ACKS: my
+  // ACK word written by producer 0..np-1 (entry of my own rank unused)].
   int ag_ctas = 0, ag_parts = 1, ag_rank = 0;
   int ag_mode = 0;                  // AgMode bits below
   const uint64_t* ag_tab = nullptr;
@@ -83,6 +84,8 @@ enum AgMode : int {
   AG_AGENT_ACQUIRE = 2,    // the gated tiles acquire at agent scope (flags set by this launch)
   AG_DEEP_LOADS = 4,       // 16 loads in flight per lane instead of 8
   AG_FILL_ROUNDS = 8,      // grow ag_ctas while the GEMM's number of tile rounds stays the same
+  AG_WAIT_ACKS = 16,       // copy workgroup 0 waits for every peer's ACK before the launch ends
+                           // (ag_tab then has np more entries: my local ACK word per producer)
 };
 
 hipError_t gemm_launch(const GemmArgs& p, int din, int dout, int tile, int mode, hipStream_t s);

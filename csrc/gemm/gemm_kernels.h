@@ -314,6 +314,22 @@ __device__ __forceinline__ void ag_copy_role(const GemmArgs& p) {
                            __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
+  if ((p.ag_mode & AG_WAIT_ACKS) && blockIdx.x == 0 && tid == 0) {
+    // every peer has finished reading my rows before the launch ends (the caller may then
+    // overwrite them): the plan's ACK wait, without a kernel of its own after this one
+    for (int q = 0; q < np; ++q) {
+      if (q == p.ag_rank) continue;
+      const GLB_AS unsigned* a = (const GLB_AS unsigned*)tab[2 * np + 2 + q];
+      unsigned spins = 0;
+      while (__hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1u << 26)) {
+          if (p.timeout_word) atomicOr(p.timeout_word, 8u);
+          break;
+        }
+      }
+    }
+  }
 }
 
 // Arrival wait for the tile whose first logical row is m0 and which has (up to) BM rows.

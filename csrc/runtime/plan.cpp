@@ -363,6 +363,7 @@ void PlanExecutor::exec(const int64_t* o, hipStream_t main) {
     case OP_WAIT_SIGNAL: {
       const int n = (int)o[2];
       if (n < 1 || n > kMaxSignal || 5 + n > kOpWords) throw std::runtime_error("plan: bad wait");
+      if (o[3] == 2) return;  // performed inside the preceding in-kernel all-gather launch
       const int64_t v = (int64_t)epoch_ + o[4];
       if (v <= 0 && !graph_on_) return;  // nothing to wait for before the first epoch
       if (o[3] == 1 && !graph_on_) {

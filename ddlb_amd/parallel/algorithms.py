@@ -42,11 +42,12 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
-from ddlb_amd.parallel.plan import (COPY_ENGINE, COPY_KERNEL, DT_SIZE, DT_U8,
+from ddlb_amd.parallel.plan import (COPY_ENGINE, COPY_KERNEL, DT_SIZE, DT_U8, SIG_IN_LAUNCH,
                                     SIG_STREAM, Plan, Ref)
 
 S_MAIN, S_COMM = 0, 1
 TILE_PT4 = 19  # csrc/gemm/gemm.h Tile::TILE_PT4 (the only kernel carrying in-kernel copies)
+AG_WAIT_ACKS = 16  # csrc/gemm/gemm.h AgMode: the launch waits for the peers' ACKs itself
 
 
 def _s_copy(i: int) -> int:
@@ -73,8 +74,9 @@ class AlgoConfig:
     # in-kernel all-gather variant (csrc/gemm/gemm.h AgMode): 14 = write-through publication, 16
     # loads in flight per lane, agent-scope gate acquire (the fastest at world 1,
     # profiles/r02/s4/r2s4_2_agk_world1_modes.txt), copy workgroups grown while the GEMM's tile
-    # rounds stay the same (flagship: 48 instead of 32 at no GEMM cost, r2s4_5_*)
-    ag_mode: int = 14
+    # rounds stay the same (flagship: 48 instead of 32 at no GEMM cost, r2s4_5_*); + 16: the
+    # launch waits for the peers' ACKs itself (no wait kernel after it)
+    ag_mode: int = 30
     act: int = 0                        # columnwise: fused GEMM epilogue activation (ACT_*)
     direction: str = "pull"             # columnwise ipc: pull peers' shards | push mine to peers
 
@@ -268,15 +270,24 @@ def build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, dou
                 cfg)
         _signal(plan, S_MAIN, [flags.ref("ARRIVE", rank * cfg.s + j) for j in range(cfg.s)], cfg)
         seg = rows * k * ein
+        in_launch = bool(cfg.ag_mode & AG_WAIT_ACKS)
         ag = dict(ctas=cfg.copy_blocks, parts=max(1, min(seg // (256 << 10), 1024)), rank=rank,
                   src=[A.at(p) for p in range(d)],
                   ack=[flags.ref("ACK", rank, owner=p) for p in range(d)],
-                  ready=flags.ref("READY", 0), count=flags.ref("CNT", 0), mode=cfg.ag_mode)
+                  ready=flags.ref("READY", 0), count=flags.ref("CNT", 0), mode=cfg.ag_mode,
+                  wait_acks=[flags.ref("ACK", p) for p in range(d)] if in_launch else None)
         gdt_ag = dict(gdt, tile=TILE_PT4)
         plan.gemm(S_MAIN, A, Bt, C, M=m, N=n, K=k, lda=k, ldb=k, ldc=n, **gdt_ag,
                   flags=flags.ref("ARRIVE", 0), flag_rows=rows, nshards=d * cfg.s, nsub=cfg.s,
                   first_shard=rank, tile_order=1, reserve_cus=cfg.ag_reserve, ag=ag)
-        _wait(plan, S_MAIN, [flags.ref("ACK", p) for p in range(d) if p != rank], cfg)
+        # the ACK wait: the launch's first copy workgroup performs it (AG_WAIT_ACKS) and the op
+        # stays in the plan for the simulator; otherwise a wait kernel / stream wait
+        acks = [flags.ref("ACK", p) for p in range(d) if p != rank]
+        if in_launch:
+            for c in _chunks(acks):
+                plan.wait_signal(S_MAIN, c, method=SIG_IN_LAUNCH)
+        else:
+            _wait(plan, S_MAIN, acks, cfg)
     elif alg == "coll_pipeline" and be == "ipc" and cfg.fused:
         # ONE flag-gated GEMM over all m rows instead of s stage GEMMs: tiles are dispatched
         # block-major (block 0 of the own shard and of every peer, then block 1, ...), the order

@@ -43,6 +43,9 @@ ACT_CODE = {"none": ACT_NONE, "gelu": ACT_GELU, "relu": ACT_RELU, "silu": ACT_SI
 # copy / signal methods
 COPY_ENGINE, COPY_KERNEL = 0, 1
 SIG_KERNEL, SIG_STREAM = 0, 1
+# a wait the preceding in-kernel all-gather launch already performs (its copy role waits for the
+# ACKs before the launch ends): skipped by the executor, simulated as an ordinary wait
+SIG_IN_LAUNCH = 2
 
 
 @dataclass(frozen=True)
@@ -146,11 +149,15 @@ class Plan:
                 raise ValueError("in-kernel all-gather needs flags and one src / ack per producer")
             if not 1 <= ag["ctas"] < 1 << 20 or not 1 <= ag["parts"] < 1 << 20:
                 raise ValueError("ag ctas / parts out of range")
-            if not 0 <= ag.get("mode", 0) < 16:
+            if not 0 <= ag.get("mode", 0) < 32:
                 raise ValueError("ag mode out of range (csrc/gemm/gemm.h AgMode bits)")
+            acks_in = list(ag.get("wait_acks") or [])
+            if bool(acks_in) != bool(ag.get("mode", 0) & 16) or (acks_in and len(acks_in) != npro):
+                raise ValueError("ag mode 16 (AG_WAIT_ACKS) needs wait_acks: one local ACK word "
+                                 "per producer (and only then)")
             ag = dict(ag, table=self.table(f"__agtab{len(self.buffers)}",
                                            list(ag["src"]) + list(ag["ack"]) +
-                                           [ag["ready"], ag["count"]]))
+                                           [ag["ready"], ag["count"]] + acks_in))
         c_table = None
         if c_shards is not None:
             if c_shard_rows <= 0 or len(c_shards) * c_shard_rows < M or c_grp not in (0, M):

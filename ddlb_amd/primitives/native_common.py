@@ -31,8 +31,8 @@ capturable and the process has >= 4 HW queues), ``direction`` (columnwise ipc: `
 ``push`` my shard into every peer's gather buffer with posted xGMI writes), ``ag_mode`` (the in-kernel
 all-gather's copy variant, csrc/gemm/gemm.h ``AgMode`` bits: 1 plain stores + release fence instead
 of write-through stores, 2 agent-scope acquire in the gated tiles, 4 16 loads in flight per lane,
-8 more copy workgroups while the GEMM's tile rounds stay the same;
-default 14).
+8 more copy workgroups while the GEMM's tile rounds stay the same, 16 the launch waits for the
+peers' ACKs itself; default 30).
 """
 
 from __future__ import annotations
@@ -57,7 +57,7 @@ COMMON_DEFAULTS = {
     "reserve_cus": 32,
     "graph": False,
     "direction": "pull",
-    "ag_mode": 14,
+    "ag_mode": 30,
 }
 COMMON_ALLOWED = {
     "backend": ["rccl", "ipc", *UCC_BACKENDS],
@@ -77,7 +77,7 @@ COMMON_ALLOWED = {
     "reserve_cus": (0, 1024),
     "graph": [True, False, "auto"],
     "direction": ["pull", "push"],
-    "ag_mode": (0, 15),
+    "ag_mode": (0, 31),
 }
 COMMON_ALIASES = {
     "backend": {"nccl": "rccl", "cuda": "ipc"},
@@ -112,7 +112,7 @@ def algo_config(options, order: str = "AG_before") -> AlgoConfig:
         copy_blocks=int(options["copy_blocks"]), fused=bool(options["fused"]),
         reserve_cus=int(options.get("reserve_cus", 32)),
         copy_streams=int(options.get("copy_streams", 1)),
-        direction=options.get("direction", "pull"), ag_mode=int(options.get("ag_mode", 14)))
+        direction=options.get("direction", "pull"), ag_mode=int(options.get("ag_mode", 30)))
 
 
 def share_cus(cfg: AlgoConfig, communicator) -> AlgoConfig:

@@ -15,7 +15,7 @@ sys.path.insert(0, ROOT)
 
 
 def build(M, N, K, npro, nsub, ctas, gated=True, unit_kb=256, mode=0):
-    from ddlb_amd.parallel.plan import DT_BF16, Plan, SIG_KERNEL
+    from ddlb_amd.parallel.plan import DT_BF16, Plan, SIG_IN_LAUNCH, SIG_KERNEL
 
     rows = M // (npro * nsub)
     plan = Plan(0, 1, nstreams=1, stream_priority=[0])
@@ -34,11 +34,13 @@ def build(M, N, K, npro, nsub, ctas, gated=True, unit_kb=256, mode=0):
     seg = rows * K * 2
     ag = dict(ctas=ctas, parts=max(1, seg // (unit_kb << 10)), rank=0,
               src=[a] + [peer] * (npro - 1), ack=[ACK + 4 * p for p in range(npro)],
-              ready=READY, count=CNT, mode=mode)
+              ready=READY, count=CNT, mode=mode,
+              wait_acks=[ACK + 4 * p for p in range(npro)] if mode & 16 else None)
     plan.gemm(0, a, bt, c, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, din=DT_BF16, dout=DT_BF16,
               tile=19, flags=ARRIVE, flag_rows=rows, nshards=npro * nsub, nsub=nsub,
               first_shard=0, tile_order=1, ag=ag)
-    plan.wait_signal(0, [ACK + 4 * p for p in range(1, npro)], method=SIG_KERNEL)
+    plan.wait_signal(0, [ACK + 4 * p for p in range(1, npro)],
+                     method=SIG_IN_LAUNCH if mode & 16 else SIG_KERNEL)
     return plan
 
 

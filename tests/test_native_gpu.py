@@ -461,7 +461,7 @@ def test_flag_gated_persistent_gemm_world1(comm, graph):
     ctx.close()
 
 
-@pytest.mark.parametrize("mode", [0, 1, 6, 14])
+@pytest.mark.parametrize("mode", [0, 1, 6, 14, 30])
 @pytest.mark.parametrize("graph", [False, True])
 def test_in_kernel_allgather_world1(comm, graph, mode):
     """The in-kernel all-gather in one process: a local buffer stands in for the peer's copy of
@@ -472,7 +472,7 @@ def test_in_kernel_allgather_world1(comm, graph, mode):
     release fence, 6 write-through + 16 loads per lane + agent-scope gate acquire, 14 = 6 + copy
     workgroups grown while the GEMM's tile rounds stay the same)."""
     from ddlb_amd.parallel.context import NativeContext
-    from ddlb_amd.parallel.plan import DT_BF16, Plan, SIG_KERNEL, SIG_STREAM
+    from ddlb_amd.parallel.plan import DT_BF16, Plan, SIG_IN_LAUNCH, SIG_KERNEL, SIG_STREAM
 
     M, N, K, nsub = 32768, 1024, 1024, 4
     half, rows = M // 2, M // (2 * nsub)
@@ -487,11 +487,11 @@ def test_in_kernel_allgather_world1(comm, graph, mode):
     plan.signal(0, [READY + 4], method=sig)
     plan.signal(0, [ARRIVE + 4 * j for j in range(nsub)], method=sig)
     ag = dict(ctas=32, parts=8, rank=0, src=[a, peer], ack=[ACK, ACK + 4], ready=READY,
-              count=CNT, mode=mode)
+              count=CNT, mode=mode, wait_acks=[ACK, ACK + 4] if mode & 16 else None)
     plan.gemm(0, a, bt, c, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, din=DT_BF16, dout=DT_BF16,
               tile=19, flags=ARRIVE, flag_rows=rows, nshards=2 * nsub, nsub=nsub, first_shard=0,
               tile_order=1, ag=ag)
-    plan.wait_signal(0, [ACK + 4], method=sig)
+    plan.wait_signal(0, [ACK + 4], method=SIG_IN_LAUNCH if mode & 16 else sig)
     ctx = NativeContext(comm)
     bound = ctx.bind(plan)
     if graph:
