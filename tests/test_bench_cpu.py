@@ -85,7 +85,9 @@ def test_prewarm_runs_agree_across_ranks():
     got = dict(q.get(timeout=120) for _ in procs)
     for p in procs:
         p.join(timeout=60)
-    assert got[0] == got[1] and got[0] >= 30, got
+    # equal counts is the property; the count itself depends on the host's sleep granularity
+    # under load (rank 0 alone would ask for ~40 / 1.x ms, rank 1 for ~10)
+    assert got[0] == got[1] and got[0] >= 8, got
 
 
 def test_bench_rowwise_world2_cpu():
