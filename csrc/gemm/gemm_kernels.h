@@ -750,6 +750,29 @@ template <> struct Store8<DT_F32> {
   }
 };
 
+// The same 8 outputs through a buffer descriptor over C with cache bits sc1 | nt (aux 18): the
+// line leaves this XCD's L2 as it is written (write-through) instead of staying there as a dirty
+// streaming line. GEMM lab, one box (profiles/r02/s4/r2s4_17_*): pt4 flagship 0.1060 -> 0.1040 ms,
+// 16384x8192x1024 0.2347 -> 0.2177 ms vs plain nt stores.
+template <int OUT>
+__device__ __forceinline__ void store8_wt(__amdgpu_buffer_rsrc_t rc, unsigned off, const f32x4 a,
+                                          const f32x4 b) {
+  typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
+  constexpr int AUX = 18;  // sc1 | nt
+  if constexpr (OUT == DT_F32) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, a), rc, off, 0, AUX);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, b), rc, off + 16, 0, AUX);
+  } else if constexpr (OUT == DT_BF16) {
+    bf16x8 o = {(__bf16)a.x, (__bf16)a.y, (__bf16)a.z, (__bf16)a.w,
+                (__bf16)b.x, (__bf16)b.y, (__bf16)b.z, (__bf16)b.w};
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), rc, off, 0, AUX);
+  } else {
+    f16x8 o = {(_Float16)a.x, (_Float16)a.y, (_Float16)a.z, (_Float16)a.w,
+               (_Float16)b.x, (_Float16)b.y, (_Float16)b.z, (_Float16)b.w};
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), rc, off, 0, AUX);
+  }
+}
+
 template <class Mma, int OUT>
 __global__ __launch_bounds__(512) void gemm_tn_ring_kernel(const GemmArgs p) {
   constexpr int NS = 4, BM = 256, BN = 256, WN = 4, ROWB = 64;
@@ -1490,7 +1513,9 @@ __global__ __launch_bounds__(512) void gemm_tn_t4_kernel(const GemmArgs p) {
 // Measured (scripts/lab, profiles/r01/s2/lab/t8_vs_ring2.txt): flagship 0.1127 vs t4 0.1160 ms.
 // GATED: the arrival-flag form (a separate instantiation, so the ungated kernel's code and
 // schedule are exactly those measured without flags).
-template <class Mma, int OUT, bool GATED, bool DS = false>
+// CMODE: 0 = grouped C rows, plain nt stores; 1 = C row-block table (direct store); 2 = grouped C
+// rows, write-through nt buffer stores (C's byte extent below 2 GiB: 32-bit offsets)
+template <class Mma, int OUT, bool GATED, int CMODE = 0>
 __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   constexpr int ROWB = 128, UNIT = 128 * ROWB, STAGE = 4 * UNIT;
   constexpr int UA0 = 0, UA1 = UNIT, UB0 = 2 * UNIT, UB1 = 3 * UNIT;
@@ -1498,6 +1523,9 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   constexpr int OSZ = out_size<OUT>();
   constexpr bool PAIR = is_pair<Mma>::value;
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  // CMODE 2: C through one wave-uniform descriptor (launch_pt4 checks the extent fits)
+  const __amdgpu_buffer_rsrc_t crc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.c, 0, 0x7FFFFFF0, 0x00020000);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -1626,7 +1654,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     for (int f = 0; f < 4; ++f) {
       const int i = mq * 4 + f;
       const int64_t row = m0 + wr * 128 + mq * 64 + f * 16 + frow;
-      char* dst = c_row<OSZ, DS ? 1 : 0>(p, row) +
+      char* dst = c_row<OSZ, CMODE == 1 ? 1 : 0>(p, row) +
                   (n0 + wc * 64 + nq * 32 + fq * 8) * OSZ;
       // one store site (two branch-local stores get merged by the optimizer, which drops the
       // non-temporal hint)
@@ -1635,7 +1663,10 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
         v0 = act4(v0, p.act);
         v1 = act4(v1, p.act);
       }
-      Store8<OUT>::st(dst, v0, v1);
+      if constexpr (CMODE == 2)
+        store8_wt<OUT>(crc, (unsigned)(dst - (char*)p.c), v0, v1);
+      else
+        Store8<OUT>::st(dst, v0, v1);
       acc[i][nq * 2] = f32x4{0.f, 0.f, 0.f, 0.f};
       acc[i][nq * 2 + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
@@ -2235,12 +2266,22 @@ hipError_t launch_pt4(const GemmArgs& p, hipStream_t s) {
   grid = (grid / 8) * 8;  // blockIdx % 8 == XCD group for every virtual tile id
   if (grid > tiles) grid = tiles;
   if (grid < 1) grid = 1;
-  if (p.flags != nullptr)
+  // write-through C stores (CMODE 2) whenever every C byte is within 2 GiB of p.c (32-bit buffer
+  // offsets); C row tables (direct store) and larger outputs keep plain nt stores
+  const int64_t cg = p.c_grp > 0 ? p.c_grp : p.M, cgs = p.c_gstride > 0 ? p.c_gstride : cg;
+  const int64_t last_row = (int64_t)(p.M - 1) / cg * cgs + (int64_t)(p.M - 1) % cg;
+  const bool wt = p.c_table == nullptr && getenv("DDLB_PT4_NT_STORES") == nullptr &&
+                  (last_row * p.ldc + p.N) * (int64_t)out_size<OUT>() < 0x7FFFFFF0LL;
+  if (p.flags != nullptr && wt)
+    hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, true, 2>), dim3(grid + q.ag_ctas), dim3(512),
+                       0, s, q);
+  else if (p.flags != nullptr)
     hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, true>), dim3(grid + q.ag_ctas), dim3(512), 0,
                        s, q);
   else if (p.c_table != nullptr)
-    hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false, true>), dim3(grid), dim3(512), 0, s,
-                       p);
+    hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false, 1>), dim3(grid), dim3(512), 0, s, p);
+  else if (wt)
+    hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false, 2>), dim3(grid), dim3(512), 0, s, p);
   else
     hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false>), dim3(grid), dim3(512), 0, s, p);
   return hipGetLastError();

@@ -1493,7 +1493,17 @@ __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
     const f32x4 v0 = acc[i][nq * 2], v1 = acc[i][nq * 2 + 1];
     bf16x8 o = {(__bf16)v0.x, (__bf16)v0.y, (__bf16)v0.z, (__bf16)v0.w,
                 (__bf16)v1.x, (__bf16)v1.y, (__bf16)v1.z, (__bf16)v1.w};
-    if constexpr ((SKIP & 32) != 0) {  // timing only: same bytes, one full 128 B line per 8 lanes
+    if constexpr ((SKIP & (16384 | 32768)) != 0) {
+      // C through a buffer descriptor with explicit cache bits: 16384 = sc1 (write-through, the
+      // line leaves this XCD's L2), + 16 = sc1 | nt, 32768 = sc0 | sc1
+      constexpr int AUX = (SKIP & 32768) ? 17 : ((SKIP & 16) ? 18 : 16);
+      const __amdgpu_buffer_rsrc_t rc =
+          __builtin_amdgcn_make_buffer_rsrc((void*)p.c, 0, 0x7FFFFFF0, 0x00020000);
+      const int64_t off = (crow - (char*)p.c) + (n0 + wc * 64 + nq * 32 + fq * 8) * 2;
+      typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), rc, (unsigned)off, 0,
+                                             AUX);
+    } else if constexpr ((SKIP & 32) != 0) {  // timing only: same bytes, one full 128 B line per 8 lanes
       const int rl = lane >> 3, ch = lane & 7;
       char* rrow = (char*)p.c + (m0 + wr * 128 + mq * 64 + f * 16 + nq * 8 + rl) * p.ldc * 2;
       char* dst = rrow + (n0 + wc * 64 + ch * 8) * 2;
@@ -2099,6 +2109,9 @@ int main(int argc, char** argv) {
       {"pt4 noLDSrd", pt4_kernel<false, 8>, 2, 512, 0},
       {"pt4 noDMA noST", pt4_kernel<false, 3>, 2, 512, 0},
       {"pt4 noDMA noST noLDSrd", pt4_kernel<false, 11>, 2, 512, 0},
+      {"pt4 wt", pt4_kernel<false, 16384>, 2, 512, 0},
+      {"pt4 wt nt", pt4_kernel<false, 16384 | 16>, 2, 512, 0},
+      {"pt4 sc01", pt4_kernel<false, 32768>, 2, 512, 0},
       {"q4", q4_kernel<0>, 2, 256, 1},
       {"q4 noDMA", q4_kernel<0, 1>, 2, 256, 1},
       {"q4 noBAR", q4_kernel<0, 2>, 2, 256, 1},
@@ -2106,14 +2119,26 @@ int main(int argc, char** argv) {
       {"q4 noMFMA", q4_kernel<0, 4>, 2, 256, 1},
   };
   Args a{A, B, C, K, K, N, M, N, K, nullptr};
-  const char* only = getenv("LAB_ONLY");  // profile one variant: skip the others
+  const char* only = getenv("LAB_ONLY");  // comma-separated variant names: skip the others
+  auto skip = [&](const char* name) {
+    if (!only) return false;
+    const size_t n = strlen(name);
+    for (const char* q = only; *q;) {
+      const char* e = strchr(q, ',');
+      const size_t l = e ? (size_t)(e - q) : strlen(q);
+      if (l == n && strncmp(q, name, n) == 0) return false;
+      if (!e) break;
+      q = e + 1;
+    }
+    return true;
+  };
   const double flop = 2.0 * M * N * K;
   std::vector<std::vector<float>> times(sizeof(vs) / sizeof(vs[0]));
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
   for (size_t v = 0; v < sizeof(vs) / sizeof(vs[0]); ++v) {
-    if (only && strcmp(only, vs[v].name) != 0) continue;
+    if (skip(vs[v].name)) continue;
     CHECK(hipMemset(C, 0, (size_t)M * N * 2));
     CHECK(hipMemset(err, 0, 4));
     const int gv = vs[v].all_tiles ? (M / 256) * (N / 256) : grid;
@@ -2126,7 +2151,7 @@ int main(int argc, char** argv) {
   }
   for (int r = 0; r < rounds; ++r)
     for (size_t v = 0; v < sizeof(vs) / sizeof(vs[0]); ++v) {
-      if (only && strcmp(only, vs[v].name) != 0) continue;
+      if (skip(vs[v].name)) continue;
       const int gv = vs[v].all_tiles ? (M / 256) * (N / 256) : grid;
       for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(vs[v].fn, dim3(gv), dim3(vs[v].threads), 0, 0, a);
       CHECK(hipEventRecord(e0));
