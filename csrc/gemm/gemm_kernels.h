@@ -1330,7 +1330,7 @@ __global__ __launch_bounds__(512) void gemm_tn_t8_kernel(const GemmArgs p) {
 // last K-tile as in t8. Measured (scripts/lab, profiles/r01/s2/lab/t8_vs_ring2.txt): 9 % faster
 // than t8 with one short-K tile per CU (16384x1024x1024), 3 % at 65536x1024x8192, 3 % slower at
 // 8192^3.
-template <class Mma, int OUT>
+template <class Mma, int OUT, int CMODE = 0>  // CMODE 2: write-through nt C stores (as pt4)
 __global__ __launch_bounds__(512) void gemm_tn_t4_kernel(const GemmArgs p) {
   constexpr int ROWB = 128, UNIT = 128 * ROWB, STAGE = 4 * UNIT;
   constexpr int UA0 = 0, UA1 = UNIT, UB0 = 2 * UNIT, UB1 = 3 * UNIT;
@@ -1479,10 +1479,12 @@ __global__ __launch_bounds__(512) void gemm_tn_t4_kernel(const GemmArgs p) {
 #undef T4_LGKM0
   wait_vm<0>();  // never leave an LDS-DMA in flight past the end of the workgroup
   constexpr int OSZ = out_size<OUT>();
+  const __amdgpu_buffer_rsrc_t crc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.c, 0, 0x7FFFFFF0, 0x00020000);
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int64_t row = m0 + wr * 128 + (i >> 2) * 64 + (i & 3) * 16 + frow;
-    char* crow = c_row<OSZ>(p, row);
+    char* crow = c_row<OSZ, CMODE == 2 ? 0 : 2>(p, row);
 #pragma unroll
     for (int nq = 0; nq < 2; ++nq) {
       char* dst = crow + (n0 + wc * 64 + nq * 32 + fq * 8) * OSZ;
@@ -1493,7 +1495,10 @@ __global__ __launch_bounds__(512) void gemm_tn_t4_kernel(const GemmArgs p) {
         v0 = act4(v0, p.act);
         v1 = act4(v1, p.act);
       }
-      Store8<OUT>::st(dst, v0, v1);
+      if constexpr (CMODE == 2)
+        store8_wt<OUT>(crc, (unsigned)(dst - (char*)p.c), v0, v1);
+      else
+        Store8<OUT>::st(dst, v0, v1);
     }
   }
 }
@@ -2233,10 +2238,24 @@ hipError_t launch_t8(const GemmArgs& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Write-through C stores (CMODE 2 of pt4 / t4) whenever every C byte is within 2 GiB of p.c
+// (32-bit buffer offsets); C row tables (direct store) and larger outputs keep plain nt stores.
+// DDLB_PT4_NT_STORES=1 forces nt stores (A/B knob).
+inline bool c_fits_wt(const GemmArgs& p, int osz) {
+  static const bool nt = getenv("DDLB_PT4_NT_STORES") != nullptr;
+  if (nt || p.c_table != nullptr || p.M <= 0) return false;
+  const int64_t cg = p.c_grp > 0 ? p.c_grp : p.M, cgs = p.c_gstride > 0 ? p.c_gstride : cg;
+  const int64_t last_row = (int64_t)(p.M - 1) / cg * cgs + (int64_t)(p.M - 1) % cg;
+  return (last_row * p.ldc + p.N) * (int64_t)osz < 0x7FFFFFF0LL;
+}
+
 template <class Mma, int OUT>
 hipError_t launch_t4(const GemmArgs& p, hipStream_t s) {
   const int tiles = (p.M / 256) * (p.N / 256);
-  hipLaunchKernelGGL((gemm_tn_t4_kernel<Mma, OUT>), dim3(tiles), dim3(512), 0, s, p);
+  if (c_fits_wt(p, out_size<OUT>()))
+    hipLaunchKernelGGL((gemm_tn_t4_kernel<Mma, OUT, 2>), dim3(tiles), dim3(512), 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm_tn_t4_kernel<Mma, OUT>), dim3(tiles), dim3(512), 0, s, p);
   return hipGetLastError();
 }
 
@@ -2266,12 +2285,7 @@ hipError_t launch_pt4(const GemmArgs& p, hipStream_t s) {
   grid = (grid / 8) * 8;  // blockIdx % 8 == XCD group for every virtual tile id
   if (grid > tiles) grid = tiles;
   if (grid < 1) grid = 1;
-  // write-through C stores (CMODE 2) whenever every C byte is within 2 GiB of p.c (32-bit buffer
-  // offsets); C row tables (direct store) and larger outputs keep plain nt stores
-  const int64_t cg = p.c_grp > 0 ? p.c_grp : p.M, cgs = p.c_gstride > 0 ? p.c_gstride : cg;
-  const int64_t last_row = (int64_t)(p.M - 1) / cg * cgs + (int64_t)(p.M - 1) % cg;
-  const bool wt = p.c_table == nullptr && getenv("DDLB_PT4_NT_STORES") == nullptr &&
-                  (last_row * p.ldc + p.N) * (int64_t)out_size<OUT>() < 0x7FFFFFF0LL;
+  const bool wt = c_fits_wt(p, out_size<OUT>());
   if (p.flags != nullptr && wt)
     hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, true, 2>), dim3(grid + q.ag_ctas), dim3(512),
                        0, s, q);
