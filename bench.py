@@ -16,16 +16,26 @@ Other BASELINE configs through the same machinery: ``--primitive tp_rowwise -m 1
 -k 8192`` (config #3, GEMM + reduce-scatter; strong scaling: the harness number is the whole-job
 aggregate) and ``--dtype float8_e4m3fn`` (config #5; adds the block-scaled MX-fp8 candidates).
 
+What runs in the timed region: only the ``native`` slot's own hand-written MFMA kernels (with
+RCCL / IPC data movement at N>1). The vendor library (hipBLASLt through ``torch.matmul``, RCCL
+through torch) is measured beside it as the ``pytorch`` / ``compute_only(torch)`` slots and
+reported as ``vendor_ms``; it becomes the headline only if every native candidate fails, and
+the JSON then says so (``implementation``, ``gemm``).
+
 Process model (robust by construction): the launched processes never touch the GPU. They form
 a gloo group and run every measurement in a child process per rank (fresh HIP context, its own
-rendezvous port, a hard timeout). An autotuner first times each candidate algorithm in its own
-children (MAX over ranks), then the winner runs the timed measurement (falling back to the next
-fastest if it fails there); a candidate that fails or hangs is killed and skipped on every rank,
-so one bad path cannot hang the job. Every rank issues the same number of run() calls (the
-pre-warm count is MAX-reduced), as each call holds collectives / epoch-matched signals.
-Candidate timings are reported in the JSON (``autotune_ms``), progress on stderr. Synthetic
-U[-1,1) inputs of the named shape (no datasets exist offline); the result is validated against
-an fp32 reference.
+rendezvous port, a hard timeout). At N>1 a preflight (``ddlb_amd.parallel.preflight``) first
+checks, in time-limited children, that RCCL and the IPC / xGMI mechanisms work across this
+node's GPUs; candidate families that fail are dropped, and a broken RCCL control plane makes
+the children coordinate over gloo instead. An autotuner then times each candidate (validated,
+MAX over ranks), RCCL candidates first, and the winner runs the timed measurement (falling back
+to the next fastest if it fails there). The whole job runs against ONE wall-clock deadline
+(``--deadline-s``): tuning stops early enough to leave the final run its time, and every child's
+timeout is cut to what is left, so a node where candidates hang still reports inside it.
+Every rank issues the same number of run() calls (the pre-warm count is MAX-reduced), as each
+call holds collectives / epoch-matched signals. Synthetic U[-1,1) inputs of the named shape (no
+datasets exist offline); the result is validated against an fp32 reference, with the
+reference's rule (atol = 1e-3 k) and a tight internal bound (max|err| <= 2^-7 max|ref| + k 2^-12).
 """
 
 from __future__ import annotations
@@ -42,141 +52,129 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-# (label, impl, options). "/blas" = the plan's plain GEMM ops on hipBLASLt (gemm_mode=blas),
-# everything else identical.
-def _blas(opts):
-    return dict(opts, gemm_mode="blas")
-
+TIMING = ("cpu_clock window: barrier + device sync, K back-to-back run() calls, device sync; "
+          "mean per step, MAX over ranks")
 
 _COLL4 = dict(algorithm="coll_pipeline", backend="rccl", s=4)
 _DEF = dict(algorithm="default", backend="rccl")
 _P2P = dict(algorithm="p2p_pipeline", backend="ipc", multicast_protocol="memcpy")
 _COLL_IPC = dict(algorithm="coll_pipeline", backend="ipc", multicast_protocol="memcpy", s=4)
 _DEF_K = dict(algorithm="default", backend="ipc", multicast_protocol="kernel", copy_blocks=128)
-# Pipeline stages use grouped-row GEMMs, which stay on the MFMA kernels (hipBLASLt only takes
-# plain GEMMs), so coll_pipeline has no "/blas" twin.
-# Flag-gated ("fused") GEMMs: ONE GEMM launch whose tiles spin until their rows have landed.
-# With ranks sharing one GPU (the only multi-rank rehearsal available here) the spinning tiles of
-# one rank hold the CUs the other needs and ran 30-100x slower (profiles/r01/s2/); on a real node
-# each rank owns its GPU and the copy engines fill the flags without any CU, so the block-major
-# fused coll_pipeline (no per-stage GEMM tails, one launch) stays in the pool. The whole-shard
-# p2p form stays a CLI option (a tile waits for its entire 1/d shard).
+# In-kernel all-gather ("agk"): ONE launch per run; its first copy_blocks workgroups pull the
+# peers' row blocks over xGMI and flag them, the rest run the persistent GEMM gated on the flags
+# (no copy streams, no host op per block, one kernel to capture).
+_AGK = dict(algorithm="coll_pipeline", backend="ipc", multicast_protocol="kernel", fused=True,
+            s=8, copy_blocks=32)
 
 
 def _graph(opts):
     return dict(opts, graph=True)
 
 
-# Ordered by expected strength at d = 8 (the tuning budget may cut the tail of the list).
-# "/graph": the whole plan is captured once and replayed with one hipGraphLaunch per run; the
-# IPC pipelines issue one HIP call per copy / event / signal (~2 us of host time each, ~200 calls
-# per run at d = 8, s = 8: host-bound without the graph, profiles/r02/r2_13_*).
-# In-kernel all-gather ("agk"): ONE launch per run; its first copy_blocks workgroups pull the
-# peers' row blocks over xGMI and flag them, the rest run the persistent GEMM gated on the flags
-# (no copy streams, no host op per block, one kernel to capture).
-_AGK = dict(algorithm="coll_pipeline", backend="ipc", multicast_protocol="kernel", fused=True,
-            s=8, copy_blocks=32)
+# N > 1, RCCL candidates first: RCCL is the vendor-proven transport and our plans drive it on
+# our own communicator and streams (BASELINE config #4 = coll_pipeline over RCCL). The IPC / xGMI
+# candidates follow; the preflight drops whichever family this node cannot run.
+# "/graph": the whole plan is captured once and replayed with one hipGraphLaunch per run (the IPC
+# pipelines issue ~200 HIP calls per run at d = 8 otherwise, profiles/r02/r2_13_*).
 CANDIDATES = [
     ("coll_pipeline/rccl/s4", "native", _COLL4),
+    ("coll_pipeline/rccl/s8", "native", dict(_COLL4, s=8)),
+    ("default/rccl", "native", _DEF),
+    # the stage GEMMs next to RCCL's CU-resident kernels: 128x128 tiles (4x as many, dispatched
+    # dynamically) let the CUs busy with RCCL simply take fewer of them
+    ("coll_pipeline/rccl/s4/128", "native", dict(_COLL4, tile="128x128")),
+    # RCCL's kernels on a CU-masked comm stream (csrc/comm: hipExtStreamCreateWithCUMask), the
+    # stage GEMMs sized to the complement; buffers registered with ncclCommRegister
+    ("coll_pipeline/rccl/s4/cumask", "native", dict(_COLL4, comm_cus=32, register=True)),
+    ("coll_pipeline/rccl/s4/128/c16", "native", dict(_COLL4, tile="128x128",
+                                                      _env={"NCCL_MAX_NCHANNELS": "16"})),
+    ("p2p_pipeline/rccl", "native", dict(algorithm="p2p_pipeline", backend="rccl")),
     ("coll_pipeline/ipc/agk32/s8/graph", "native", _graph(_AGK)),
     ("coll_pipeline/ipc/agk64/s8/graph", "native", _graph(dict(_AGK, copy_blocks=64))),
     ("coll_pipeline/ipc/memcpy/s8/graph", "native", _graph(dict(_COLL_IPC, s=8))),
     ("coll_pipeline/ipc/kernel/s8/graph", "native", _graph(dict(
         _COLL_IPC, s=8, multicast_protocol="kernel", copy_blocks=128, tile="128x128"))),
-    ("coll_pipeline/ipc/memcpy/s8/fused/graph", "native", _graph(dict(_COLL_IPC, s=8,
-                                                                      fused=True))),
     ("direct/ipc", "native", dict(algorithm="direct", backend="ipc")),
-    ("coll_pipeline/ipc/memcpy/s4/fused/graph", "native", _graph(dict(_COLL_IPC, fused=True))),
+    ("coll_pipeline/ipc/batch/s8/graph", "native", _graph(dict(
+        _COLL_IPC, s=8, multicast_protocol="batch_memcpy"))),
     ("coll_pipeline/ipc/memcpy/s4/graph", "native", _graph(_COLL_IPC)),
-    # each peer's chunks split over 2 copy streams (2 copy engines per link): a hedge for links
-    # faster than one engine, which is what bounds the few-GPU runs (one link per peer); not
-    # graph-captured (hipGraph replay of split copies segfaulted, profiles/r02/r2_22_*)
+    ("p2p_pipeline/ipc/memcpy/graph", "native", _graph(_P2P)),
+    # one flag-gated GEMM fed by copy-engine pulls: eager only (a graph would have to order the
+    # gated GEMM after every copy stream, see PlanExecutor::graph_capturable)
+    ("coll_pipeline/ipc/memcpy/s8/fused", "native", dict(_COLL_IPC, s=8, fused=True)),
+    # each peer's chunks split over 2 copy streams (2 copy engines per link)
     ("coll_pipeline/ipc/memcpy/s8/cs2", "native", dict(_COLL_IPC, s=8, copy_streams=2)),
-    # Stage GEMMs next to CU-resident comm kernels (our copy kernel): 128x128 tiles (4x as many,
-    # dispatched dynamically) let the CUs busy with copies simply take fewer of them
     ("coll_pipeline/ipc/kernel/s4", "native", dict(_COLL_IPC, multicast_protocol="kernel",
                                                    copy_blocks=128, tile="128x128")),
-    ("default/rccl", "native", _DEF),
-    ("default/rccl/blas", "native", _blas(_DEF)),
-    ("p2p_pipeline/ipc/memcpy/graph", "native", _graph(_P2P)),
-    ("p2p_pipeline/ipc/memcpy/cs2", "native", dict(_P2P, copy_streams=2)),
-    # HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default); the
-    # memcpy protocol uses one copy stream per peer (9 streams at d=8): a variant where no two of
-    # its streams share a queue (one process per GPU here, so 12 queues on the device)
-    ("coll_pipeline/ipc/memcpy/s8/q12", "native", dict(_COLL_IPC, s=8,
-                                                        _env={"GPU_MAX_HW_QUEUES": "12"})),
     ("coll_pipeline/ipc/memcpy/s8", "native", dict(_COLL_IPC, s=8)),
     ("coll_pipeline/ipc/agk32/s4/graph", "native", _graph(dict(_AGK, s=4))),
-    ("coll_pipeline/ipc/agk32/s8", "native", _AGK),
     ("default/ipc/kernel", "native", _DEF_K),
-    # the same reasoning for RCCL's CU-resident kernels, and RCCL held to 16 channels (16 CUs)
-    ("coll_pipeline/rccl/s4/128", "native", dict(_COLL4, tile="128x128")),
-    ("coll_pipeline/rccl/s8", "native", dict(_COLL4, s=8)),
-    ("coll_pipeline/rccl/s8/128", "native", dict(_COLL4, s=8, tile="128x128")),
-    ("coll_pipeline/rccl/s4/128/c16", "native", dict(_COLL4, tile="128x128",
-                                                      _env={"NCCL_MAX_NCHANNELS": "16"})),
-    ("coll_pipeline/ipc/kernel/s8", "native", dict(_COLL_IPC, s=8, multicast_protocol="kernel",
-                                                   copy_blocks=128, tile="128x128")),
-    ("coll_pipeline/ipc/memcpy/s4", "native", _COLL_IPC),
-    ("p2p_pipeline/ipc/memcpy", "native", _P2P),
-    ("p2p_pipeline/ipc/push", "native", dict(_P2P, direction="push")),
-    ("default/ipc/push", "native", dict(_P2P, algorithm="default", direction="push")),
+    ("p2p_pipeline/ipc/memcpy/cs2", "native", dict(_P2P, copy_streams=2)),
     ("coll_pipeline/ipc/push/s4", "native", dict(_COLL_IPC, direction="push")),
-    ("default/ipc/kernel/push", "native", dict(_DEF_K, direction="push")),
-    ("p2p_pipeline/rccl", "native", dict(algorithm="p2p_pipeline", backend="rccl")),
-    # kernel-side flags (one spin / store kernel for all flags of an op instead of one rocclr
-    # stream-memop kernel per flag)
-    ("default/ipc/kernel/ksig", "native", dict(_DEF_K, signal="kernel")),
+    ("default/ipc/push", "native", dict(_P2P, algorithm="default", direction="push")),
+]
+VENDOR = [
     ("pytorch(rccl+hipblaslt)", "pytorch", dict(backend="nccl", empty_cache=False)),
 ]
-# world 1: the all-gather is the identity; the plan is one GEMM on either kernel family
+# world 1: the all-gather is the identity; the plan is one GEMM (our kernel families)
 WORLD1 = [
-    ("gemm (world=1)/hip", "native", _DEF),
-    ("gemm (world=1)/blas", "native", _blas(_DEF)),
+    ("gemm (world=1)/auto", "native", _DEF),
+    ("gemm (world=1)/t4", "native", dict(_DEF, tile="t4")),
+    ("gemm (world=1)/pt8", "native", dict(_DEF, tile="pt8")),
+]
+WORLD1_VENDOR = [
+    ("compute_only(hipblaslt)", "compute_only", dict(size="unsharded", gemm="torch")),
+    ("pytorch(rccl+hipblaslt)", "pytorch", dict(backend="nccl", empty_cache=False)),
 ]
 # tp_rowwise (GEMM + sequence-parallel reduce-scatter; BASELINE config #3)
 _RK = dict(backend="ipc", multicast_protocol="kernel", copy_blocks=128)
 ROW_CANDIDATES = [
     ("row/default/rccl", "native", dict(algorithm="default", backend="rccl")),
-    ("row/default/rccl/blas", "native", _blas(dict(algorithm="default", backend="rccl"))),
     ("row/coll_pipeline/rccl/s4", "native", dict(algorithm="coll_pipeline", backend="rccl", s=4)),
     ("row/coll_pipeline/rccl/s4/128", "native", dict(algorithm="coll_pipeline", backend="rccl",
                                                      s=4, tile="128x128")),
     ("row/p2p_pipeline/rccl", "native", dict(algorithm="p2p_pipeline", backend="rccl")),
-    ("row/default/ipc/kernel", "native", dict(_RK, algorithm="default")),
-    ("row/default/ipc/kernel/blas", "native", _blas(dict(_RK, algorithm="default"))),
-    ("row/coll_pipeline/ipc/kernel/s4", "native", dict(_RK, algorithm="coll_pipeline", s=4)),
     # direct store: ONE GEMM whose epilogue writes every peer's partial into its receive slot
     # over xGMI (shard-interleaved tiles: all links at once), then one local d-way reduce
     ("row/p2p_pipeline/ipc/direct/graph", "native", _graph(dict(algorithm="p2p_pipeline",
                                                                 backend="ipc", fused=True))),
     ("row/p2p_pipeline/ipc/direct", "native", dict(algorithm="p2p_pipeline", backend="ipc",
                                                    fused=True)),
+    ("row/default/ipc/kernel", "native", dict(_RK, algorithm="default")),
+    ("row/coll_pipeline/ipc/kernel/s4", "native", dict(_RK, algorithm="coll_pipeline", s=4)),
     ("row/p2p_pipeline/ipc/memcpy", "native", dict(algorithm="p2p_pipeline", backend="ipc")),
     ("row/coll_pipeline/ipc/kernel/s4/graph", "native", _graph(dict(_RK, algorithm="coll_pipeline",
                                                                     s=4))),
     ("row/p2p_pipeline/ipc/memcpy/graph", "native", _graph(dict(algorithm="p2p_pipeline",
                                                                  backend="ipc"))),
+]
+ROW_VENDOR = [
     ("row/pytorch(rccl+hipblaslt)", "pytorch", dict(backend="nccl", empty_cache=False)),
 ]
 ROW_WORLD1 = [
-    ("row/gemm (world=1)/hip", "native", dict(algorithm="default", backend="rccl")),
-    ("row/gemm (world=1)/blas", "native", _blas(dict(algorithm="default", backend="rccl"))),
+    ("row/gemm (world=1)/auto", "native", dict(algorithm="default", backend="rccl")),
+    ("row/gemm (world=1)/t4", "native", dict(algorithm="default", backend="rccl", tile="t4")),
+]
+ROW_WORLD1_VENDOR = [
+    ("row/compute_only(hipblaslt)", "compute_only", dict(gemm="torch")),
+    ("row/pytorch(rccl+hipblaslt)", "pytorch", dict(backend="nccl", empty_cache=False)),
 ]
 
 
 def candidate_pool(primitive: str, dtype: str, world: int):
-    """(label, impl, options) list for one primitive / dtype / world size. fp8 inputs add the
-    block-scaled MX-fp8 MFMA (2x the bf16 rate) and drop hipBLASLt (no fp8 in the plain path)."""
-    if primitive == "tp_rowwise":
-        pool = ROW_WORLD1 if world == 1 else ROW_CANDIDATES
+    """(label, impl, options) list for one primitive / dtype / world size: our native
+    candidates first, then the vendor-library slots (measured for ``vendor_ms``). fp8 inputs add
+    the block-scaled MX-fp8 MFMA (2x the bf16 rate) to every native candidate."""
+    row = primitive == "tp_rowwise"
+    if world == 1:
+        native, vendor = (ROW_WORLD1, ROW_WORLD1_VENDOR) if row else (WORLD1, WORLD1_VENDOR)
     else:
-        pool = WORLD1 if world == 1 else CANDIDATES
+        native, vendor = (ROW_CANDIDATES, ROW_VENDOR) if row else (CANDIDATES, VENDOR)
     if dtype == "float8_e4m3fn":
-        pool = [c for c in pool if c[2].get("gemm_mode") != "blas"]
-        pool = pool + [(lbl + "/mx", impl, dict(opts, gemm_mode="mx")) for lbl, impl, opts in pool
-                       if impl == "native"]
-    return pool
+        native = native + [(lbl + "/mx", impl, dict(opts, gemm_mode="mx"))
+                           for lbl, impl, opts in native]
+        vendor = [c for c in vendor if c[1] != "compute_only"]  # torch.matmul has no fp8
+    return list(native) + list(vendor)
 
 
 # ------------------------------------------------------------------------------- child
@@ -200,13 +198,38 @@ def prewarm_runs(impl, comm, prewarm_ms: float, calib: int = 4) -> int:
 
 
 def _check(impl, out, res) -> bool:
-    """Validate one output; a mismatch is recorded in ``res`` (not raised)."""
+    """Validate one output: the reference's rule, then the tight internal bound. A mismatch is
+    recorded in ``res`` (not raised)."""
     try:
         impl.validate(out)
-        return True
     except AssertionError as e:
         res["validation"] = str(e).splitlines()[0][:200]
         return False
+    num = impl.numerics(out)
+    res["max_err"], res["err_bound"] = round(num["max_err"], 6), round(num["bound"], 6)
+    if not num["ok"]:
+        res["validation"] = (f"tight check: max|err| {num['max_err']:.4g} > "
+                             f"{num['bound']:.4g} (2^-7 max|ref| + k 2^-12)")
+        return False
+    return True
+
+
+def harness_times(impl, comm, iters: int):
+    """The reference's default timing (``ddlb/benchmark.py:161-172``): per iteration a device
+    sync + barrier, then perf_counter around run(); synchronize(). MAX over ranks per
+    iteration (``:190-204``); returns the per-iteration ms."""
+    import torch
+
+    times = []
+    for _ in range(iters):
+        comm.barrier()
+        t0 = time.perf_counter()
+        impl.run()
+        comm.synchronize()
+        times.append((time.perf_counter() - t0) * 1e3)
+    t = torch.tensor(times, dtype=torch.float64, device=comm.device)
+    comm.all_reduce_max(t)
+    return [float(x) for x in t.cpu()]
 
 
 def child_main(a) -> int:
@@ -254,6 +277,10 @@ def child_main(a) -> int:
         impl.check_health()
         if a.validate and valid:
             valid = _check(impl, out, res)
+        if a.harness_iters > 0:
+            ht = harness_times(impl, comm, a.harness_iters)
+            res["harness_mean_ms"] = sum(ht) / len(ht)
+            impl.check_health()
         res.update(ok=True, ms=float(t.item()), valid=valid)
         impl.close()
         comm.destroy()
@@ -261,6 +288,25 @@ def child_main(a) -> int:
         res["error"] = f"{type(e).__name__}: {str(e)[:300]}"
     with open(a.child_out, "w") as f:
         json.dump(res, f)
+    return 0
+
+
+def preflight_child(a) -> int:
+    """One preflight family on this rank's GPU (progress file rewritten after every phase)."""
+    from ddlb_amd.communicator import Communicator
+    from ddlb_amd.parallel import preflight
+
+    try:
+        comm = Communicator()
+        comm.ensure_process_group(timeout_s=min(a.child_timeout, 60.0))
+        if a.child_impl == "preflight_rccl":
+            preflight.run_rccl_checks(comm, progress_path=a.child_out)
+        else:
+            preflight.run_ipc_checks(comm, progress_path=a.child_out)
+        comm.destroy()
+    except Exception as e:
+        with open(a.child_out + ".err", "w") as f:
+            f.write(f"{type(e).__name__}: {str(e)[:300]}")
     return 0
 
 
@@ -273,12 +319,23 @@ def _free_port() -> int:
     return p
 
 
+def _gpu_count() -> int:
+    """Visible GPUs, without initialising HIP in this (parent) process."""
+    if os.environ.get("DDLB_DEVICE", "auto") == "cpu":
+        return 0
+    import torch
+
+    return torch.cuda.device_count()
+
+
 class Job:
     def __init__(self, a):
         self.a = a
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
+        self.t_start = time.time()
         self.pg = None
+        self.child_env = {}  # e.g. DDLB_PG_BACKEND=gloo when the RCCL control plane failed
         if self.world > 1:
             import datetime
 
@@ -294,8 +351,12 @@ class Job:
     def log(self, msg: str) -> None:
         """Progress line on rank 0's stderr (the JSON result stays the only stdout line)."""
         if self.rank == 0:
-            sys.stderr.write(f"[bench] {msg}\n")
+            sys.stderr.write(f"[bench {time.time() - self.t_start:5.0f}s] {msg}\n")
             sys.stderr.flush()
+
+    def left(self) -> float:
+        """Seconds left before the job deadline (rank 0's clock; broadcast where it decides)."""
+        return self.a.deadline_s - (time.time() - self.t_start)
 
     def bcast(self, obj):
         if self.pg is None:
@@ -311,114 +372,207 @@ class Job:
         self.pg.all_gather_object(out, obj)
         return out
 
-    def measure(self, impl: str, opts: dict, steps: int, warmup: int, validate: bool,
-                timeout: float, prewarm_ms: float = 0.0) -> dict:
-        """Run one measurement in a child per rank; every rank returns the same dict."""
+    def _spawn(self, mode: str, opts: dict, timeout: float, extra=()):
+        """Run one child per rank; returns (local result path, exit info). The timeout and the
+        rendezvous port come from rank 0 so every rank kills its child at the same point."""
         self.counter += 1
-        port = self.bcast(_free_port() if self.rank == 0 else None)
+        port, timeout = self.bcast((_free_port(), timeout) if self.rank == 0 else None)
         out = os.path.join(self.tmp, f"ddlb_bench_{os.getpid()}_{self.counter}.json")
+        for p in (out, out + ".err"):
+            if os.path.exists(p):
+                os.remove(p)
         env = dict(os.environ)
+        env.update(self.child_env)
         env["DDLB_CHILD_INIT_METHOD"] = f"tcp://127.0.0.1:{port}"
         opts = dict(opts)
         env.update(opts.pop("_env", {}))  # per-candidate runtime settings (e.g. RCCL channels)
         cmd = [sys.executable, os.path.abspath(__file__), "--child", "--child-out", out,
-               "--child-impl", impl, "--child-opts", json.dumps(opts), "--steps", str(steps),
-               "--warmup", str(warmup), "--primitive", self.a.primitive,
-               "-m", str(self.a.m), "-n", str(self.a.n), "-k",
-               str(self.a.k), "--dtype", self.a.dtype, "--child-timeout", str(timeout),
-               "--prewarm-ms", str(prewarm_ms)]
-        if validate:
-            cmd.append("--validate")
+               "--child-impl", mode, "--child-opts", json.dumps(opts),
+               "--primitive", self.a.primitive, "-m", str(self.a.m), "-n", str(self.a.n),
+               "-k", str(self.a.k), "--dtype", self.a.dtype,
+               "--child-timeout", str(max(timeout, 1.0)), *extra]
         proc = subprocess.Popen(cmd, env=env)
+        status = "exit"
         try:
-            proc.wait(timeout=timeout)
-            local = json.load(open(out)) if os.path.exists(out) else {
-                "ok": False, "error": f"child exit {proc.returncode}"}
+            proc.wait(timeout=max(timeout, 1.0))
         except subprocess.TimeoutExpired:
             proc.kill()
             proc.wait()
+            status = "timeout"
+        return out, status, proc.returncode, timeout
+
+    def measure(self, impl: str, opts: dict, steps: int, warmup: int, validate: bool,
+                timeout: float, prewarm_ms: float = 0.0, harness_iters: int = 0) -> dict:
+        """Run one measurement in a child per rank; every rank returns the same dict."""
+        extra = ["--steps", str(steps), "--warmup", str(warmup), "--prewarm-ms",
+                 str(prewarm_ms), "--harness-iters", str(harness_iters)]
+        if validate:
+            extra.append("--validate")
+        out, status, rc, timeout = self._spawn(impl, opts, timeout, extra)
+        if status == "timeout":
             local = {"ok": False, "error": f"timeout after {timeout:.0f}s"}
-        finally:
-            if os.path.exists(out):
-                os.remove(out)
+        elif os.path.exists(out):
+            local = json.load(open(out))
+        else:
+            local = {"ok": False, "error": f"child exit {rc}"}
+        if os.path.exists(out):
+            os.remove(out)
         results = self.gather(local)
         if all(r.get("ok") for r in results):
             ms = max(r["ms"] for r in results)
             valid = all(r.get("valid") is not False for r in results)
             why = [r["validation"] for r in results if r.get("validation")]
-            return {"ok": True, "ms": ms, "valid": valid if validate else None,
-                    "validation": why[0] if why else ""}
+            res = {"ok": True, "ms": ms, "valid": valid if validate else None,
+                   "validation": why[0] if why else ""}
+            errs = [r["max_err"] for r in results if "max_err" in r]
+            if errs:
+                res["max_err"] = max(errs)
+                res["err_bound"] = min(r["err_bound"] for r in results if "err_bound" in r)
+            hm = [r["harness_mean_ms"] for r in results if "harness_mean_ms" in r]
+            if hm:
+                res["harness_mean_ms"] = max(hm)
+            return res
         errs = [r.get("error") for r in results if not r.get("ok")]
         return {"ok": False, "error": errs[0] if errs else "unknown"}
 
+    def preflight(self, timeout: float) -> dict:
+        """Run the preflight families (RCCL, then IPC), each in its own child per rank."""
+        from ddlb_amd.parallel import preflight as pf
 
-def autotune(job, pool, a, world: int, tune: dict):
+        fake = os.environ.get("DDLB_PREFLIGHT_FAKE")
+        if fake:  # tests: scripted results
+            return json.loads(fake)
+        if self.world == 1:
+            return {"skipped": "world 1 (no cross-GPU data plane)"}
+        if _gpu_count() == 0:
+            return {"skipped": "no GPU visible"}
+        merged = {}
+        for mode, phases in (("preflight_rccl", pf.RCCL_PHASES), ("preflight_ipc", pf.IPC_PHASES)):
+            t0 = time.time()
+            env_saved = dict(self.child_env)
+            self.child_env["DDLB_PG_BACKEND"] = "gloo"  # checks independent of torch's RCCL PG
+            out, status, rc, _ = self._spawn(mode, {}, timeout)
+            self.child_env = env_saved
+            local = {}
+            if os.path.exists(out):
+                local = json.load(open(out))
+            if os.path.exists(out + ".err"):
+                local.setdefault("_error", open(out + ".err").read())
+            for p in (out, out + ".err", out + ".tmp"):
+                if os.path.exists(p):
+                    os.remove(p)
+            per_rank = self.gather(local)
+            got = pf.merge(per_rank, phases)
+            errs = [r.get("_error") for r in per_rank if r.get("_error")]
+            if errs:
+                for ph in phases:
+                    if not got[ph].startswith("ok") and got[ph] == "failed: timeout":
+                        got[ph] = f"failed: {errs[0][:160]}"
+            merged.update(got)
+            self.log(f"preflight {mode}: {json.dumps(got)} ({time.time() - t0:.1f} s)")
+        return merged
+
+
+def _blocked(opts_needs, pre: dict):
+    """The first preflight check a candidate needs that did not pass (None = runnable)."""
+    for ch in opts_needs:
+        st = pre.get(ch)
+        if st is not None and not str(st).startswith("ok"):
+            return ch
+    return None
+
+
+def autotune(job, pool, a, world: int, tune: dict, pre: dict = None):
     """Time every candidate (validated) in its own children; returns (winner, fallbacks) or
-    None when every candidate failed. ``tune`` collects per-candidate results for the report."""
-    t_tune = time.time()
+    None when every candidate failed. ``tune`` collects per-candidate results for the report.
+    Candidates needing a failed preflight check are skipped; a family whose candidates time out
+    twice is skipped for the rest of the search (a hang costs the whole candidate timeout)."""
+    from ddlb_amd.parallel.preflight import needs
+
+    pre = pre or {}
     rounds = a.tune_rounds if a.tune_rounds > 0 else (2 if world == 1 else 1)
     tune_steps = a.tune_steps if a.tune_steps > 0 else (50 if world == 1 else 20)
+    natives = [c for c in pool if c[1] == "native"]
+    vendors = [c for c in pool if c[1] != "native"]
+    order = natives * rounds + vendors  # the vendor slots once: they only feed vendor_ms
     best_ms = {}
-    # several rounds over the pool in the same order, best time per candidate: a candidate
-    # measured first after an idle gap otherwise pays the clock ramp the others do not
-    for label, impl, opts in pool * rounds:
-        # wall-clock cap on the search (the decision is broadcast from rank 0, so every
-        # rank stops at the same candidate): the best candidate so far runs the final
-        native_ok = any(lb in best_ms for lb, i, _ in pool if i == "native")
+    timeouts = {}
+    t_tune = time.time()
+    for label, impl, opts in order:
+        req = needs(impl, opts)
+        why = _blocked(req, pre)
+        if why is None:
+            hung = [ch for ch in req if timeouts.get(ch, 0) >= 2]
+            why = f"{hung[0]} candidates timed out twice" if hung else None
+        if why is not None:
+            tune.setdefault(label, f"skipped ({why})")
+            continue
+        # the search stops where the final run would no longer fit before the deadline (the
+        # decision is rank 0's, broadcast, so every rank stops at the same candidate)
+        native_ok = any(lb in best_ms for lb, _, _ in natives)
         spent = time.time() - t_tune
-        over = (native_ok and spent > a.tune_budget_s) or (best_ms and spent > a.tune_cap_s)
+        room = job.left() - a.final_reserve_s
+        over = (room < 10.0 or (native_ok and spent > a.tune_budget_s)
+                or (best_ms and spent > a.tune_cap_s))
         if job.bcast(over if job.rank == 0 else None):
-            tune.setdefault(label, "skipped (tuning budget)")
+            tune.setdefault(label, "skipped (deadline / tuning budget)")
             continue
         t0 = time.time()
         # tuning runs validate too (first run and last timed step): a fast candidate that
         # computes the wrong numbers must never win the search
-        r = job.measure(impl, opts, tune_steps, 3, a.validate, a.candidate_timeout,
+        r = job.measure(impl, opts, tune_steps, 3, a.validate,
+                        min(a.candidate_timeout, max(room, 10.0)),
                         prewarm_ms=min(a.prewarm_ms, 100.0))
         if r["ok"] and r.get("valid") is False:
             r = {"ok": False, "error": f"invalid result: {r.get('validation', '')}"}
         if r["ok"]:
             best_ms[label] = min(r["ms"], best_ms.get(label, float("inf")))
             tune[label] = round(best_ms[label], 4)
-        elif label not in best_ms:
-            tune[label] = r["error"][:160]
+        else:
+            if r["error"].startswith("timeout"):
+                for ch in req:
+                    timeouts[ch] = timeouts.get(ch, 0) + 1
+            if label not in best_ms:
+                tune[label] = r["error"][:160]
         job.log(f"tune {label}: {round(r['ms'], 4) if r['ok'] else r['error'][:160]} "
                 f"({time.time() - t0:.1f} s)")
-    ranked = [(best_ms[label], (label, impl, opts)) for label, impl, opts in pool
-              if impl == "native" and label in best_ms]
+    ranked = sorted(((best_ms[lb], (lb, i, o)) for lb, i, o in natives if lb in best_ms),
+                    key=lambda x: x[0])
+    vend = sorted(((best_ms[lb], (lb, i, o)) for lb, i, o in vendors if lb in best_ms),
+                  key=lambda x: x[0])
     if not ranked:
-        # every native path failed on this machine: report the vendor-library slot (our
-        # pytorch implementation, RCCL + hipBLASLt) rather than no number; the result line
-        # names the implementation
-        ranked = [(best_ms[label], (label, impl, opts)) for label, impl, opts in pool
-                  if label in best_ms]
+        # every native path failed on this machine: report the vendor-library slot rather than
+        # no number; the result line names the implementation and the library
+        ranked = vend
         tune["native_failed"] = True
     if not ranked:
         return None
-    ranked.sort(key=lambda x: x[0])
     chosen = ranked[0][1]
     fallbacks = [c for _, c in ranked[1:4]]
     # last resort: the vendor-library slot, so a job whose native paths all break in the
     # final run still reports a measured (and labelled) number
-    vendor = sorted(((best_ms[lbl], (lbl, i, o)) for lbl, i, o in pool
-                     if i != "native" and lbl in best_ms), key=lambda x: x[0])
-    if vendor and vendor[0][1] not in fallbacks and vendor[0][1] is not chosen:
-        fallbacks.append(vendor[0][1])
+    if vend and vend[0][1] not in fallbacks and vend[0][1] is not chosen:
+        fallbacks.append(vend[0][1])
     return chosen, fallbacks
 
 
 def final_measure(job, chosen, fallbacks, a, tune: dict):
     """The timed measurement of the contract. Should the winner fail or not validate there (a
     flaky transport, a cross-rank ordering bug under back-to-back epochs), the next fastest
-    candidates are tried before giving up, so one bad path cannot sink the job. Returns
-    (candidate, result); result is None if nothing ran, or has valid=False if nothing
+    candidates are tried while the deadline leaves room, so one bad path cannot sink the job.
+    Returns (candidate, result); result is None if nothing ran, or has valid=False if nothing
     validated (then the first completed run is reported, with a nonzero exit code)."""
-    final, invalid = None, None
+    invalid = None
     first = chosen
-    for cand in [chosen] + list(fallbacks):
+    for idx, cand in enumerate([chosen] + list(fallbacks)):
+        room = job.left() - 5.0
+        if job.bcast(room < 15.0 if job.rank == 0 else None):
+            tune.setdefault("final_rejected", []).append(f"{cand[0]}: no time left (deadline)")
+            break
         t0 = time.time()
-        r = job.measure(cand[1], cand[2], a.steps, a.warmup, a.validate,
-                        a.candidate_timeout + a.steps * 0.05, prewarm_ms=a.prewarm_ms)
+        timeout = min(a.candidate_timeout + a.steps * 0.05 + a.harness_iters * 0.05, room)
+        r = job.measure(cand[1], cand[2], a.steps, a.warmup, a.validate, timeout,
+                        prewarm_ms=a.prewarm_ms, harness_iters=a.harness_iters)
         job.log(f"final {cand[0]}: {r.get('ms', r.get('error'))} valid={r.get('valid')} "
                 f"({time.time() - t0:.1f} s)")
         if r["ok"] and r.get("valid") is not False:
@@ -431,7 +585,7 @@ def final_measure(job, chosen, fallbacks, a, tune: dict):
             f"{cand[0]}: {r.get('error') or 'invalid ' + r.get('validation', '')}"[:200])
     if invalid is not None:
         return invalid
-    return chosen, final
+    return chosen, None
 
 
 def main(argv=None) -> int:
@@ -453,18 +607,30 @@ def main(argv=None) -> int:
     p.add_argument("--tune-steps", type=int, default=0,
                    help="timed steps per autotune measurement (0 = 50 at world 1, 20 otherwise)")
     p.add_argument("--tune-rounds", type=int, default=0,
-                   help="passes over the candidate pool (0 = 2 at world 1, 1 otherwise)")
-    p.add_argument("--candidate-timeout", type=float, default=60.0,
+                   help="passes over the native pool (0 = 2 at world 1, 1 otherwise)")
+    p.add_argument("--candidate-timeout", type=float, default=45.0,
                    help="per-candidate child timeout (a healthy candidate takes ~3-15 s)")
+    p.add_argument("--deadline-s", type=float, default=480.0,
+                   help="wall-clock deadline of the WHOLE job (preflight, tuning, final run and "
+                        "fallbacks): the driver allows 600 s")
+    p.add_argument("--final-reserve-s", type=float, default=100.0,
+                   help="time kept free of tuning for the final run and its fallbacks")
+    p.add_argument("--preflight-timeout", type=float, default=40.0,
+                   help="per-family timeout of the N>1 preflight children")
     p.add_argument("--tune-budget-s", type=float, default=300.0,
                    help="stop trying further candidates after this much autotuning wall time "
-                        "(once a native candidate has succeeded); sized so the whole job, "
-                        "final run and fallbacks included, stays well inside 10 minutes")
-    p.add_argument("--tune-cap-s", type=float, default=420.0,
+                        "(once a native candidate has succeeded)")
+    p.add_argument("--tune-cap-s", type=float, default=360.0,
                    help="hard cap on autotuning wall time (once any candidate has succeeded)")
     p.add_argument("--no-validate", dest="validate", action="store_false", default=True)
     p.add_argument("--prewarm-ms", type=float, default=300.0,
                    help="untimed GPU pre-warm before the warmup steps (clock ramp)")
+    p.add_argument("--preflight-only", action="store_true",
+                   help="run the N>1 data-plane preflight, print its JSON line and exit")
+    p.add_argument("--harness-iters", type=int, default=-1,
+                   help="iterations of the reference-default timing (barrier before each, "
+                        "MAX over ranks) after the timed window -> harness_mean_ms "
+                        "(-1 = --steps, 0 = off)")
     # child-mode arguments (internal)
     p.add_argument("--child", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--child-out", help=argparse.SUPPRESS)
@@ -473,7 +639,11 @@ def main(argv=None) -> int:
     p.add_argument("--child-timeout", type=float, default=600.0, help=argparse.SUPPRESS)
     p.add_argument("--validate", dest="validate", action="store_true", help=argparse.SUPPRESS)
     a = p.parse_args(argv)
+    if a.harness_iters < 0:
+        a.harness_iters = a.steps
     if a.child:
+        if a.child_impl.startswith("preflight_"):
+            return preflight_child(a)
         return child_main(a)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -490,6 +660,17 @@ def main(argv=None) -> int:
         if unknown:
             raise SystemExit(f"unknown candidates {unknown}")
         pool = [c for c in every if c[0] in want]
+    pre = job.preflight(min(a.preflight_timeout, max(job.left() / 4, 10.0)))
+    if a.preflight_only:
+        if job.rank == 0:
+            print(json.dumps({"preflight": pre, "n_gpus": world}), flush=True)
+        if job.pg is not None:
+            job.pg.destroy_process_group()
+        return 0 if all(str(v).startswith("ok") for v in pre.values()) else 1
+    if not str(pre.get("torch_nccl", "ok")).startswith("ok"):
+        # torch's RCCL group is broken on this node: the children coordinate over gloo (the
+        # control plane: barriers, the MAX over ranks), our native data plane is unaffected
+        job.child_env["DDLB_PG_BACKEND"] = "gloo"
     fallbacks = []
     if a.algorithm != "auto":
         match = [c for c in every if c[0] == a.algorithm]
@@ -498,7 +679,7 @@ def main(argv=None) -> int:
                              f"{[c[0] for c in every]}")
         chosen = match[0]
     else:
-        picked = autotune(job, pool, a, world, tune)
+        picked = autotune(job, pool, a, world, tune, pre)
         if picked is None:
             sys.stderr.write(f"every candidate failed: {json.dumps(tune)}\n")
             return 1
@@ -515,9 +696,12 @@ def main(argv=None) -> int:
     # N-slice (weak scaling, N x the harness number); tp_rowwise = the ranks share one
     # [m,k]x[k,n] split along K (strong scaling, the harness number IS the aggregate)
     value = harness_tflops * world if col else harness_tflops
+    vendor = {lbl: tune[lbl] for lbl, impl, _ in pool
+              if impl != "native" and isinstance(tune.get(lbl), float)}
     if job.rank == 0:
         dt = {"bfloat16": "bf16", "float16": "fp16", "float32": "fp32",
               "float8_e4m3fn": "fp8_e4m3"}.get(a.dtype, a.dtype)
+        native = chosen[1] == "native"
         line = {
             "metric": (f"tp_columnwise AG+GEMM effective TFLOP/s (whole job, m={a.m} {dt})" if col
                        else f"tp_rowwise GEMM+RS effective TFLOP/s (whole job, m={a.m} {dt})"),
@@ -531,9 +715,17 @@ def main(argv=None) -> int:
                        "implementation": chosen[1], "algorithm": chosen[0]},
             "per_gpu_tflops": round(harness_tflops if col else harness_tflops / world, 6),
             "harness_tflops": round(harness_tflops, 6), "valid": final.get("valid"),
-            "gemm": ("hipblaslt" if chosen[1] == "pytorch" or chosen[2].get("gemm_mode") == "blas"
-                     else "ddlb_amd MFMA"),
+            "gemm": "ddlb_amd MFMA" if native else "hipblaslt (vendor slot: every native failed)",
+            "timing": TIMING,
+            "harness_mean_ms": (round(final["harness_mean_ms"], 5)
+                                if "harness_mean_ms" in final else None),
+            "harness_timing": "reference default: cpu_clock, barrier before every iteration, "
+                              "MAX over ranks per iteration (ddlb/benchmark.py:161-172)",
+            "max_err": final.get("max_err"), "err_bound": final.get("err_bound"),
+            "vendor_ms": vendor,
+            "preflight": pre,
             "prewarm_ms": a.prewarm_ms,
+            "deadline_s": a.deadline_s, "job_wall_s": round(time.time() - job.t_start, 1),
             "autotune_ms": tune,
         }
         print(json.dumps(line), flush=True)

@@ -31,7 +31,7 @@ void check(hipError_t e, const char* what) {
 }
 
 struct DLCtx {
-  std::shared_ptr<SymmetricBuffer> owner;
+  std::shared_ptr<void> owner;  // keeps the allocation (symmetric buffer / RCCL memory) alive
   int64_t shape[1];
 };
 
@@ -47,10 +47,10 @@ void capsule_destructor(PyObject* cap) {
   }
 }
 
-py::object buffer_dlpack(std::shared_ptr<SymmetricBuffer> buf, int device) {
-  auto* ctx = new DLCtx{buf, {(int64_t)buf->bytes()}};
+py::object raw_dlpack(std::shared_ptr<void> owner, uintptr_t ptr, size_t bytes, int device) {
+  auto* ctx = new DLCtx{std::move(owner), {(int64_t)bytes}};
   auto* t = new DLManagedTensor();
-  t->dl_tensor.data = (void*)buf->local();
+  t->dl_tensor.data = (void*)ptr;
   t->dl_tensor.device = DLDevice{kDLROCM, device};
   t->dl_tensor.ndim = 1;
   t->dl_tensor.dtype = DLDataType{kDLUInt, 8, 1};
@@ -60,6 +60,10 @@ py::object buffer_dlpack(std::shared_ptr<SymmetricBuffer> buf, int device) {
   t->manager_ctx = ctx;
   t->deleter = dl_deleter;
   return py::reinterpret_steal<py::object>(PyCapsule_New(t, "dltensor", capsule_destructor));
+}
+
+py::object buffer_dlpack(std::shared_ptr<SymmetricBuffer> buf, int device) {
+  return raw_dlpack(buf, buf->local(), buf->bytes(), device);
 }
 
 GemmArgs make_args(uintptr_t a, uintptr_t b, uintptr_t c, int64_t lda, int64_t ldb, int64_t ldc,
@@ -138,6 +142,20 @@ PYBIND11_MODULE(_C, m) {
           }
           check(copy_launch(a, max_blocks, (hipStream_t)s), "copy_multi");
         });
+  m.def("copy_batch_api_available", &copy_batch_api_available);
+  m.def("copy_batch",  // copy-engine copies (dst, src, bytes) submitted as one batch
+        [](std::vector<std::tuple<uintptr_t, uintptr_t, int64_t>> segs, uintptr_t s) {
+          std::vector<void*> d, sr;
+          std::vector<size_t> b;
+          for (auto& t : segs) {
+            d.push_back((void*)std::get<0>(t));
+            sr.push_back((void*)std::get<1>(t));
+            b.push_back((size_t)std::get<2>(t));
+          }
+          if (d.empty()) return;
+          check(copy_batch(d.data(), sr.data(), b.data(), d.size(), (hipStream_t)s), "copy_batch");
+        });
+  m.def("install_crash_handler", &install_crash_handler);
   m.def("device_synchronize", []() { check(hipDeviceSynchronize(), "hipDeviceSynchronize"); });
   m.def("get_last_error", []() { return std::string(hipGetErrorString(hipGetLastError())); });
 
@@ -151,6 +169,17 @@ PYBIND11_MODULE(_C, m) {
       .def("async_error", &RcclComm::async_error)
       .def_property_readonly("rank", &RcclComm::rank)
       .def_property_readonly("nranks", &RcclComm::nranks);
+
+  py::class_<RcclMem, std::shared_ptr<RcclMem>>(m, "RcclMem")
+      .def(py::init<std::shared_ptr<RcclComm>, size_t, int>(), py::arg("comm"), py::arg("bytes"),
+           py::arg("device"))
+      .def("release", &RcclMem::release)
+      .def("local", &RcclMem::local)
+      .def_property_readonly("registered", &RcclMem::registered)
+      .def_property_readonly("bytes", &RcclMem::bytes);
+  m.def("rccl_mem_dlpack", [](std::shared_ptr<RcclMem> b, int device) {
+    return raw_dlpack(b, b->local(), b->bytes(), device);
+  });
 
   py::class_<SymmetricBuffer, std::shared_ptr<SymmetricBuffer>>(m, "SymmetricBuffer")
       .def(py::init<size_t, int, bool>(), py::arg("bytes"), py::arg("device"),
@@ -174,7 +203,6 @@ PYBIND11_MODULE(_C, m) {
   py::class_<PlanExecutor, std::shared_ptr<PlanExecutor>>(m, "PlanExecutor")
       .def(py::init<int, int, int, const std::vector<int>&>())
       .def("load", &PlanExecutor::load)
-      .def("prepare", &PlanExecutor::prepare)
       .def("set_comm", [](PlanExecutor& p, std::shared_ptr<RcclComm> c) { p.set_comm(c.get()); },
            py::keep_alive<1, 2>())
       .def("run", &PlanExecutor::run)
@@ -188,5 +216,8 @@ PYBIND11_MODULE(_C, m) {
       .def("graph_capturable", &PlanExecutor::graph_capturable)
       .def("set_timeline", &PlanExecutor::set_timeline)
       .def("timeline", &PlanExecutor::timeline)
-      .def("host_times", &PlanExecutor::host_times);
+      .def("host_times", &PlanExecutor::host_times)
+      .def("set_cu_split", &PlanExecutor::set_cu_split)
+      .def("cu_split", &PlanExecutor::cu_split)
+      .def("set_trace", &PlanExecutor::set_trace);
 }

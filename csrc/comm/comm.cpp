@@ -57,6 +57,39 @@ ncclDataType_t nccl_dtype(int dt) {
   }
 }
 
+RcclMem::RcclMem(std::shared_ptr<RcclComm> comm, size_t bytes, int device)
+    : comm_(std::move(comm)), bytes_(bytes ? bytes : 256), device_(device) {
+  if (!comm_ || comm_->get() == nullptr) throw std::runtime_error("RcclMem: no communicator");
+  DDLB_HIP(hipSetDevice(device));
+  DDLB_NCCL(ncclMemAlloc(&ptr_, bytes_));
+  DDLB_HIP(hipMemset(ptr_, 0, bytes_));
+  DDLB_HIP(hipDeviceSynchronize());
+  const ncclResult_t r = ncclCommRegister(comm_->get(), ptr_, bytes_, &handle_);
+  if (r != ncclSuccess) {
+    ncclMemFree(ptr_);
+    ptr_ = nullptr;
+    throw std::runtime_error(std::string("ncclCommRegister: ") + ncclGetErrorString(r));
+  }
+}
+
+RcclMem::~RcclMem() {
+  try {
+    release();
+  } catch (...) {
+  }
+}
+
+void RcclMem::release() {
+  if (ptr_ == nullptr) return;
+  hipSetDevice(device_);
+  hipDeviceSynchronize();
+  if (handle_ != nullptr && comm_ && comm_->get() != nullptr)
+    ncclCommDeregister(comm_->get(), handle_);
+  handle_ = nullptr;
+  ncclMemFree(ptr_);
+  ptr_ = nullptr;
+}
+
 SymmetricBuffer::SymmetricBuffer(size_t bytes, int device, bool uncached)
     : bytes_(bytes), device_(device), uncached_(uncached) {
   DDLB_HIP(hipSetDevice(device));

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -45,6 +46,26 @@ class RcclComm {
 };
 
 ncclDataType_t nccl_dtype(int dt);  // DT_* -> ncclDataType_t
+
+// A buffer RCCL may use zero-copy: allocated with ncclMemAlloc and registered with the
+// communicator (ncclCommRegister), the analogue of nvFuser's symmetric-memory allocations
+// (reference TPColumnwise/fuser.py:44-45). Deregistered and freed before the communicator goes.
+class RcclMem {
+ public:
+  RcclMem(std::shared_ptr<RcclComm> comm, size_t bytes, int device);
+  ~RcclMem();
+  void release();
+  uintptr_t local() const { return (uintptr_t)ptr_; }
+  size_t bytes() const { return bytes_; }
+  bool registered() const { return handle_ != nullptr; }
+
+ private:
+  std::shared_ptr<RcclComm> comm_;
+  void* ptr_ = nullptr;
+  void* handle_ = nullptr;
+  size_t bytes_ = 0;
+  int device_ = 0;
+};
 
 // One symmetric allocation: a hipMalloc'd buffer on this device + the IPC-mapped pointers of the
 // same-named buffer on every peer (index = rank; own rank -> local pointer).

@@ -28,8 +28,9 @@ enum Tile : int { TILE_AUTO = 0, TILE_256x256 = 1, TILE_256x128 = 2, TILE_128x25
                   TILE_PT8 = 17,      // PT8: persistent T8 (tiles streamed, C stores spread)
                   TILE_T4 = 18,       // T4: 2-phase ping-pong (32 MFMAs per section)
                   TILE_PT4 = 19 };    // PT4: persistent T4
-enum GemmMode : int { GEMM_MODE_AUTO = 0, GEMM_MODE_GENERIC = 1, GEMM_MODE_MX = 2,
-                      GEMM_MODE_BLAS = 3 };  // BLAS: hipBLASLt for plain GEMMs (blaslt.cpp)
+// Every mode runs one of this file's hand-written kernels: vendor libraries (hipBLASLt through
+// torch.matmul) are only the comparison baseline of the `pytorch` slot, never behind `native`.
+enum GemmMode : int { GEMM_MODE_AUTO = 0, GEMM_MODE_GENERIC = 1, GEMM_MODE_MX = 2 };
 
 // C[M,N] = A[M,K] * Bt[N,K]^T. Leading dimensions in ELEMENTS.
 // Logical row i of A (and of C) lives at physical row (i / grp) * gstride + (i % grp).
@@ -93,11 +94,5 @@ bool gemm_fast_path_ok(const GemmArgs& p, int din, int dout);
 int choose_tile(int64_t M, int64_t N, int64_t K, int din);
 int tile_rows(int tile);
 int tile_cols(int tile);
-// hipBLASLt backend (csrc/gemm/blaslt.cpp): plain bf16, f16, f32 GEMMs (algorithm autotuned).
-bool blaslt_supports(const GemmArgs& p, int din, int dout);
-hipError_t blaslt_gemm(const GemmArgs& p, int din, int dout, hipStream_t s);
-// Build (and autotune, with a host wait) the plan of p's shape ahead of time, e.g. when a
-// native plan is bound, so no tuning happens while a run is being enqueued.
-hipError_t blaslt_prepare(const GemmArgs& p, int din, int dout, hipStream_t s);
 
 }  // namespace ddlb

@@ -2271,10 +2271,12 @@ template <class Mma, int OUT>
 hipError_t launch_pt4(const GemmArgs& p, hipStream_t s) {
   const int tiles = (p.M / 256) * (p.N / 256);
   int grid = num_cus();
-  // Flag-gated: leave reserve_cus CUs free. A pt4 workgroup takes a CU's whole register file, so
-  // with every CU holding a (spinning) tile, the copy / signal kernels that set the flags could
-  // not be scheduled; the reserve keeps the gate deadlock-free whoever moves the data.
-  if (p.flags != nullptr && p.reserve_cus > 0) grid -= p.reserve_cus;
+  // Leave reserve_cus CUs free. A pt4 workgroup takes a CU's whole register file, so with every
+  // CU holding a (spinning) tile, the copy / signal kernels that set a flag-gated GEMM's flags
+  // could not be scheduled; the reserve keeps the gate deadlock-free whoever moves the data.
+  // Without flags it sizes the persistent grid to a CU-masked compute stream (plans with a CU
+  // split: the complement of the communication's CUs), so no workgroup waits for a free CU.
+  if (p.reserve_cus > 0 && p.reserve_cus < grid) grid -= p.reserve_cus;
   GemmArgs q = p;
   q.ag_ctas = p.flags != nullptr && p.ag_ctas > 0 ? (p.ag_ctas + 7) / 8 * 8 : 0;
   // The GEMM takes ceil(tiles / gemm_ctas) rounds of tiles; every copy workgroup that leaves that

@@ -88,7 +88,7 @@ hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mo
   if (p.a_table != nullptr) {
     // direct-access A: only the tiled and ring kernels read A through the shard table
     if (p.shard_rows <= 0 || p.flags != nullptr) return hipErrorInvalidValue;
-    if (mode == GEMM_MODE_BLAS || mode == GEMM_MODE_MX) mode = GEMM_MODE_AUTO;
+    if (mode == GEMM_MODE_MX) mode = GEMM_MODE_AUTO;
     if (tile == TILE_PP256 || tile == TILE_P256 || tile == TILE_PI256 || tile == TILE_PI256W4)
       tile = TILE_I256;
     if (tile == TILE_P128) tile = TILE_I128;
@@ -104,12 +104,11 @@ hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mo
     if (mode == GEMM_MODE_GENERIC || !gemm_fast_path_ok(p, din, dout)) return hipErrorNotSupported;
   }
   if (p.c_table != nullptr) {
-    // direct-store C: every fast kernel addresses C rows through c_row(); hipBLASLt and the
-    // generic kernel cannot, and an interleaved shard order needs whole tiles per shard
+    // direct-store C: every fast kernel addresses C rows through c_row(); the generic kernel
+    // cannot, and an interleaved shard order needs whole tiles per shard
     if (p.c_shard_rows <= 0 || p.c_grp != p.M || mode == GEMM_MODE_GENERIC ||
         p.flags != nullptr || p.ag_ctas > 0 || !gemm_fast_path_ok(p, din, dout))
       return hipErrorNotSupported;
-    if (mode == GEMM_MODE_BLAS) mode = GEMM_MODE_AUTO;
   }
   if (p.tile_order == 2 && (p.nshards <= 0 || p.M % p.nshards != 0))
     return hipErrorInvalidValue;
@@ -123,16 +122,11 @@ hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mo
         p.nsub < 1 || p.nshards % p.nsub || p.nshards / p.nsub > 32 || p.ag_parts < 1 ||
         p.ag_tab == nullptr || p.flag_rows * p.lda * esz / p.ag_parts >= (int64_t(1) << 30))
       return hipErrorNotSupported;  // (a copy unit is addressed by one 32-bit buffer descriptor)
-    if (mode == GEMM_MODE_BLAS) mode = GEMM_MODE_AUTO;
     tile = TILE_PT4;
   } else if (p.ag_mode != 0) {
     return hipErrorNotSupported;  // agent-scope gate acquire only for flags this launch sets
   }
-  if (mode == GEMM_MODE_BLAS) {
-    const hipError_t e = blaslt_gemm(p, din, dout, s);
-    if (e != hipErrorNotSupported) return e;
-    mode = GEMM_MODE_AUTO;  // fused / fp8 / ragged-group GEMMs stay on the MFMA kernels
-  }
+  if (mode < GEMM_MODE_AUTO || mode > GEMM_MODE_MX) return hipErrorInvalidValue;
   const bool fast = mode != GEMM_MODE_GENERIC && gemm_fast_path_ok(p, din, dout);
   if (p.tile_order && !fast) p.tile_order = 0;
   if (fast) {

@@ -1,14 +1,104 @@
 // Plan executor implementation (see plan.h).
 #include "plan.h"
 
+#include <dlfcn.h>
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include <chrono>
 #include <cstdlib>
+#include <cstring>
 #include <stdexcept>
 
 #include "../gemm/gemm.h"
 #include "kernels.h"
 
 namespace ddlb {
+
+namespace {
+
+// roctx, resolved lazily from the library the Python side (ddlb_amd.utils.profiling) or the
+// profiler already mapped, else loaded here: no link-time dependency on the tracer.
+struct Roctx {
+  int (*push)(const char*) = nullptr;
+  int (*pop)() = nullptr;
+};
+const Roctx& roctx() {
+  static Roctx r = [] {
+    Roctx x;
+    const char* names[] = {"librocprofiler-sdk-roctx.so.1", "librocprofiler-sdk-roctx.so",
+                           "/opt/rocm/lib/librocprofiler-sdk-roctx.so.1", "libroctx64.so.4"};
+    for (const char* n : names) {
+      void* h = dlopen(n, RTLD_NOW | RTLD_GLOBAL | RTLD_NOLOAD);
+      if (!h) h = dlopen(n, RTLD_NOW | RTLD_GLOBAL);
+      if (!h) continue;
+      x.push = (int (*)(const char*))dlsym(h, "roctxRangePushA");
+      x.pop = (int (*)())dlsym(h, "roctxRangePop");
+      if (x.push && x.pop) break;
+      x.push = nullptr;
+      x.pop = nullptr;
+    }
+    return x;
+  }();
+  return r;
+}
+
+using BatchFn = hipError_t (*)(void**, void**, size_t*, size_t, hipMemcpyAttributes*, size_t*,
+                               size_t, size_t*, hipStream_t);
+BatchFn batch_fn() {
+  static BatchFn f = [] {
+    // look the symbol up in the HIP runtime this module is bound to (torch's copy)
+    Dl_info info;
+    BatchFn fn = nullptr;
+    if (dladdr((void*)&hipMemcpyAsync, &info) && info.dli_fname) {
+      void* h = dlopen(info.dli_fname, RTLD_NOW | RTLD_NOLOAD);
+      if (h) fn = (BatchFn)dlsym(h, "hipMemcpyBatchAsync");
+    }
+    if (!fn) fn = (BatchFn)dlsym(RTLD_DEFAULT, "hipMemcpyBatchAsync");
+    return fn;
+  }();
+  return f;
+}
+
+void crash_handler(int sig) {
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  static const char msg[] = "ddlb_amd: fatal signal, native backtrace follows\n";
+  ssize_t w = write(2, msg, sizeof(msg) - 1);
+  (void)w;
+  backtrace_symbols_fd(frames, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
+}  // namespace
+
+bool copy_batch_api_available() { return batch_fn() != nullptr; }
+
+hipError_t copy_batch(void** dst, void** src, size_t* bytes, size_t n, hipStream_t s) {
+  static bool api_ok = true;  // off after the first refusal (the header marks attrs unsupported)
+  if (BatchFn fn = batch_fn(); fn && api_ok) {
+    size_t fail = 0;
+    const hipError_t e = fn(dst, src, bytes, n, nullptr, nullptr, 0, &fail, s);
+    if (e == hipSuccess) return e;
+    (void)hipGetLastError();
+    api_ok = false;
+  }
+  for (size_t i = 0; i < n; ++i) {
+    const hipError_t e = hipMemcpyAsync(dst[i], src[i], bytes[i], hipMemcpyDeviceToDevice, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+void install_crash_handler() {
+  struct sigaction sa;
+  std::memset(&sa, 0, sizeof(sa));
+  sa.sa_handler = crash_handler;
+  sa.sa_flags = SA_RESETHAND;
+  for (int sig : {SIGSEGV, SIGBUS, SIGABRT, SIGFPE}) sigaction(sig, &sa, nullptr);
+}
 
 PlanExecutor::PlanExecutor(int device, int nstreams, int nevents,
                            const std::vector<int>& priorities)
@@ -44,6 +134,12 @@ PlanExecutor::~PlanExecutor() {
   if (graph_exec_) hipGraphExecDestroy(graph_exec_);
   if (graph_) hipGraphDestroy(graph_);
   if (cap_stream_) hipStreamDestroy(cap_stream_);
+  if (compute_) {
+    hipStreamSynchronize(compute_);
+    hipStreamDestroy(compute_);
+  }
+  if (compute_fork_) hipEventDestroy(compute_fork_);
+  if (compute_join_) hipEventDestroy(compute_join_);
   for (size_t i = 1; i < streams_.size(); ++i)
     if (streams_[i]) {
       hipStreamSynchronize(streams_[i]);
@@ -82,16 +178,25 @@ void PlanExecutor::load(const std::vector<int64_t>& ops) {
 }
 
 bool PlanExecutor::graph_capturable() const {
-  // In graph mode the epoch-dependent ops (cross-process signals / waits, arrival-flag GEMMs)
-  // read the run counter from device memory (d_epoch_, bumped by the first node of every
-  // replay) instead of a value baked in at enqueue time, so they capture. RCCL calls do not:
-  // replaying a captured RCCL collective crashed the process on this image (torch's RCCL 2.26,
-  // profiles/r02/r2_19*); RCCL plans issue few calls per run anyway.
+  // In graph mode the epoch-dependent ops (cross-process signals / waits, the in-kernel
+  // all-gather's flags) read the run counter from device memory (d_epoch_, bumped by the first
+  // node of every replay) instead of a value baked in at enqueue time, so they capture. Not
+  // captured:
+  //  * RCCL calls: replaying a captured RCCL collective crashed the process on this image
+  //    (torch's RCCL 2.26, profiles/r02/r2_19*); RCCL plans issue few calls per run anyway.
+  //  * a flag-gated GEMM whose flags other streams set (the fused copy-engine pipelines): the
+  //    graph may place it ahead of the copy / signal nodes in one hardware queue, and its
+  //    spinning tiles would then wait for nodes queued behind them; ordering it after every
+  //    copy stream instead serialises copy-then-GEMM and removes the overlap it exists for
+  //    (ADVICE r2). Such plans run eagerly, where the enqueue order puts the copies first.
+  //  * a CU split (set_cu_split): masked streams are not carried into graph nodes.
+  if (comm_cus_ > 0) return false;
   for (size_t i = 0; i < ops_.size(); i += kOpWords) {
     const int64_t k = ops_[i];
     if (k == OP_ALLGATHER || k == OP_REDUCE_SCATTER || k == OP_SEND || k == OP_RECV ||
         k == OP_GROUP_START || k == OP_GROUP_END)
       return false;
+    if (k == OP_GEMM && ops_[i + 19] != 0 && ops_[i + 29] == 0) return false;
   }
   return true;
 }
@@ -99,8 +204,9 @@ bool PlanExecutor::graph_capturable() const {
 void PlanExecutor::enable_graph(bool on) {
   if (on && timeline_on_) throw std::runtime_error("hipGraph replay: turn the plan timeline off");
   if (on && !graph_capturable())
-    throw std::runtime_error("hipGraph replay: plans with RCCL calls are not captured (see "
-                             "graph_capturable)");
+    throw std::runtime_error("hipGraph replay: plans with RCCL calls, copy-engine-fed "
+                             "flag-gated GEMMs or a CU split are not captured (see "
+                             "PlanExecutor::graph_capturable)");
   if (on) {  // the device run counter continues from the host one (see graph_capturable)
     DDLB_HIP(hipSetDevice(device_));
     DDLB_HIP(hipDeviceSynchronize());
@@ -109,8 +215,39 @@ void PlanExecutor::enable_graph(bool on) {
   graph_on_ = on;
   if (on && cap_stream_ == nullptr) {
     DDLB_HIP(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking));
-    prepare((uintptr_t)cap_stream_);  // hipBLASLt workspaces exist before the capture
   }
+}
+
+void PlanExecutor::set_cu_split(int comm_cus) {
+  if (comm_cus == comm_cus_) return;
+  if (graph_on_) throw std::runtime_error("CU split: not with hipGraph replay");
+  if (comm_cus_ != 0) throw std::runtime_error("CU split: set once per executor");
+  DDLB_HIP(hipSetDevice(device_));
+  int ncu = 0;
+  DDLB_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device_));
+  if (comm_cus < 0 || comm_cus >= ncu)
+    throw std::runtime_error("CU split: comm_cus must be in [0, " + std::to_string(ncu) + ")");
+  DDLB_HIP(hipDeviceSynchronize());
+  // mask bit i = CU i (the driver spreads consecutive bits over the XCDs / shader engines)
+  const int words = (ncu + 31) / 32;
+  std::vector<uint32_t> comm((size_t)words, 0u), comp((size_t)words, 0u);
+  for (int i = 0; i < ncu; ++i) (i < comm_cus ? comm : comp)[(size_t)(i / 32)] |= 1u << (i % 32);
+  for (size_t i = 1; i < streams_.size(); ++i) {
+    if (streams_[i]) DDLB_HIP(hipStreamDestroy(streams_[i]));
+    streams_[i] = nullptr;
+    DDLB_HIP(hipExtStreamCreateWithCUMask(&streams_[i], (uint32_t)words, comm.data()));
+  }
+  DDLB_HIP(hipExtStreamCreateWithCUMask(&compute_, (uint32_t)words, comp.data()));
+  DDLB_HIP(hipEventCreateWithFlags(&compute_fork_, hipEventDisableTiming));
+  DDLB_HIP(hipEventCreateWithFlags(&compute_join_, hipEventDisableTiming));
+  comm_cus_ = comm_cus;
+}
+
+void PlanExecutor::set_trace(bool on, const std::vector<std::string>& labels) {
+  if (on && (roctx().push == nullptr))
+    throw std::runtime_error("plan trace: no roctx library (librocprofiler-sdk-roctx) found");
+  trace_on_ = on;
+  labels_ = labels;
 }
 
 unsigned PlanExecutor::read_timeout() {
@@ -178,27 +315,36 @@ void PlanExecutor::enqueue(hipStream_t main) {
     }
     DDLB_HIP(bump_signal_launch(b, main));
   }
-  if (any_side_) {
-    // fork: every used side stream waits for everything already queued on `main`
+  if (any_side_ || compute_) {
+    // fork: every used side stream (and the CU-split compute stream) waits for everything
+    // already queued on `main`
     DDLB_HIP(hipEventRecord(fork_join_[0], main));
     for (size_t i = 1; i < streams_.size(); ++i)
       if (used_[i]) DDLB_HIP(hipStreamWaitEvent(streams_[i], fork_join_[0], 0));
+    if (compute_) DDLB_HIP(hipStreamWaitEvent(compute_, fork_join_[0], 0));
   }
   if (timeline_on_) host_us_.assign(ops_.size() / kOpWords, 0.f);
   for (size_t i = first; i < ops_.size(); i += kOpWords) {
     const int64_t* o = &ops_[i];
-    if (graph_on_ && (o[0] == OP_WAIT_SIGNAL || (o[0] == OP_GEMM && o[19] != 0)))
-      join_others(o[1], main);
+    // graph mode: a cross-process wait is ordered after everything enqueued before it on any
+    // stream (the deadlock-freedom argument of the eager enqueue order, kept under any node
+    // order the graph may pick); flag-gated GEMMs fed by other streams are not captured at all
+    if (graph_on_ && o[0] == OP_WAIT_SIGNAL) join_others(o[1], main);
     touched_[(size_t)o[1]] = true;
+    const size_t idx = i / kOpWords;
+    const bool tr = trace_on_ && idx < labels_.size();
+    if (tr) roctx().push(labels_[idx].c_str());
     if (!timeline_on_) {
       exec(&ops_[i], main);
+      if (tr) roctx().pop();
       continue;
     }
     const auto t0 = std::chrono::steady_clock::now();
     exec(&ops_[i], main);
     const auto t1 = std::chrono::steady_clock::now();
-    host_us_[i / kOpWords] = std::chrono::duration<float, std::micro>(t1 - t0).count();
-    DDLB_HIP(hipEventRecord(tl_ops_[i / kOpWords], S(ops_[i + 1], main)));
+    host_us_[idx] = std::chrono::duration<float, std::micro>(t1 - t0).count();
+    DDLB_HIP(hipEventRecord(tl_ops_[idx], S(ops_[i + 1], main)));
+    if (tr) roctx().pop();
   }
   if (any_side_) {  // join
     for (size_t i = 1; i < streams_.size(); ++i)
@@ -206,6 +352,10 @@ void PlanExecutor::enqueue(hipStream_t main) {
         DDLB_HIP(hipEventRecord(fork_join_[streams_.size() + i], streams_[i]));
         DDLB_HIP(hipStreamWaitEvent(main, fork_join_[streams_.size() + i], 0));
       }
+  }
+  if (compute_) {
+    DDLB_HIP(hipEventRecord(compute_join_, compute_));
+    DDLB_HIP(hipStreamWaitEvent(main, compute_join_, 0));
   }
 }
 
@@ -266,22 +416,6 @@ GemmArgs PlanExecutor::gemm_args(const int64_t* o) const {
   return g;
 }
 
-void PlanExecutor::prepare(uintptr_t main_stream) {
-  // hipBLASLt GEMMs (mode blas): build and autotune every shape now, on the stream the op will
-  // run on, so enqueueing a run never blocks on a tuning pass (blaslt.cpp autotune).
-  hipStream_t main = (hipStream_t)main_stream;
-  bool any = false;
-  for (size_t i = 0; i < ops_.size(); i += kOpWords) {
-    const int64_t* o = &ops_[i];
-    if (o[0] != OP_GEMM || o[18] != GEMM_MODE_BLAS) continue;
-    const GemmArgs g = gemm_args(o);
-    (void)blaslt_prepare(g, (int)o[15], (int)o[16], S(o[1], main));  // unsupported: MFMA path
-    if (cap_stream_ != nullptr) (void)blaslt_prepare(g, (int)o[15], (int)o[16], cap_stream_);
-    any = true;
-  }
-  if (any) DDLB_HIP(hipDeviceSynchronize());
-}
-
 void PlanExecutor::exec(const int64_t* o, hipStream_t main) {
   hipStream_t s = S(o[1], main);
   switch (o[0]) {
@@ -328,6 +462,26 @@ void PlanExecutor::exec(const int64_t* o, hipStream_t main) {
         DDLB_HIP(copy_launch(c, (int)o[6], s));
       }
       return;
+    case OP_COPY_BATCH: {
+      const int n = (int)o[2];
+      if (n < 1 || n > kMaxCopySeg || 4 + 3 * n > kOpWords)
+        throw std::runtime_error("plan: bad batch copy");
+      void* dst[kMaxCopySeg];
+      void* src[kMaxCopySeg];
+      size_t bytes[kMaxCopySeg];
+      for (int i = 0; i < n; ++i) {
+        dst[i] = (void*)o[4 + 3 * i];
+        src[i] = (void*)o[5 + 3 * i];
+        bytes[i] = (size_t)o[6 + 3 * i];
+      }
+      if (graph_on_) {  // captured as memcpy nodes (the batch API is not a capturable call)
+        for (int i = 0; i < n; ++i)
+          DDLB_HIP(hipMemcpyAsync(dst[i], src[i], bytes[i], hipMemcpyDeviceToDevice, s));
+      } else {
+        DDLB_HIP(copy_batch(dst, src, bytes, (size_t)n, s));
+      }
+      return;
+    }
     case OP_COPY_MULTI: {
       CopyArgs c;
       c.nseg = (int)o[2];

@@ -47,17 +47,33 @@ enum OpKind : int64_t {
   OP_REDUCE = 13,     // 2 dst, 3 count, 4 dtype, 5 nsrc, 6.. src ptrs
   OP_MEMSET = 14,     // 2 dst, 3 bytes, 4 byte value
   OP_COPY_MULTI = 15, // 2 nseg, 3 max blocks, then (dst, src, bytes) triples from word 4
+  OP_COPY_BATCH = 16, // 2 nseg, then (dst, src, bytes) triples from word 4: copy-engine copies
+                      //   submitted as ONE hipMemcpyBatchAsync (multicast_protocol=batch_memcpy)
 };
+// hipMemcpyBatchAsync, resolved at run time (dlsym): the HIP runtime torch ships (7.0) predates
+// it, so a batch falls back to one hipMemcpyAsync per segment on the same stream there.
+bool copy_batch_api_available();
+hipError_t copy_batch(void** dst, void** src, size_t* bytes, size_t n, hipStream_t s);
+// Host stack trace on SIGSEGV / SIGABRT / SIGBUS (glibc backtrace to stderr, then the default
+// action): a native frame list for crashes inside the HIP runtime without attaching a debugger.
+void install_crash_handler();
 
 class PlanExecutor {
  public:
   PlanExecutor(int device, int nstreams, int nevents, const std::vector<int>& priorities);
   ~PlanExecutor();
   void load(const std::vector<int64_t>& ops);
-  // Bind-time work that must not happen inside run(): hipBLASLt plan building / autotuning
-  // (host-synchronous) for the plan's blas GEMMs. Call once after load().
-  void prepare(uintptr_t main_stream);
   void set_comm(RcclComm* comm) { comm_ = comm; }
+  // CU budget of the communication: the side streams (RCCL / copy kernels /
+  // flag kernels) are created with hipExtStreamCreateWithCUMask on `comm_cus` CUs, and the
+  // plan's stream-0 ops run on a private compute stream masked to the complement (forked from
+  // and joined back into the caller's stream). 0 = unmasked. Call before the first run().
+  void set_cu_split(int comm_cus);
+  int cu_split() const { return comm_cus_; }
+  // Stage-level tracing: while on, every op's enqueue is wrapped in a roctx range named by
+  // `labels` (e.g. "gemm s3", "copy p2 b1"), so `rocprofv3 --marker-trace --kernel-rename`
+  // splits a pipeline run into its stages. roctx is loaded lazily (no link dependency).
+  void set_trace(bool on, const std::vector<std::string>& labels);
   // Enqueue the whole plan behind `main_stream`; returns the epoch used (1, 2, ...).
   unsigned run(uintptr_t main_stream);
   unsigned epoch() const { return epoch_; }
@@ -90,8 +106,13 @@ class PlanExecutor {
   hipGraph_t graph_ = nullptr;
   hipGraphExec_t graph_exec_ = nullptr;
   hipStream_t S(int64_t idx, hipStream_t main) const {
-    return idx == 0 ? main : streams_.at((size_t)idx);
+    return idx == 0 ? (compute_ ? compute_ : main) : streams_.at((size_t)idx);
   }
+  int comm_cus_ = 0;
+  hipStream_t compute_ = nullptr;        // stream-0 ops under a CU split
+  hipEvent_t compute_fork_ = nullptr, compute_join_ = nullptr;
+  bool trace_on_ = false;
+  std::vector<std::string> labels_;
   int device_;
   std::vector<hipStream_t> streams_;  // [0] unused (= caller stream)
   std::vector<hipEvent_t> events_;

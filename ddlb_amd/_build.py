@@ -40,7 +40,6 @@ SOURCES = [  # heaviest translation units first (the parallel build's critical p
     "gemm/gemm_mx.hip",
     "gemm/gemm_generic.hip",
     "gemm/gemm_mfma.hip",
-    "gemm/blaslt.cpp",
     "runtime/kernels.hip",
     "comm/comm.cpp",
     "runtime/plan.cpp",
@@ -123,7 +122,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
         return out
     tl = _torch_lib_dir()
     cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", out + ".tmp",
-           f"-L{ROCM}/lib", "-lrccl", "-lhipblaslt", "-lamdhip64"]
+           f"-L{ROCM}/lib", "-lrccl", "-lamdhip64"]
     if tl:
         cmd.append(f"-Wl,-rpath,{tl}")
     if verbose:

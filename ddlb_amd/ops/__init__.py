@@ -1,8 +1,8 @@
 """Native ops: loader for the in-tree extension ``ddlb_amd._C``.
 
-``load()`` imports torch FIRST (so the extension's ``libamdhip64.so.7`` / ``librccl.so.1`` /
-``libhipblaslt.so.1`` resolve to the copies torch ships), then the extension. On a GPU box a missing or
-stale extension is an error, never a silent PyTorch fallback.
+``load()`` imports torch FIRST (so the extension's ``libamdhip64.so.7`` / ``librccl.so.1`` resolve
+to the copies torch ships), then the extension. On a GPU box a missing or stale extension is an
+error, never a silent PyTorch fallback.
 """
 
 from __future__ import annotations
@@ -24,8 +24,6 @@ def load(build_if_missing: bool = None):
         return _C
     import torch  # noqa: F401  (must precede the extension, see module docstring)
 
-    _pin_torch_libs(torch)
-
     if build_if_missing is None:
         build_if_missing = os.environ.get("DDLB_AUTOBUILD", "1") == "1"
     try:
@@ -40,19 +38,6 @@ def load(build_if_missing: bool = None):
         importlib.invalidate_caches()
         _C = importlib.import_module("ddlb_amd._C")
     return _C
-
-
-def _pin_torch_libs(torch) -> None:
-    """Map torch's own hipBLASLt before the extension (torch loads it lazily), so both use one
-    copy of the library and of its kernel database."""
-    import ctypes
-
-    lib = os.path.join(os.path.dirname(torch.__file__), "lib", "libhipblaslt.so")
-    if os.path.exists(lib):
-        try:
-            ctypes.CDLL(lib, mode=ctypes.RTLD_GLOBAL)
-        except OSError:
-            pass
 
 
 def available() -> bool:

@@ -22,7 +22,7 @@ TILES = {"auto": 0, "256x256": 1, "256x128": 2, "128x256": 3, "128x128": 4, "pp2
          "256x128w4": 7, "p256": 8, "p128": 9,
          "i256": 10, "i128": 11, "i256w4": 12, "pi256": 13, "pi256w4": 14, "r256": 15,
          "t8": 16, "pt8": 17, "t4": 18, "pt4": 19}
-MODES = {"auto": 0, "generic": 1, "mx": 2, "blas": 3}
+MODES = {"auto": 0, "generic": 1, "mx": 2}
 ACTS = {"none": 0, "gelu": 1, "relu": 2, "silu": 3}
 
 SUPPORTED_IN = ("float32", "float16", "bfloat16", "float8_e4m3fn", "float64")

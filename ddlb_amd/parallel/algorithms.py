@@ -42,8 +42,8 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
-from ddlb_amd.parallel.plan import (COPY_ENGINE, COPY_KERNEL, DT_SIZE, DT_U8, SIG_IN_LAUNCH,
-                                    SIG_STREAM, Plan, Ref)
+from ddlb_amd.parallel.plan import (COPY_ENGINE, COPY_KERNEL, DT_SIZE, DT_U8, OP_GEMM,
+                                    SIG_IN_LAUNCH, SIG_KERNEL, SIG_STREAM, Plan, Ref)
 
 S_MAIN, S_COMM = 0, 1
 TILE_PT4 = 19  # csrc/gemm/gemm.h Tile::TILE_PT4 (the only kernel carrying in-kernel copies)
@@ -79,6 +79,10 @@ class AlgoConfig:
     ag_mode: int = 30
     act: int = 0                        # columnwise: fused GEMM epilogue activation (ACT_*)
     direction: str = "pull"             # columnwise ipc: pull peers' shards | push mine to peers
+    # CU budget of the communication: side streams on comm_cus CUs
+    # (hipExtStreamCreateWithCUMask), stream-0 GEMMs on the complement; 0 = unmasked
+    comm_cus: int = 0
+    register: bool = False              # RCCL buffers from ncclMemAlloc + ncclCommRegister
 
 
 @dataclass
@@ -137,6 +141,17 @@ class _Flags:
         return Ref("flags", 4 * (base + idx), owner)
 
 
+def _finish(plan: Plan, cfg: AlgoConfig) -> None:
+    """Record the data-plane settings the binder applies (CU split, RCCL registration) and size
+    the compute-stream GEMMs to the CUs a split leaves them: a persistent GEMM's grid is one
+    workgroup per CU, so on a masked stream it must not count the communication's CUs."""
+    plan.meta.update(comm_cus=cfg.comm_cus, register=cfg.register)
+    if cfg.comm_cus > 0:
+        for op in plan.ops:
+            if op.kind == OP_GEMM and op.stream == S_MAIN and op.args.get("flags") is None:
+                op.args["reserve_cus"] = max(op.args.get("reserve_cus", 0), cfg.comm_cus)
+
+
 def _chunks(flags: List[Ref], n: int = 16):
     for i in range(0, len(flags), n):
         yield flags[i:i + n]
@@ -190,6 +205,13 @@ def check_columnwise(d: int, m: int, n: int, k: int, cfg: AlgoConfig, ein: int =
 
 def build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, dout: int,
                         cfg: AlgoConfig) -> Tuple[Plan, PlanIO]:
+    plan, io = _build_tp_columnwise(rank, d, m, n, k, din, dout, cfg)
+    _finish(plan, cfg)
+    return plan, io
+
+
+def _build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, dout: int,
+                         cfg: AlgoConfig) -> Tuple[Plan, PlanIO]:
     check_columnwise(d, m, n, k, cfg, DT_SIZE[din])
     ein, eout = DT_SIZE[din], DT_SIZE[dout]
     ml = m // d
@@ -467,8 +489,10 @@ def _ipc_pull_shards(plan: Plan, rank: int, d: int, cfg: AlgoConfig, flags: _Fla
         after_ready()
     done: Dict[int, List[int]] = {}
     nblk = len(jobs[0][1])
-    if cfg.protocol == "kernel":
-        # one CU copy kernel per block index, reading every peer (copy_multi, <= 8 segments)
+    if cfg.protocol in ("kernel", "batch_memcpy") and not (
+            cfg.protocol == "batch_memcpy" and cfg.inter_stream_sync):
+        # ONE op per block index reading every peer: a CU copy kernel (copy_multi) or one
+        # batched copy-engine submission (copy_batch = hipMemcpyBatchAsync), <= 8 segments each
         st = _s_copy(0)
         _wait(plan, st, [flags.ref("READY", p) for p, _ in jobs], cfg)
         for b in range(nblk):
@@ -477,9 +501,10 @@ def _ipc_pull_shards(plan: Plan, rank: int, d: int, cfg: AlgoConfig, flags: _Fla
                 r0, nr = blocks[b]
                 segs.append((row_ref(r0), row_ref(r0).at(p), nr * row_bytes))
             for i in range(0, len(segs), 8):
-                plan.copy_multi(st, segs[i:i + 8], max_blocks=cfg.copy_blocks)
-            if arrive_block is not None:
-                _signal(plan, st, [arrive_block(p, b) for p, _ in jobs], cfg)
+                if cfg.protocol == "kernel":
+                    plan.copy_multi(st, segs[i:i + 8], max_blocks=cfg.copy_blocks)
+                else:
+                    plan.copy_batch(st, segs[i:i + 8])
             if arrive_block is not None:
                 _signal(plan, st, [arrive_block(p, b) for p, _ in jobs], cfg)
             e = plan.event()
@@ -636,6 +661,13 @@ def check_rowwise(d: int, m: int, n: int, k: int, cfg: AlgoConfig) -> None:
 
 def build_tp_rowwise(rank: int, d: int, m: int, n: int, k: int, din: int, dout: int,
                      cfg: AlgoConfig) -> Tuple[Plan, PlanIO]:
+    plan, io = _build_tp_rowwise(rank, d, m, n, k, din, dout, cfg)
+    _finish(plan, cfg)
+    return plan, io
+
+
+def _build_tp_rowwise(rank: int, d: int, m: int, n: int, k: int, din: int, dout: int,
+                      cfg: AlgoConfig) -> Tuple[Plan, PlanIO]:
     check_rowwise(d, m, n, k, cfg)
     ein, eout = DT_SIZE[din], DT_SIZE[dout]
     kl, ml = k // d, m // d
@@ -703,7 +735,11 @@ def build_tp_rowwise(rank: int, d: int, m: int, n: int, k: int, din: int, dout: 
         slots = [(RECV + rank * blk).at(q) if q != rank else RECV + rank * blk for q in range(d)]
         gemm(S_MAIN, 0, RECV + rank * blk, m, c_shards=slots, c_shard_rows=ml, nshards=d,
              tile_order=2)
-        _signal(plan, S_MAIN, [flags.ref("READY", rank, owner=p) for p in peers], cfg)
+        # READY always from the signal kernel: its system-scope release fence orders the GEMM's
+        # remote C stores (over xGMI, into the peers' RECV) before the flag, whatever cfg.signal
+        # says (a stream memop has no such fence for stores another kernel issued)
+        for c in _chunks([flags.ref("READY", rank, owner=p) for p in peers]):
+            plan.signal(S_MAIN, c, method=SIG_KERNEL)
         _wait(plan, S_MAIN, [flags.ref("READY", p) for p in peers], cfg)
         plan.reduce(S_MAIN, OUT, [RECV + q * blk for q in range(d)], ml * n, dout)
         _signal(plan, S_MAIN, [flags.ref("ACK", rank, owner=p) for p in peers], cfg)
@@ -763,6 +799,14 @@ def _row_gather_sources(plan, rank, d, cfg, own_ref, blk, peers, stage_name):
     if cfg.protocol == "kernel":
         return [own_ref] + [own_ref.at(p) for p in peers]
     R = plan.buffer(stage_name, d * blk)
+    if cfg.protocol == "batch_memcpy":  # every peer's block in one batched submission
+        st = _s_copy(0)
+        plan.edge(S_MAIN, st)
+        segs = [(R + p * blk, own_ref.at(p), blk) for p in peers]
+        for i in range(0, len(segs), 8):
+            plan.copy_batch(st, segs[i:i + 8])
+        plan.edge(st, S_MAIN)
+        return [own_ref] + [R + p * blk for p in peers]
     evs = []
     for idx, p in enumerate(peers):
         st = _s_copy(0) if cfg.protocol == "batch_memcpy" else _s_copy(idx)

@@ -14,8 +14,7 @@ from __future__ import annotations
 import os
 from typing import Dict, List, Optional
 
-from ddlb_amd.parallel.plan import (OP_ALLGATHER, OP_RECV, OP_REDUCE_SCATTER, OP_SEND, DT_SIZE,
-                                    Plan, Ref)
+from ddlb_amd.parallel.plan import DT_SIZE, RCCL_OPS, Plan, Ref
 from ddlb_amd.parallel.sim import TORCH_DT
 
 
@@ -144,8 +143,8 @@ class NativeContext:
             b.release()
         self._owned = [b for b in self._owned if b.h is not None]
 
-    def bind(self, plan: Plan, externals=None) -> "BoundPlan":
-        return BoundPlan(self, plan, externals)
+    def bind(self, plan: Plan, externals=None, trace: bool = False) -> "BoundPlan":
+        return BoundPlan(self, plan, externals, trace=trace)
 
     def close(self) -> None:
         for b in self._owned:
@@ -158,19 +157,44 @@ class NativeContext:
                 self._rccl = None
 
 
+def rccl_buffers(plan: Plan) -> List[str]:
+    """Names of the buffers the plan's RCCL ops read or write (registration candidates)."""
+    names: List[str] = []
+    for op in plan.ops:
+        if op.kind in RCCL_OPS:
+            for key in ("send", "recv", "buf"):
+                ref = op.args.get(key)
+                if ref is not None and ref.buf not in names:
+                    names.append(ref.buf)
+    return names
+
+
 class BoundPlan:
     """``externals`` maps a LOCAL buffer name to an existing device tensor that backs it
-    (zero-copy chaining: e.g. the columnwise output feeding the rowwise input of an MLP)."""
+    (zero-copy chaining: e.g. the columnwise output feeding the rowwise input of an MLP).
 
-    def __init__(self, ctx: NativeContext, plan: Plan, externals=None):
+    Plan settings applied here (``plan.meta``): ``register`` — the buffers RCCL touches come from
+    ``ncclMemAlloc`` and are registered with our communicator (``ncclCommRegister``);
+    ``comm_cus`` — the executor's CU split (side streams on that many CUs, stream-0 ops on the
+    rest). ``trace`` (or ``DDLB_PLAN_TRACE=1``) turns on a roctx range per op."""
+
+    def __init__(self, ctx: NativeContext, plan: Plan, externals=None, trace: bool = False):
         import torch
 
         self.ctx, self.plan = ctx, plan
         self.local: Dict[str, torch.Tensor] = {}
         self.sym: Dict[str, SymmetricBuffer] = {}
+        self.rmem: Dict[str, object] = {}
         dev = torch.device("cuda", ctx.device_index)
         externals = dict(externals or {})
+        registered = set(rccl_buffers(plan)) if plan.meta.get("register") else set()
         for name, spec in plan.buffers.items():  # dict order == identical on every rank
+            if name in registered and name not in externals and not spec.symmetric:
+                # zero-copy RCCL buffer: ncclMemAlloc + ncclCommRegister on our communicator
+                mem = ctx.C.RcclMem(ctx.rccl(), max(spec.nbytes, 16), ctx.device_index)
+                self.rmem[name] = mem
+                self.local[name] = torch.from_dlpack(ctx.C.rccl_mem_dlpack(mem, ctx.device_index))
+                continue
             if name in externals:
                 t = externals.pop(name)
                 if spec.symmetric:
@@ -199,9 +223,12 @@ class BoundPlan:
         self.ex = C.PlanExecutor(ctx.device_index, plan.nstreams, max(plan.nevents, 1),
                                  list(plan.stream_priority))
         self.ex.load(words)
-        self.ex.prepare(_raw_stream(ctx.device_index))  # bind-time hipBLASLt tuning, if any
-        if any(op.kind in (OP_ALLGATHER, OP_REDUCE_SCATTER, OP_SEND, OP_RECV) for op in plan.ops):
+        if any(op.kind in RCCL_OPS for op in plan.ops):
             self.ex.set_comm(ctx.rccl())
+        if plan.meta.get("comm_cus", 0):
+            self.ex.set_cu_split(int(plan.meta["comm_cus"]))
+        if trace or os.environ.get("DDLB_PLAN_TRACE", "0") == "1":
+            self.ex.set_trace(True, plan.labels())
         torch.cuda.synchronize(dev)
 
     def resolve(self, ref: Ref) -> int:
@@ -279,4 +306,7 @@ class BoundPlan:
         torch.cuda.synchronize()
         self.ex = None
         self.ctx.release_symmetric(list(self.sym.values()))
+        for name in list(self.rmem):  # deregister + ncclMemFree while the communicator lives
+            self.local.pop(name, None)
+            self.rmem.pop(name).release()
         self.sym, self.local = {}, {}

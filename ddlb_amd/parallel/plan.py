@@ -22,12 +22,14 @@ from typing import Callable, Dict, List, Optional, Sequence, Tuple
 OP_WORDS = 34
 (OP_NOP, OP_GEMM, OP_RECORD, OP_WAIT, OP_ALLGATHER, OP_REDUCE_SCATTER, OP_SEND, OP_RECV,
  OP_GROUP_START, OP_GROUP_END, OP_COPY, OP_SIGNAL, OP_WAIT_SIGNAL, OP_REDUCE, OP_MEMSET,
- OP_COPY_MULTI) = range(16)
+ OP_COPY_MULTI, OP_COPY_BATCH) = range(17)
 OP_NAMES = {OP_NOP: "nop", OP_GEMM: "gemm", OP_RECORD: "record", OP_WAIT: "wait",
             OP_ALLGATHER: "allgather", OP_REDUCE_SCATTER: "reduce_scatter", OP_SEND: "send",
             OP_RECV: "recv", OP_GROUP_START: "group_start", OP_GROUP_END: "group_end",
             OP_COPY: "copy", OP_SIGNAL: "signal", OP_WAIT_SIGNAL: "wait_signal",
-            OP_REDUCE: "reduce", OP_MEMSET: "memset", OP_COPY_MULTI: "copy_multi"}
+            OP_REDUCE: "reduce", OP_MEMSET: "memset", OP_COPY_MULTI: "copy_multi",
+            OP_COPY_BATCH: "copy_batch"}
+RCCL_OPS = (OP_ALLGATHER, OP_REDUCE_SCATTER, OP_SEND, OP_RECV)
 
 # dtype codes (csrc/gemm/gemm.h)
 DT_F32, DT_F16, DT_BF16, DT_FP8, DT_F64, DT_U8 = 0, 1, 2, 3, 4, 5
@@ -229,6 +231,13 @@ class Plan:
             raise ValueError("copy_multi takes 1..8 segments")
         return self._add(OP_COPY_MULTI, stream, segs=list(segs), max_blocks=max_blocks)
 
+    def copy_batch(self, stream: int, segs: Sequence[Tuple[Ref, Ref, int]]) -> Op:
+        """Copy-engine copies submitted together (``hipMemcpyBatchAsync``: the
+        ``batch_memcpy`` protocol, one API call per block across all peers)."""
+        if not 1 <= len(segs) <= 8:
+            raise ValueError("copy_batch takes 1..8 segments")
+        return self._add(OP_COPY_BATCH, stream, segs=list(segs))
+
     def signal(self, stream: int, flags: Sequence[Ref], method: int = SIG_STREAM,
                delta: int = 0) -> Op:
         if not 1 <= len(flags) <= 16:
@@ -284,8 +293,8 @@ class Plan:
             elif k == OP_COPY:
                 w[2:7] = [resolve(a["dst"]), resolve(a["src"]), a["nbytes"], a["method"],
                           a["max_blocks"]]
-            elif k == OP_COPY_MULTI:
-                w[2], w[3] = len(a["segs"]), a["max_blocks"]
+            elif k in (OP_COPY_MULTI, OP_COPY_BATCH):
+                w[2], w[3] = len(a["segs"]), a.get("max_blocks", 0)
                 for i, (d, s, n) in enumerate(a["segs"]):
                     w[4 + 3 * i:7 + 3 * i] = [resolve(d), resolve(s), n]
             elif k in (OP_SIGNAL, OP_WAIT_SIGNAL):
@@ -300,6 +309,49 @@ class Plan:
                 w[2:5] = [resolve(a["dst"]), a["nbytes"], a["value"]]
             words.extend(int(x) for x in w)
         return words
+
+    def labels(self) -> List[str]:
+        """One trace label per op (the roctx range names of ``PlanExecutor.set_trace``): GEMMs
+        numbered in issue order ("gemm s3"; "+ag" in-kernel all-gather, "+gated" arrival
+        flags), copies by peer and block ("copy p2 b1"), collectives numbered, flag ops by
+        their first flag word."""
+        out: List[str] = []
+        count: Dict[str, int] = {}
+        blocks: Dict[Tuple[str, int], int] = {}
+
+        def nxt(key: str) -> int:
+            count[key] = count.get(key, 0) + 1
+            return count[key] - 1
+
+        def peer_of(refs) -> int:
+            for r in refs:
+                if r.owner is not None and r.owner != self.rank:
+                    return r.owner
+            return self.rank
+
+        for op in self.ops:
+            a, k = op.args, op.kind
+            if k == OP_GEMM:
+                tag = "+ag" if a.get("ag") else ("+gated" if a.get("flags") is not None else "")
+                out.append(f"gemm s{nxt('gemm')}{tag}")
+            elif k in (OP_COPY, OP_COPY_MULTI, OP_COPY_BATCH):
+                refs = ([a["src"], a["dst"]] if k == OP_COPY else
+                        [r for seg in a["segs"] for r in seg[:2]])
+                p = peer_of(refs)
+                key = ("copy", p)
+                blocks[key] = blocks.get(key, -1) + 1
+                multi = "" if k == OP_COPY else f" x{len(a['segs'])}"
+                out.append(f"{OP_NAMES[k]} p{p} b{blocks[key]}{multi}")
+            elif k in (OP_SIGNAL, OP_WAIT_SIGNAL):
+                f = a["flags"][0]
+                out.append(f"{OP_NAMES[k]} {f.buf}+{f.off}" +
+                           (f"@{f.owner}" if f.owner is not None else "") +
+                           (f" x{len(a['flags'])}" if len(a["flags"]) > 1 else ""))
+            elif k in RCCL_OPS:
+                out.append(f"{OP_NAMES[k]} #{nxt(OP_NAMES[k])}")
+            else:
+                out.append(OP_NAMES[k])
+        return out
 
     def describe(self) -> str:
         """Human-readable listing (``python -m ddlb_amd.parallel.explain`` prints this)."""

@@ -1,0 +1,304 @@
+"""Multi-GPU preflight: is the N>1 data plane of THIS node sound, before a benchmark spends time on it?
+
+The reference's product is ``mpirun -np N`` runs on real GPUs (``/root/reference/README.md:80-88``),
+each child building its NCCL process group (``ddlb/primitives/TPColumnwise/pytorch.py:53-59``).
+Here every N>1 path runs on mechanisms a shared-GPU rehearsal cannot exercise (RCCL at world > 1,
+IPC peer memory and flag words over xGMI), so ``bench.py`` runs these checks once per job, each in
+its own time-limited child, and drops the candidate families that fail:
+
+==============  ==================================================================================
+check           what it proves (every rank, every peer, two epochs)
+==============  ==================================================================================
+``torch_nccl``  torch's RCCL process group (the ``pytorch`` slot and the control plane): a SUM
+                all-reduce of rank-dependent integers
+``rccl``        our own ``ncclComm_t`` (``NativeContext.rccl``) on our streams: an all-gather of a
+                byte pattern and an f32 reduce-scatter, compared bytewise
+``ipc``         IPC mapping of symmetric buffers + the READY/ACK epoch handshake with every peer,
+                with stream-memop signals (``hipStreamWriteValue32`` / ``WaitValue32``)
+``ipc_ksig``    the same handshake with the signal / wait kernels (system-scope release, the
+                form graph replay and ``signal=kernel`` use)
+``ipc_kernel``  CU-copy pull (``copy_multi``: peer HBM read by a kernel over xGMI) of every
+                peer's pattern, then a flag, then a read-back check
+``ipc_sdma``    copy-engine pull (``hipMemcpyAsync`` from IPC-mapped peer memory, one stream per
+                peer) of every peer's pattern
+``ipc_push``    copy-engine push (posted writes into each peer's receive slot) + DONE flag
+==============  ==================================================================================
+
+Every check is a :class:`~ddlb_amd.parallel.plan.Plan` executed by the native executor, so the
+same plans run on the CPU simulator in the tests (``tests/test_preflight.py``). A check that hangs
+(a flag that never arrives over the link) leaves its phase missing from the progress file the
+child rewrites after each phase; the parent reports it as ``failed: timeout``.
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import time
+from typing import Callable, Dict, List, Optional
+
+from ddlb_amd.parallel.plan import (COPY_ENGINE, DT_F32, DT_U8, SIG_KERNEL, SIG_STREAM, Plan,
+                                    Ref)
+
+IPC_PHASES = ("ipc", "ipc_ksig", "ipc_kernel", "ipc_sdma", "ipc_push")
+RCCL_PHASES = ("torch_nccl", "rccl")
+PATTERN_BYTES = 1 << 20      # per rank and phase: 1 MiB (several xGMI packets, small enough)
+RS_COUNT = 4096              # f32 elements per rank of the reduce-scatter check
+
+
+def pattern(owner: int, nbytes: int, epoch: int = 1):
+    """int32 words that differ per owner, epoch and position (no two ranks agree anywhere)."""
+    import torch
+
+    idx = torch.arange(nbytes // 4, dtype=torch.int64)
+    v = (idx * 2654435761 + (owner + 1) * 40503 + epoch * 7919) & 0x7FFFFFFF
+    return v.to(torch.int32)
+
+
+def _flags(plan: Plan, d: int) -> Dict[str, Callable[..., Ref]]:
+    plan.buffer("flags", max(256, 4 * 3 * d), symmetric=True, zero=True)
+
+    def slot(base: int) -> Callable[..., Ref]:
+        return lambda i, owner=None: Ref("flags", 4 * (base * d + i), owner)
+
+    return {"READY": slot(0), "ACK": slot(1), "DONE": slot(2)}
+
+
+def build_ipc_plan(rank: int, d: int, phase: str, nbytes: int = PATTERN_BYTES) -> Plan:
+    """Plan of one IPC check. Buffers: ``X`` (symmetric, my pattern), ``R`` (receive region,
+    ``d`` slots of ``nbytes``; symmetric for the push check)."""
+    if phase not in IPC_PHASES:
+        raise ValueError(f"unknown IPC preflight phase {phase}")
+    peers = [p for p in range(d) if p != rank]
+    plan = Plan(rank, d, nstreams=2 + max(d - 1, 1), stream_priority=[0] * (2 + max(d - 1, 1)))
+    plan.meta.update(preflight=phase)
+    f = _flags(plan, d)
+    X = plan.buffer("X", nbytes, symmetric=True)
+    R = plan.buffer("R", d * nbytes, symmetric=(phase == "ipc_push"))
+    sig = SIG_KERNEL if phase == "ipc_ksig" else SIG_STREAM
+    plan.signal(0, [f["READY"](rank, owner=p) for p in peers], method=sig)
+    plan.wait_signal(0, [f["READY"](p) for p in peers], method=sig)
+    if phase == "ipc_kernel":
+        segs = [(R + p * nbytes, X.at(p), nbytes) for p in peers]
+        for i in range(0, len(segs), 8):
+            plan.copy_multi(0, segs[i:i + 8], max_blocks=64)
+    elif phase == "ipc_sdma":
+        evs = []
+        for idx, p in enumerate(peers):
+            st = 2 + idx
+            plan.edge(0, st)
+            plan.copy(st, R + p * nbytes, X.at(p), nbytes, method=COPY_ENGINE)
+            e = plan.event()
+            plan.record(st, e)
+            evs.append(e)
+        for e in evs:
+            plan.wait(0, e)
+    elif phase == "ipc_push":
+        for idx, p in enumerate(peers):
+            st = 2 + idx
+            plan.edge(0, st)
+            plan.copy(st, (R + rank * nbytes).at(p), X, nbytes, method=COPY_ENGINE)
+            plan.signal(st, [f["DONE"](rank, owner=p)], method=SIG_STREAM)
+        plan.wait_signal(0, [f["DONE"](p) for p in peers], method=SIG_STREAM)
+    # nobody's X / R is touched again (next epoch's fill, teardown) before every peer is done
+    plan.signal(0, [f["ACK"](rank, owner=p) for p in peers], method=sig)
+    plan.wait_signal(0, [f["ACK"](p) for p in peers], method=sig)
+    return plan
+
+
+def build_rccl_plan(rank: int, d: int, nbytes: int = PATTERN_BYTES,
+                    count: int = RS_COUNT) -> Plan:
+    """All-gather of ``SEND`` (bytes) into ``AG`` and an f32 reduce-scatter ``RSIN`` -> ``RSOUT``
+    on our own communicator, on a side stream (as the pipelines enqueue them)."""
+    plan = Plan(rank, d, nstreams=2, stream_priority=[0, 1])
+    plan.meta.update(preflight="rccl")
+    send = plan.buffer("SEND", nbytes)
+    ag = plan.buffer("AG", d * nbytes)
+    rsin = plan.buffer("RSIN", d * count * 4)
+    rsout = plan.buffer("RSOUT", count * 4)
+    plan.edge(0, 1)
+    plan.allgather(1, send, ag, nbytes, DT_U8)
+    plan.reduce_scatter(1, rsin, rsout, count, DT_F32)
+    plan.edge(1, 0)
+    return plan
+
+
+def rs_input(owner: int, d: int, count: int = RS_COUNT):
+    """Reduce-scatter input of ``owner``: small integers, so every f32 sum is exact."""
+    import torch
+
+    idx = torch.arange(d * count, dtype=torch.int64)
+    return ((idx % 13) + 1 + owner * 3).to(torch.float32)
+
+
+def rs_expected(rank: int, d: int, count: int = RS_COUNT):
+    import torch
+
+    return sum(rs_input(q, d, count) for q in range(d))[rank * count:(rank + 1) * count].to(
+        torch.float32)
+
+
+# ------------------------------------------------------------------------------ execution
+class _Progress:
+    """Per-phase results, rewritten to ``path`` after every phase (a hang leaves the rest out)."""
+
+    def __init__(self, path: Optional[str]):
+        self.path = path
+        self.res: Dict[str, str] = {}
+
+    def put(self, phase: str, status: str) -> None:
+        self.res[phase] = status
+        if self.path:
+            tmp = self.path + ".tmp"
+            with open(tmp, "w") as fh:
+                json.dump(self.res, fh)
+            os.replace(tmp, self.path)
+
+
+def _run_checked(name: str, progress: _Progress, fn: Callable[[], None]) -> bool:
+    t0 = time.perf_counter()
+    try:
+        fn()
+    except Exception as e:  # recorded, never raised: the other phases still run
+        progress.put(name, f"failed: {type(e).__name__}: {str(e).splitlines()[0][:160]}"
+                     if str(e) else f"failed: {type(e).__name__}")
+        return False
+    progress.put(name, f"ok ({(time.perf_counter() - t0) * 1e3:.0f} ms)")
+    return True
+
+
+def _check_eq(got, want, what: str) -> None:
+    import torch
+
+    if not torch.equal(got.cpu(), want.cpu()):
+        bad = int((got.cpu() != want.cpu()).sum())
+        raise AssertionError(f"{what}: {bad} of {want.numel()} words differ")
+
+
+def run_ipc_checks(comm, phases=IPC_PHASES, progress_path: Optional[str] = None,
+                   nbytes: int = PATTERN_BYTES, epochs: int = 2) -> Dict[str, str]:
+    import torch
+
+    ctx = comm.native()
+    prog = _Progress(progress_path)
+    r, d = comm.rank, comm.world_size
+    dev = comm.device
+    for phase in phases:
+        def one():
+            plan = build_ipc_plan(r, d, phase, nbytes)
+            bound = ctx.bind(plan)
+            try:
+                for ep in range(1, epochs + 1):
+                    x = bound.buffer("X").view(torch.int32)
+                    x.copy_(pattern(r, nbytes, ep).to(dev))
+                    bound.buffer("R").view(torch.int32).fill_(-1)
+                    torch.cuda.synchronize(dev)
+                    comm.barrier()  # every rank's X of this epoch is in place
+                    bound.run()
+                    torch.cuda.synchronize(dev)
+                    bound.check_health()
+                    if phase in ("ipc_kernel", "ipc_sdma", "ipc_push"):
+                        rv = bound.buffer("R").view(torch.int32)
+                        for p in range(d):
+                            if p != r:
+                                _check_eq(rv[p * nbytes // 4:(p + 1) * nbytes // 4],
+                                          pattern(p, nbytes, ep), f"{phase} slot of rank {p}")
+                    comm.barrier()  # nobody refills X while a peer may still read it
+            finally:
+                bound.close()
+
+        _run_checked(phase, prog, one)
+    return prog.res
+
+
+def run_rccl_checks(comm, phases=RCCL_PHASES, progress_path: Optional[str] = None,
+                    nbytes: int = PATTERN_BYTES, count: int = RS_COUNT) -> Dict[str, str]:
+    import torch
+    import torch.distributed as dist
+
+    prog = _Progress(progress_path)
+    r, d = comm.rank, comm.world_size
+    dev = comm.device
+    if "torch_nccl" in phases:
+        def torch_pg():
+            if dist.get_backend() == "nccl":
+                grp = None
+            else:  # control plane forced to gloo: build a separate RCCL group
+                grp = dist.new_group(backend="nccl")
+            t = torch.full((1024,), float(r + 1), device=dev)
+            dist.all_reduce(t, group=grp)
+            torch.cuda.synchronize(dev)
+            want = torch.full((1024,), float(d * (d + 1) // 2))
+            _check_eq(t, want, "all_reduce")
+            if grp is not None:
+                dist.destroy_process_group(grp)
+
+        _run_checked("torch_nccl", prog, torch_pg)
+    if "rccl" in phases:
+        def own():
+            ctx = comm.native()
+            bound = ctx.bind(build_rccl_plan(r, d, nbytes, count))
+            try:
+                for ep in (1, 2):
+                    bound.buffer("SEND").view(torch.int32).copy_(pattern(r, nbytes, ep).to(dev))
+                    bound.buffer("RSIN").view(torch.float32).copy_(rs_input(r, d, count).to(dev))
+                    torch.cuda.synchronize(dev)
+                    bound.run()
+                    torch.cuda.synchronize(dev)
+                    ag = bound.buffer("AG").view(torch.int32)
+                    for q in range(d):
+                        _check_eq(ag[q * nbytes // 4:(q + 1) * nbytes // 4],
+                                  pattern(q, nbytes, ep), f"all-gather slot of rank {q}")
+                    _check_eq(bound.buffer("RSOUT").view(torch.float32)[:count],
+                              rs_expected(r, d, count), "reduce-scatter")
+                    comm.barrier()
+            finally:
+                bound.close()
+
+        _run_checked("rccl", prog, own)
+    return prog.res
+
+
+def families_ok(results: Dict[str, str]) -> Dict[str, bool]:
+    """Which data-plane families a benchmark may use, from merged (all-rank) phase results."""
+    ok = {k: str(v).startswith("ok") for k, v in results.items()}
+    return ok
+
+
+def needs(impl: str, opts: Dict) -> List[str]:
+    """Preflight checks a benchmark candidate relies on (``bench.py`` drops it if any failed)."""
+    if impl == "pytorch":
+        return ["torch_nccl"]
+    if impl != "native":
+        return []
+    backend = opts.get("backend", "rccl")
+    if backend in ("rccl", "nccl"):
+        return ["rccl"]
+    out = ["ipc"]
+    if opts.get("graph") in (True, "auto") or opts.get("signal") == "kernel":
+        out.append("ipc_ksig")
+    proto = opts.get("multicast_protocol", "memcpy")
+    alg = opts.get("algorithm", "default")
+    if alg == "direct" or proto == "kernel":
+        out.append("ipc_kernel")   # peer HBM read by CUs (copy kernel, in-kernel AG, LDS-DMA)
+    elif opts.get("direction") == "push":
+        out.append("ipc_push")
+    else:
+        out.append("ipc_sdma")
+    return out
+
+
+def merge(per_rank: List[Dict[str, str]], phases) -> Dict[str, str]:
+    """One status per phase over every rank: ok only if every rank passed it; a phase missing on
+    some rank (its child was killed mid-phase) is a timeout."""
+    out: Dict[str, str] = {}
+    for ph in phases:
+        st = [res.get(ph) for res in per_rank]
+        bad = [s for s in st if s is not None and not str(s).startswith("ok")]
+        if bad:
+            out[ph] = str(bad[0])
+        elif any(s is None for s in st):
+            out[ph] = "failed: timeout"
+        else:
+            out[ph] = st[0]
+    return out

@@ -27,7 +27,8 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 
 from ddlb_amd.parallel.plan import (DT_BF16, DT_F16, DT_F32, DT_F64, DT_FP8, DT_SIZE, DT_U8,
-                                    OP_ALLGATHER, OP_COPY, OP_COPY_MULTI, OP_GEMM, OP_GROUP_END,
+                                    OP_ALLGATHER, OP_COPY, OP_COPY_BATCH, OP_COPY_MULTI, OP_GEMM,
+                                    OP_GROUP_END,
                                     OP_GROUP_START, OP_MEMSET, OP_NAMES, OP_NOP, OP_RECORD, OP_RECV,
                                     OP_REDUCE, OP_REDUCE_SCATTER, OP_SEND, OP_SIGNAL, OP_WAIT,
                                     OP_WAIT_SIGNAL, Plan, Ref)
@@ -53,6 +54,24 @@ class Deadlock(RuntimeError):
 
 class RaceDetected(RuntimeError):
     pass
+
+
+class RedundantOp(ValueError):
+    """A plan op that repeats the previous op of its stream exactly (same flags, same value):
+    a wasted launch / memop per run that the executor would faithfully enqueue."""
+
+
+def check_redundant(plan: Plan) -> None:
+    """Flag identical back-to-back signals on one stream (e.g. a copy-paste duplicate of an
+    arrival signal): raises :class:`RedundantOp`."""
+    last: Dict[int, object] = {}
+    for i, op in enumerate(plan.ops):
+        prev = last.get(op.stream)
+        if (op.kind == OP_SIGNAL and prev is not None and prev.kind == OP_SIGNAL
+                and prev.args == op.args):
+            raise RedundantOp(f"op {i} (stream {op.stream}) repeats the signal before it: "
+                              f"{[f'{f.buf}+{f.off}' for f in op.args['flags']]}")
+        last[op.stream] = op
 
 
 def _view(buf: torch.Tensor, off: int, count: int, dt: int) -> torch.Tensor:
@@ -82,6 +101,8 @@ class Simulator:
     def __init__(self, plans: Sequence[Plan], buffers: Sequence[Dict[str, torch.Tensor]],
                  check_races: bool = True):
         self.plans = list(plans)
+        for p in self.plans:
+            check_redundant(p)
         self.d = len(plans)
         self.bufs = list(buffers)
         self.check_races = check_races
@@ -206,7 +227,7 @@ class Simulator:
             self._touch(r, a["dst"], a["nbytes"], True, vc, what + ".dst")
             src = self._buf(r, a["src"])[a["src"].off:a["src"].off + a["nbytes"]]
             self._buf(r, a["dst"])[a["dst"].off:a["dst"].off + a["nbytes"]] = src
-        elif k == OP_COPY_MULTI:
+        elif k in (OP_COPY_MULTI, OP_COPY_BATCH):
             for (dst, src, nb) in a["segs"]:
                 self._touch(r, src, nb, False, vc, what + ".src")
                 self._touch(r, dst, nb, True, vc, what + ".dst")

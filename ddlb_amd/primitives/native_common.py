@@ -21,13 +21,19 @@ inter_stream_synchronization       serialise the per-peer transfers
 
 Native-only: ``signal`` (``stream`` = hipStreamWrite/WaitValue32 memops, ``kernel`` = tiny spin
 kernels), ``tile`` (GEMM tile or ``auto``), ``gemm_mode`` (``auto`` | ``mx`` for block-scaled fp8 |
-``blas`` = hipBLASLt for the plain GEMM ops of the plan, fused ones stay on the MFMA kernels),
+``generic``; every mode is one of our MFMA kernels: hipBLASLt stays the ``pytorch`` slot's baseline),
 ``copy_blocks`` (CU budget of the kernel protocol), ``copy_streams`` (memcpy pulls: copy streams,
 i.e. copy engines, per peer — a hedge for links faster than one engine), ``fused`` (p2p / coll: one
 arrival-flag-gated GEMM; ``reserve_cus`` = CUs its persistent form leaves free for the
 kernels that set the flags), ``graph`` (capture the plan once and replay it as one hipGraph launch;
-signal plans read a device-side run counter; not for plans with RCCL calls; ``auto`` = whenever
-capturable and the process has >= 4 HW queues), ``direction`` (columnwise ipc: ``pull`` peers' shards, or
+signal plans read a device-side run counter; not for plans with RCCL calls, copy-engine-fed
+flag-gated GEMMs or a CU split; ``auto``, the default = whenever capturable, the plan has more than
+a few ops and the process has >= 4 HW queues), ``comm_cus`` (CU budget of the communication: the
+side streams run on that many CUs via ``hipExtStreamCreateWithCUMask``, the GEMMs on the rest; 0 =
+unmasked), ``register`` (RCCL buffers allocated with ``ncclMemAlloc`` and registered with
+``ncclCommRegister`` for zero-copy transfers), ``trace`` (a roctx range per plan op, e.g.
+``gemm s3`` / ``copy p2 b1``, for ``rocprofv3 --marker-trace --kernel-rename``; also
+``DDLB_PLAN_TRACE=1``), ``direction`` (columnwise ipc: ``pull`` peers' shards, or
 ``push`` my shard into every peer's gather buffer with posted xGMI writes), ``ag_mode`` (the in-kernel
 all-gather's copy variant, csrc/gemm/gemm.h ``AgMode`` bits: 1 plain stores + release fence instead
 of write-through stores, 2 agent-scope acquire in the gated tiles, 4 16 loads in flight per lane,
@@ -55,9 +61,12 @@ COMMON_DEFAULTS = {
     "copy_streams": 1,
     "fused": False,
     "reserve_cus": 32,
-    "graph": False,
+    "graph": "auto",
     "direction": "pull",
     "ag_mode": 30,
+    "comm_cus": 0,
+    "register": False,
+    "trace": False,
 }
 COMMON_ALLOWED = {
     "backend": ["rccl", "ipc", *UCC_BACKENDS],
@@ -70,7 +79,7 @@ COMMON_ALLOWED = {
     "tile": ["auto", "pp256", "256x256", "256x128", "128x256", "128x128", "256x256w4",
              "256x128w4", "p256", "p128", "i256", "i128", "i256w4", "pi256", "pi256w4", "r256",
              "t8", "pt8", "t4", "pt4"],
-    "gemm_mode": ["auto", "mx", "generic", "blas"],
+    "gemm_mode": ["auto", "mx", "generic"],
     "copy_blocks": (1, 4096),
     "copy_streams": (1, 4),
     "fused": [True, False],
@@ -78,6 +87,9 @@ COMMON_ALLOWED = {
     "graph": [True, False, "auto"],
     "direction": ["pull", "push"],
     "ag_mode": (0, 31),
+    "comm_cus": (0, 1024),
+    "register": [True, False],
+    "trace": [True, False],
 }
 COMMON_ALIASES = {
     "backend": {"nccl": "rccl", "cuda": "ipc"},
@@ -88,7 +100,7 @@ TILE_CODE = {"auto": 0, "256x256": 1, "256x128": 2, "128x256": 3, "128x128": 4, 
              "256x256w4": 6, "256x128w4": 7, "p256": 8, "p128": 9, "i256": 10,
              "i128": 11, "i256w4": 12, "pi256": 13, "pi256w4": 14, "r256": 15, "t8": 16, "pt8": 17,
              "t4": 18, "pt4": 19}
-MODE_CODE = {"auto": 0, "generic": 1, "mx": 2, "blas": 3}
+MODE_CODE = {"auto": 0, "generic": 1, "mx": 2}
 
 
 def algo_config(options, order: str = "AG_before") -> AlgoConfig:
@@ -112,7 +124,8 @@ def algo_config(options, order: str = "AG_before") -> AlgoConfig:
         copy_blocks=int(options["copy_blocks"]), fused=bool(options["fused"]),
         reserve_cus=int(options.get("reserve_cus", 32)),
         copy_streams=int(options.get("copy_streams", 1)),
-        direction=options.get("direction", "pull"), ag_mode=int(options.get("ag_mode", 30)))
+        direction=options.get("direction", "pull"), ag_mode=int(options.get("ag_mode", 30)),
+        comm_cus=int(options.get("comm_cus", 0)), register=bool(options.get("register", False)))
 
 
 def share_cus(cfg: AlgoConfig, communicator) -> AlgoConfig:
@@ -140,14 +153,20 @@ def dtype_codes(dtype_name: str):
     return din, dout
 
 
+GRAPH_MIN_OPS = 4  # graph=auto: plans this long (host-issued signals / copies per run) replay
+
+
 def maybe_enable_graph(bound, option) -> bool:
-    """Apply the ``graph`` option to a bound plan; returns whether graph replay is on."""
+    """Apply the ``graph`` option to a bound plan; returns whether graph replay is on. ``auto``
+    replays plans whose per-run host work the graph removes (>= GRAPH_MIN_OPS ops); a
+    one-GEMM plan (world 1) stays a plain launch: a replay would add the run-counter kernel."""
     if option is True or option == "true":
         bound.enable_graph(True)
         return True
     from ddlb_amd.parallel.context import graph_replay_supported
 
-    if (option == "auto" and bound.ex.graph_capturable() and graph_replay_supported()
+    if (option == "auto" and len(bound.plan.ops) >= GRAPH_MIN_OPS
+            and bound.ex.graph_capturable() and graph_replay_supported()
             and bound.plan.meta.get("copy_streams", 1) <= 1):
         bound.enable_graph(True)
         return True

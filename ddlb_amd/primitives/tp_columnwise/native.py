@@ -41,7 +41,7 @@ class NativeTPColumnwise(TPColumnwise):
         self.plan, self.io = build_tp_columnwise(self.rank, self.world_size, self.m, self.n,
                                                  self.k, din, dout, self.cfg)
         self.ctx = self.communicator.native()
-        self.bound = self.ctx.bind(self.plan)
+        self.bound = self.ctx.bind(self.plan, trace=bool(self.options["trace"]))
         self.graph = maybe_enable_graph(self.bound, self.options["graph"])
         self.a_slot = self.bound.view(self.io.a)
         self.a_slot.copy_(self.A)

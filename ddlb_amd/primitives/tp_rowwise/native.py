@@ -33,7 +33,7 @@ class NativeTPRowwise(TPRowwise):
         self.plan, self.io = build_tp_rowwise(self.rank, self.world_size, self.m, self.n, self.k,
                                               din, dout, self.cfg)
         self.ctx = self.communicator.native()
-        self.bound = self.ctx.bind(self.plan)
+        self.bound = self.ctx.bind(self.plan, trace=bool(self.options["trace"]))
         self.graph = maybe_enable_graph(self.bound, self.options["graph"])
         self.bound.view(self.io.a).copy_(self.A)
         self.bound.view(self.io.b).copy_(self.B.t())

@@ -115,11 +115,21 @@ def test_candidate_pools():
 
     col8 = bench.candidate_pool("tp_columnwise", "bfloat16", 8)
     assert any(c[0] == "direct/ipc" for c in col8) and all(c[0][:4] != "row/" for c in col8)
+    # RCCL candidates first, the vendor slot last; no vendor-library GEMM behind "native"
+    natives = [c for c in col8 if c[1] == "native"]
+    assert natives[0][2]["backend"] == "rccl" and col8[-1][1] == "pytorch"
+    first_ipc = next(i for i, c in enumerate(natives) if c[2]["backend"] == "ipc")
+    assert all(c[2]["backend"] == "rccl" for c in natives[:first_ipc])
+    for pool in (col8, bench.candidate_pool("tp_rowwise", "bfloat16", 8),
+                 bench.candidate_pool("tp_columnwise", "bfloat16", 1)):
+        assert not any("blas" in str(c[2]) for c in pool)
     row1 = bench.candidate_pool("tp_rowwise", "bfloat16", 1)
-    assert [c[0] for c in row1] == ["row/gemm (world=1)/hip", "row/gemm (world=1)/blas"]
+    assert [c[0] for c in row1 if c[1] == "native"] == ["row/gemm (world=1)/auto",
+                                                       "row/gemm (world=1)/t4"]
     fp8 = bench.candidate_pool("tp_columnwise", "float8_e4m3fn", 1)
     labels = [c[0] for c in fp8]
-    assert "gemm (world=1)/hip/mx" in labels and not any("blas" in x for x in labels)
+    assert "gemm (world=1)/auto/mx" in labels
+    assert "compute_only(hipblaslt)" not in labels  # torch.matmul has no fp8
 
 
 class _FakeJob:
@@ -127,6 +137,9 @@ class _FakeJob:
     calls of that candidate (tuning first, then the final run)."""
 
     rank = 0
+
+    def left(self):
+        return 1e9
 
     def __init__(self, pool, script):
         self.by_opts = {json.dumps(o, sort_keys=True): lbl for lbl, _, o in pool}
@@ -139,7 +152,8 @@ class _FakeJob:
     def log(self, msg):
         pass
 
-    def measure(self, impl, opts, steps, warmup, validate, timeout, prewarm_ms=0.0):
+    def measure(self, impl, opts, steps, warmup, validate, timeout, prewarm_ms=0.0,
+                harness_iters=0):
         label = self.by_opts[json.dumps(opts, sort_keys=True)]
         self.calls.append((label, validate))
         return self.script[label].pop(0)
@@ -149,7 +163,8 @@ def _args(**kw):
     import argparse
 
     d = dict(tune_rounds=1, tune_steps=5, validate=True, candidate_timeout=10.0,
-             tune_budget_s=1e9, tune_cap_s=1e9, prewarm_ms=0.0, steps=5, warmup=1)
+             tune_budget_s=1e9, tune_cap_s=1e9, prewarm_ms=0.0, steps=5, warmup=1,
+             final_reserve_s=0.0, harness_iters=0)
     d.update(kw)
     return argparse.Namespace(**d)
 
@@ -202,3 +217,71 @@ def test_final_reports_invalid_when_nothing_validates():
     job = _FakeJob(pool, {"a": [_ok(0.5, False, "bad")]})
     cand, final = bench.final_measure(job, pool[0], [], _args(), {})
     assert cand[0] == "a" and final["valid"] is False
+
+
+def test_autotune_skips_families_failing_preflight():
+    """A candidate family whose preflight check failed is never run; the vendor slot never
+    becomes the headline while a native candidate succeeded."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    pool = [("r", "native", {"backend": "rccl"}),
+            ("i", "native", {"backend": "ipc", "multicast_protocol": "kernel"}),
+            ("v", "pytorch", {"backend": "nccl"})]
+    job = _FakeJob(pool, {"r": [_ok(0.9)], "v": [_ok(0.5)]})
+    tune = {}
+    pre = {"rccl": "ok (3 ms)", "ipc": "ok", "ipc_kernel": "failed: timeout",
+           "torch_nccl": "ok"}
+    chosen, fallbacks = bench.autotune(job, pool, _args(), 8, tune, pre)
+    assert chosen[0] == "r" and [c[0] for c in fallbacks] == ["v"]
+    assert tune["i"].startswith("skipped (ipc_kernel")
+    assert [c for c, _ in job.calls] == ["r", "v"]
+
+
+def test_autotune_drops_family_after_two_timeouts():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    pool = [(f"i{j}", "native", {"backend": "ipc", "multicast_protocol": "memcpy", "j": j})
+            for j in range(4)] + [("r", "native", {"backend": "rccl"})]
+    to = {"ok": False, "error": "timeout after 45s"}
+    job = _FakeJob(pool, {"i0": [to], "i1": [to], "r": [_ok(1.0)]})
+    tune = {}
+    chosen, _ = bench.autotune(job, pool, _args(), 8, tune, {})
+    assert chosen[0] == "r"
+    assert "timed out twice" in tune["i2"] and "timed out twice" in tune["i3"]
+
+
+def test_deadline_stops_tuning_and_final():
+    """No time left before the deadline: tuning skips, the final run is not started."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    pool = [("a", "native", {"x": 1}), ("b", "native", {"x": 2})]
+    job = _FakeJob(pool, {"a": [_ok(1.0)]})
+    job.left = lambda: 35.0 if job.calls else 1e9  # 35 - 30 reserved < 10 s
+    tune = {}
+    chosen, _ = bench.autotune(job, pool, _args(final_reserve_s=30.0), 2, tune)
+    assert chosen[0] == "a" and tune["b"].startswith("skipped (deadline")
+    job.left = lambda: 12.0
+    cand, final = bench.final_measure(job, chosen, [], _args(), tune)
+    assert final is None and "deadline" in tune["final_rejected"][0]
+
+
+def test_bench_world2_cpu_preflight_fields():
+    """The JSON line names the timing mode, the preflight outcome and the vendor time; a
+    scripted preflight failure of a family is reported (DDLB_PREFLIGHT_FAKE)."""
+    from conftest import free_port
+
+    env = _env()
+    env["DDLB_PREFLIGHT_FAKE"] = json.dumps({"torch_nccl": "ok", "rccl": "ok",
+                                             "ipc": "failed: scripted"})
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", *ARGS]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    d = _json_line(r.stdout)
+    assert d["preflight"]["ipc"] == "failed: scripted"
+    assert d["timing"].startswith("cpu_clock window")
+    assert d["harness_mean_ms"] > 0 and d["max_err"] <= d["err_bound"]

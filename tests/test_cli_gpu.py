@@ -30,7 +30,7 @@ def test_cli_every_slot_world1(tmp_path, primitive):
 
     out = tmp_path / "res_{timestamp}.csv"
     impls = ["native;algorithm=default,coll_pipeline,p2p_pipeline;s=2",
-             "native;gemm_mode=blas", "fuser;algorithm=coll_pipeline;s=2",
+             "native;gemm_mode=generic", "fuser;algorithm=coll_pipeline;s=2",
              "transformer_engine", "pytorch;empty_cache=false",
              "compute_only;size=unsharded"]
     if primitive == "tp_columnwise":

@@ -248,46 +248,16 @@ def test_ring_grouped_rows(gen):
     assert torch.count_nonzero(C[~mask].float()) == 0
 
 
-@pytest.mark.parametrize("dt", [(torch.bfloat16, torch.bfloat16), (torch.bfloat16, torch.float32),
-                                (torch.float16, torch.float16), (torch.float32, torch.float32)],
-                         ids=lambda d: f"{str(d[0])[6:]}-{str(d[1])[6:]}")
-def test_blas_mode(dt, gen):
-    """gemm_mode=blas: hipBLASLt for plain GEMMs; grouped-row (pipeline stage) addressing falls
-    back to the MFMA kernels — same contract either way."""
-    from ddlb_amd.ops.gemm import gemm
+def test_no_vendor_mode(gen):
+    """The native GEMM never dispatches to a vendor library: an unknown mode (the former
+    hipBLASLt mode 3) is refused by the launcher, not silently routed anywhere."""
+    from ddlb_amd.ops import load
 
-    din, dout = dt
-    M, N, K = 1024, 768, 512
-    a, w = _rand((M, K), din, gen), _rand((N, K), din, gen)
-    out = gemm(a, w, out_dtype=dout, mode="blas")
-    torch.cuda.synchronize()
-    torch.testing.assert_close(out.float(), _ref(a, w), rtol=0, atol=_tol(din, K))
-    # grouped rows (pipeline stage addressing): rows j*blk.. of each of d blocks
-    d, blk, j = 4, 128, 1
-    A = _rand((d * 512, K), din, gen)
-    C = torch.zeros((d * 512, N), dtype=dout, device=DEV)
-    gemm(A[j * blk:], w, C[j * blk:], M=d * blk, a_grp=blk, a_gstride=512, c_grp=blk,
-         c_gstride=512, mode="blas")
-    torch.cuda.synchronize()
-    ref = _ref(A, w)
-    for r in range(d):
-        rows = slice(r * 512 + j * blk, r * 512 + (j + 1) * blk)
-        torch.testing.assert_close(C[rows].float(), ref[rows], rtol=0, atol=_tol(din, K))
-
-
-def test_blas_mode_falls_back_for_fused(gen):
-    """Fused epilogues / fp8 are not sent to the library: the MFMA kernels still run them."""
-    from ddlb_amd.ops.gemm import gemm
-    from ddlb_amd.parallel.sim import apply_act
-
-    a, w = _rand((512, 256), torch.bfloat16, gen), _rand((512, 256), torch.bfloat16, gen)
-    out = gemm(a, w, mode="blas", act="relu")
-    torch.cuda.synchronize()
-    torch.testing.assert_close(out.float(), apply_act(_ref(a, w), 2), rtol=0.02, atol=0.05)
-    a8, w8 = _rand((512, 256), torch.float8_e4m3fn, gen), _rand((256, 256), torch.float8_e4m3fn, gen)
-    out8 = gemm(a8, w8, mode="blas")
-    torch.cuda.synchronize()
-    torch.testing.assert_close(out8.float(), _ref(a8, w8), rtol=0, atol=_tol(torch.float8_e4m3fn, 256))
+    a, w = _rand((256, 256), torch.bfloat16, gen), _rand((256, 256), torch.bfloat16, gen)
+    out = torch.empty((256, 256), dtype=torch.bfloat16, device=DEV)
+    with pytest.raises(RuntimeError):
+        load().gemm(a.data_ptr(), w.data_ptr(), out.data_ptr(), 256, 256, 256, 256, 256, 256,
+                    2, 2, 0, 3, 0, 0, 0, 0, torch.cuda.current_stream().cuda_stream, 0)
 
 
 @pytest.mark.parametrize("tile", ["t8", "pt8", "t4", "pt4"])

@@ -162,3 +162,54 @@ def test_direct_access_without_ack_is_a_race():
     with pytest.raises((RaceDetected, Deadlock)):
         for _ in range(3):
             sim.run_epoch()
+
+
+def test_redundant_back_to_back_signal_is_flagged():
+    """Two identical signals in a row on one stream (the copy-paste duplicate ADVICE r2 found in
+    the kernel-protocol pull) are rejected by the simulator instead of silently costing a launch
+    per run."""
+    from ddlb_amd.parallel.plan import Plan, Ref
+    from ddlb_amd.parallel.sim import RedundantOp, Simulator, make_buffers
+
+    plan = Plan(0, 1, nstreams=2)
+    plan.buffer("flags", 256, symmetric=True, zero=True)
+    f = [Ref("flags", 0)]
+    plan.signal(1, f)
+    plan.signal(0, f)      # another stream: fine
+    plan.signal(1, f, delta=1)  # different value: fine
+    Simulator([plan], make_buffers([plan]))
+    plan.signal(1, f, delta=1)
+    with pytest.raises(RedundantOp):
+        Simulator([plan], make_buffers([plan]))
+
+
+def test_no_bench_plan_has_redundant_signals():
+    from ddlb_amd.parallel.algorithms import AlgoConfig, build_tp_columnwise
+    from ddlb_amd.parallel.plan import DT_BF16
+    from ddlb_amd.parallel.sim import check_redundant
+
+    for proto in ("memcpy", "batch_memcpy", "kernel"):
+        for alg in ("default", "coll_pipeline", "p2p_pipeline"):
+            for fused in (False, True):
+                cfg = AlgoConfig(algorithm=alg, backend="ipc", protocol=proto, s=2, fused=fused)
+                try:
+                    plan, _ = build_tp_columnwise(0, 4, 2048, 256, 256, DT_BF16, DT_BF16, cfg)
+                except ValueError:
+                    continue
+                check_redundant(plan)
+
+
+def test_plan_labels_name_stages():
+    from ddlb_amd.parallel.algorithms import AlgoConfig, build_tp_columnwise
+    from ddlb_amd.parallel.plan import DT_BF16
+
+    plan, _ = build_tp_columnwise(0, 2, 1024, 64, 64, DT_BF16, DT_BF16,
+                                  AlgoConfig(algorithm="coll_pipeline", backend="ipc", s=2))
+    labels = plan.labels()
+    assert len(labels) == len(plan.ops)
+    assert "gemm s0" in labels and "gemm s1" in labels
+    assert "copy p1 b0" in labels and "copy p1 b1" in labels
+    assert any(x.startswith("wait_signal flags+") for x in labels)
+    plan, _ = build_tp_columnwise(0, 2, 1024, 64, 64, DT_BF16, DT_BF16,
+                                  AlgoConfig(algorithm="coll_pipeline", backend="rccl", s=2))
+    assert {"allgather #0", "allgather #1"} <= set(plan.labels())

@@ -49,19 +49,6 @@ def test_native_world1(comm, alg, backend, dtype):
         impl.close()
 
 
-@pytest.mark.parametrize("alg", ["default", "coll_pipeline", "p2p_pipeline"])
-def test_native_blas_world1(comm, alg):
-    from ddlb_amd.primitives.tp_columnwise.native import NativeTPColumnwise
-    from ddlb_amd.primitives.tp_rowwise.native import NativeTPRowwise
-
-    for cls in (NativeTPColumnwise, NativeTPRowwise):
-        impl = cls(m=2048, n=512, k=512, dtype="bfloat16", algorithm=alg, s=2, gemm_mode="blas")
-        out = impl.run()
-        torch.cuda.synchronize()
-        impl.validate(out)
-        impl.close()
-
-
 @pytest.mark.parametrize("dtype", ["bfloat16", "float8_e4m3fn", "float32"])
 def test_native_direct_world1(comm, dtype):
     from ddlb_amd.primitives.tp_columnwise.native import NativeTPColumnwise
@@ -175,8 +162,6 @@ def _ipc_cfgs():
             ("col/coll/kernel/graph", "col", dict(algorithm="coll_pipeline", s=2,
                                                   multicast_protocol="kernel")),
             ("col/p2p/memcpy/graph", "col", dict(algorithm="p2p_pipeline")),
-            ("col/p2p/fused/graph", "col", dict(algorithm="p2p_pipeline", fused=True)),
-            ("col/coll/fused/graph", "col", dict(algorithm="coll_pipeline", s=2, fused=True)),
             ("col/coll/agk/graph", "col", dict(algorithm="coll_pipeline", s=2, fused=True,
                                                multicast_protocol="kernel", copy_blocks=8)),
             ("col/direct/graph", "col", dict(algorithm="direct")),
@@ -190,9 +175,6 @@ def _ipc_cfgs():
     for alg in ("default", "coll_pipeline", "p2p_pipeline"):  # pulls split over 2 copy streams
         cfgs.append((f"col/{alg}/memcpy/cs2", "col", dict(algorithm=alg, backend="ipc", s=2,
                                                           copy_streams=2)))
-    for alg in ("default", "coll_pipeline", "p2p_pipeline"):  # bench.py's "/blas" candidates
-        cfgs.append((f"col/{alg}/ipc/blas", "col", dict(algorithm=alg, backend="ipc", s=2,
-                                                        gemm_mode="blas")))
     return cfgs
 
 
@@ -261,6 +243,57 @@ def test_graph_replay_world1(comm, prim):
     impl.close()
 
 
+def test_fused_copy_engine_plans_are_not_captured():
+    """A flag-gated GEMM whose flags copy streams set is never graph-captured (a replay could
+    queue its spinning tiles ahead of the copies; ordering it after them serialises the
+    pipeline); graph=auto leaves such a plan eager, graph=True refuses it. The
+    in-kernel all-gather (the gate's flags set by the same launch) still captures."""
+    from ddlb_amd.parallel.algorithms import AlgoConfig, build_tp_columnwise
+    from ddlb_amd.parallel.plan import DT_BF16
+    from ddlb_amd.ops import load
+
+    C = load()
+    for alg, proto, ok in (("p2p_pipeline", "memcpy", False), ("coll_pipeline", "memcpy", False),
+                           ("coll_pipeline", "kernel", True)):
+        plan, _ = build_tp_columnwise(0, 2, 1024, 256, 256, DT_BF16, DT_BF16,
+                                      AlgoConfig(algorithm=alg, backend="ipc", fused=True, s=2,
+                                                 protocol=proto, copy_blocks=8))
+        ex = C.PlanExecutor(0, plan.nstreams, max(plan.nevents, 1), list(plan.stream_priority))
+        ex.load(plan.encode(lambda ref: 4096))
+        assert ex.graph_capturable() == ok, (alg, proto)
+
+
+def test_copy_batch_moves_every_segment():
+    """multicast_protocol=batch_memcpy submits every peer's block as ONE hipMemcpyBatchAsync when
+    the HIP runtime has it (torch's HIP 7.0 does not: then one hipMemcpyAsync per segment on the
+    same stream); either way every byte lands."""
+    from ddlb_amd.ops import load
+
+    C = load()
+    sizes = [(1 << 20) + 16 * i for i in range(5)]
+    srcs = [torch.randint(0, 255, (n,), dtype=torch.uint8, device="cuda") for n in sizes]
+    dsts = [torch.zeros_like(x) for x in srcs]
+    C.copy_batch([(d.data_ptr(), s.data_ptr(), s.numel()) for d, s in zip(dsts, srcs)],
+                 torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    for d, s in zip(dsts, srcs):
+        assert torch.equal(d, s)
+    print(f"hipMemcpyBatchAsync available: {C.copy_batch_api_available()}")
+
+
+def test_plan_trace_ranges(comm):
+    """trace=True: every op's enqueue inside a roctx range named by Plan.labels() (the stage
+    names rocprofv3 --kernel-rename gives the kernels); the run itself is unchanged."""
+    from ddlb_amd.primitives.tp_columnwise.native import NativeTPColumnwise
+
+    impl = NativeTPColumnwise(m=2048, n=512, k=512, dtype="bfloat16", algorithm="coll_pipeline",
+                              s=4, trace=True)
+    out = impl.run()
+    torch.cuda.synchronize()
+    impl.validate(out)
+    impl.close()
+
+
 def test_signal_plans_are_graph_capturable():
     """Cross-process signal / wait plans can be captured: in graph mode their epoch-dependent
     values come from a device-side run counter (the replay itself is exercised by the IPC
@@ -302,12 +335,15 @@ def test_copy_multi_segments(nseg, max_blocks):
         assert torch.equal(d, s)
 
 
-@pytest.mark.parametrize("graph", [False, True])
-def test_rccl_data_plane_world1(comm, graph):
+@pytest.mark.parametrize("mode", ["plain", "graph", "register", "cumask", "register+cumask"])
+def test_rccl_data_plane_world1(comm, mode):
     """Our own RCCL communicator (csrc/comm) driven by the plan executor on its own stream:
     all-gather, reduce-scatter and a grouped send/recv to self, then a GEMM ordered after them
     by an event. At world 1 the collectives are copies, but the linkage, ncclCommInitRank from
-    a unique id, dtype mapping and stream/event plumbing are the ones the N>1 plans use."""
+    a unique id, dtype mapping and stream/event plumbing are the ones the N>1 plans use.
+    ``register``: the RCCL buffers come from ncclMemAlloc and are ncclCommRegister'ed;
+    ``cumask``: RCCL's stream on 32 CUs (hipExtStreamCreateWithCUMask), the GEMM on the rest."""
+    graph = mode == "graph"
     from ddlb_amd.parallel.context import NativeContext
     from ddlb_amd.parallel.plan import DT_BF16, DT_F32, Plan
 
@@ -330,9 +366,15 @@ def test_rccl_data_plane_world1(comm, graph):
     plan.record(1, e)
     plan.wait(0, e)
     plan.gemm(0, a, bt, c, M=256, N=128, K=128, lda=128, ldb=128, ldc=128, din=DT_BF16,
-              dout=DT_F32)
+              dout=DT_F32, reserve_cus=32 if "cumask" in mode else 0)
+    plan.meta.update(register="register" in mode, comm_cus=32 if "cumask" in mode else 0)
     ctx = NativeContext(comm)
     bound = ctx.bind(plan)
+    if "register" in mode:
+        assert set(bound.rmem) == {"src", "ag", "rs", "rv"}
+        assert all(m.registered for m in bound.rmem.values())
+    if "cumask" in mode:
+        assert bound.ex.cu_split() == 32 and not bound.ex.graph_capturable()
     if graph:  # RCCL plans are not captured (replaying captured RCCL calls crashed here)
         assert not bound.ex.graph_capturable()
         with pytest.raises(RuntimeError):
@@ -515,11 +557,11 @@ def test_in_kernel_allgather_world1(comm, graph, mode):
     ctx.close()
 
 
-@pytest.mark.parametrize("tile,mode", [(0, 0), (18, 0), (4, 0), (0, 3)])
+@pytest.mark.parametrize("tile,mode", [(0, 0), (18, 0), (4, 0)])
 def test_direct_store_gemm_world1(comm, tile, mode):
     """Direct-store C (c_shards): row block q of one GEMM lands in its own buffer (the peers'
     receive slots in the rowwise p2p plan), tiles dispatched shard-interleaved (tile_order=2).
-    Every kernel family that can take it (pt4 auto, t4, 128x128; blas falls back to MFMA)."""
+    Every kernel family that can take it (pt4 auto, t4, 128x128)."""
     from ddlb_amd.parallel.context import NativeContext
     from ddlb_amd.parallel.plan import DT_BF16, Plan
 
@@ -548,3 +590,25 @@ def test_direct_store_gemm_world1(comm, tile, mode):
             torch.testing.assert_close(out, ref[q * rows:(q + 1) * rows], rtol=0, atol=1e-3 * K)
     bound.close()
     ctx.close()
+
+
+def test_bench_preflight_shared_gpu():
+    """bench.py's N>1 preflight with 2 ranks sharing this GPU: every IPC check (stream and kernel
+    handshakes, CU-copy / copy-engine pulls, copy-engine push) passes; the RCCL checks fail as
+    they must here (RCCL refuses two ranks on one device) and are reported, not hung."""
+    from conftest import free_port
+
+    env = dict(os.environ, DDLB_ALLOW_SHARED_GPU="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "DDLB_CHILD_INIT_METHOD"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--preflight-only",
+           "--preflight-timeout", "60"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert lines, (r.stdout[-2000:], r.stderr[-4000:])
+    pre = json.loads(lines[0])["preflight"]
+    for ph in ("ipc", "ipc_ksig", "ipc_kernel", "ipc_sdma", "ipc_push"):
+        assert pre[ph].startswith("ok"), (ph, pre, r.stderr[-3000:])
+    assert set(pre) >= {"rccl", "torch_nccl"}

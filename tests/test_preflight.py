@@ -1,0 +1,79 @@
+"""Multi-GPU preflight plans on the CPU simulator (d simulated ranks, byte-exact, race-checked):
+the checks bench.py runs before an N>1 job must themselves be correct and deadlock-free, or a
+healthy node would be reported broken."""
+
+import pytest
+import torch
+
+from ddlb_amd.parallel import preflight as pf
+from ddlb_amd.parallel.sim import Simulator, make_buffers
+
+NB = 4096
+
+
+@pytest.mark.parametrize("d", [2, 3, 4, 8])
+@pytest.mark.parametrize("phase", pf.IPC_PHASES)
+def test_ipc_plan_moves_every_peers_pattern(d, phase):
+    plans = [pf.build_ipc_plan(r, d, phase, NB) for r in range(d)]
+    bufs = make_buffers(plans)
+    sim = Simulator(plans, bufs, check_races=True)
+    for ep in (1, 2):
+        for r in range(d):
+            bufs[r]["X"].view(torch.int32)[:] = pf.pattern(r, NB, ep)
+            bufs[r]["R"].view(torch.int32).fill_(-1)
+        sim.run_epoch()
+        if phase in ("ipc_kernel", "ipc_sdma", "ipc_push"):
+            for r in range(d):
+                rv = bufs[r]["R"].view(torch.int32)
+                for p in range(d):
+                    if p != r:
+                        assert torch.equal(rv[p * NB // 4:(p + 1) * NB // 4],
+                                           pf.pattern(p, NB, ep)), (r, p, ep)
+        # every flag word ends at this epoch: the handshakes completed
+        for r in range(d):
+            flags = bufs[r]["flags"].view(torch.int32)
+            assert int(flags[d:2 * d].sum()) == ep * (d - 1)  # ACKs from every peer
+
+
+def test_pattern_differs_per_owner_and_epoch():
+    a, b, c = pf.pattern(0, NB, 1), pf.pattern(1, NB, 1), pf.pattern(0, NB, 2)
+    assert not torch.equal(a, b) and not torch.equal(a, c)
+    assert int((a == b).sum()) == 0
+
+
+@pytest.mark.parametrize("d", [2, 4, 8])
+def test_rccl_plan(d):
+    plans = [pf.build_rccl_plan(r, d, NB, 256) for r in range(d)]
+    bufs = make_buffers(plans)
+    for r in range(d):
+        bufs[r]["SEND"].view(torch.int32)[:] = pf.pattern(r, NB, 1)
+        bufs[r]["RSIN"].view(torch.float32)[:] = pf.rs_input(r, d, 256)
+    Simulator(plans, bufs, check_races=True).run_epoch()
+    for r in range(d):
+        ag = bufs[r]["AG"].view(torch.int32)
+        for q in range(d):
+            assert torch.equal(ag[q * NB // 4:(q + 1) * NB // 4], pf.pattern(q, NB, 1))
+        assert torch.equal(bufs[r]["RSOUT"].view(torch.float32), pf.rs_expected(r, d, 256))
+
+
+def test_needs_maps_candidates_to_checks():
+    assert pf.needs("pytorch", {}) == ["torch_nccl"]
+    assert pf.needs("native", {"backend": "rccl"}) == ["rccl"]
+    assert pf.needs("native", {"backend": "ipc", "multicast_protocol": "memcpy"}) == \
+        ["ipc", "ipc_sdma"]
+    agk = pf.needs("native", {"backend": "ipc", "multicast_protocol": "kernel", "fused": True,
+                              "graph": True})
+    assert agk == ["ipc", "ipc_ksig", "ipc_kernel"]
+    assert "ipc_kernel" in pf.needs("native", {"backend": "ipc", "algorithm": "direct"})
+    assert "ipc_push" in pf.needs("native", {"backend": "ipc", "direction": "push"})
+    assert pf.needs("compute_only", {}) == []
+
+
+def test_merge_over_ranks():
+    per_rank = [{"ipc": "ok (3 ms)", "ipc_sdma": "ok"},
+                {"ipc": "ok (4 ms)", "ipc_sdma": "failed: AssertionError: 3 words differ"},
+                {"ipc": "ok (2 ms)"}]
+    m = pf.merge(per_rank, ("ipc", "ipc_sdma", "ipc_kernel"))
+    assert m["ipc"].startswith("ok")
+    assert m["ipc_sdma"].startswith("failed: AssertionError")
+    assert m["ipc_kernel"] == "failed: timeout"
