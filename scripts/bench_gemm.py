@@ -56,6 +56,7 @@ def main():
     p.add_argument("--modes", default="auto")
     p.add_argument("--shapes", default="all")
     p.add_argument("--json", default=None)
+    p.add_argument("--check", action="store_true", help="tight numerics check first")
     a = p.parse_args()
     dt = getattr(torch, a.dtype)
     g = torch.Generator(device="cuda")
@@ -80,10 +81,25 @@ def main():
                 print("scaled_mm unavailable:", e)
         else:
             variants["hipblaslt"] = lambda: torch.matmul(A, Bkn, out=out)
+            # the K-contiguous weight layout (te.Linear / F.linear), hipBLASLt's fastest form
+            variants["hipblaslt_linear"] = lambda: torch.nn.functional.linear(A, W)
         for t in a.tiles.split(","):
             for mode in a.modes.split(","):
                 variants[f"native[{t},{mode}]"] = (lambda t=t, mode=mode: gemm(A, W, out, tile=t,
                                                                                mode=mode))
+        if a.check:  # tight numerics of every native variant before timing it
+            ref = A.float() @ W.float().t()
+            bound = 2.0 ** -7 * float(ref.abs().max()) + K * 2.0 ** -12
+            for k, fn in variants.items():
+                if not k.startswith("native"):
+                    continue
+                out.fill_(float("nan"))
+                fn()
+                torch.cuda.synchronize()
+                err = float((out.float() - ref).abs().max())
+                print(f"  check {k:24s} max|err| {err:.4g} (bound {bound:.4g}) "
+                      f"{'ok' if err <= bound else 'FAIL'}")
+            del ref
         times = {k: [] for k in variants}
         for _ in range(a.rounds):
             for k, fn in variants.items():

@@ -16,9 +16,8 @@ def main():
     p.add_argument("-n", type=int, default=1024)
     p.add_argument("-k", type=int, default=1024)
     p.add_argument("--tiles", default="256x256,pp256,128x128")
-    p.add_argument("--hipblaslt", action="store_true", help="also torch.matmul")
-    p.add_argument("--blas", action="store_true",
-                   help="also our hipBLASLt path (per-shape algorithm autotune)")
+    p.add_argument("--hipblaslt", action="store_true",
+                   help="also the vendor GEMM (F.linear: hipBLASLt, K-contiguous weight)")
     p.add_argument("--iters", type=int, default=20)
     a = p.parse_args()
     g = torch.Generator(device="cuda")
@@ -29,13 +28,9 @@ def main():
     for t in [t for t in a.tiles.split(",") if t]:
         for _ in range(a.iters):
             gemm(A, W, out, tile=t)
-    if a.blas:
-        for _ in range(a.iters):
-            gemm(A, W, out, mode="blas")
     if a.hipblaslt:
-        Bkn = W.t().contiguous()
         for _ in range(a.iters):
-            torch.matmul(A, Bkn, out=out)
+            torch.nn.functional.linear(A, W)
     torch.cuda.synchronize()
 
 
