@@ -24,6 +24,8 @@ import json
 import os
 import queue as _queue
 import socket
+import subprocess
+import sys
 import time
 import traceback
 from typing import Any, Dict, List, Optional
@@ -235,9 +237,16 @@ class PrimitiveBenchmarkRunner:
                  output_csv: Optional[str] = None, time_measurement_backend: str = "cpu_clock",
                  barrier_at_each_iteration: bool = True, profile_iterations: int = 5,
                  child_timeout_s: float = 1800.0, resume: bool = False, isolate: bool = True,
-                 validate_every_iteration: bool = False):
+                 validate_every_iteration: bool = False, pmc=None,
+                 pmc_dir: str = "results/pmc"):
         if primitive not in self.ALLOWED_PRIMITIVES:
             raise ValueError(f"Unknown primitive: {primitive}")
+        from ddlb_amd.utils import pmc as pmc_mod
+
+        self.pmc = pmc_mod.parse(pmc)
+        if self.pmc:
+            pmc_mod.check_limits(self.pmc)  # before any launch: an over-full pass hangs
+        self.pmc_dir = pmc_dir
         self.primitive = primitive
         self.m, self.n, self.k = int(m), int(n), int(k)
         self.implementations = list(implementations)
@@ -305,9 +314,47 @@ class PrimitiveBenchmarkRunner:
                           r.get("world_size")))
         return keys
 
+    def _run_child_pmc(self, impl_id: str, init: str, kwargs: Dict[str, Any]) -> Dict[str, Any]:
+        """The child as a fresh program under ``rocprofv3 --pmc ... --selected-regions``: the
+        counters cover the profiler window (``profile_iterations`` run() calls); their
+        per-kernel means come back in the row's ``pmc`` column."""
+        from ddlb_amd.utils import pmc as pmc_mod
+
+        tag = f"{self.primitive}_{self.m}x{self.n}x{self.k}_{impl_id}_rank{get_rank()}"
+        out_dir = os.path.abspath(os.path.join(self.pmc_dir, tag))
+        os.makedirs(out_dir, exist_ok=True)
+        jin, jout = os.path.join(out_dir, "kwargs.json"), os.path.join(out_dir, "row.json")
+        with open(jin, "w") as f:
+            json.dump(kwargs, f)
+        if os.path.exists(jout):
+            os.remove(jout)
+        env = dict(os.environ, DDLB_CHILD_INIT_METHOD=init)
+        cmd = pmc_mod.rocprof_cmd(self.pmc, out_dir) + [
+            sys.executable, "-m", "ddlb_amd.benchmark", "--worker", jin, jout]
+        proc = subprocess.Popen(cmd, env=env)
+        try:
+            proc.wait(timeout=self.child_timeout_s)
+        except subprocess.TimeoutExpired:
+            proc.kill()
+            proc.wait()
+            return {"valid": False, "error": f"child timed out after {self.child_timeout_s:.0f}s",
+                    "pmc": ""}
+        if not os.path.exists(jout):
+            return {"valid": False, "error": f"profiled child exited with code {proc.returncode}",
+                    "pmc": ""}
+        with open(jout) as f:
+            row = json.load(f)
+        try:
+            row["pmc"] = json.dumps(pmc_mod.summarize(out_dir), sort_keys=True)
+        except Exception as e:  # the measurement stands without counters
+            row["pmc"] = f"unavailable: {type(e).__name__}: {e}"
+        return row
+
     def _run_child(self, impl_id: str) -> Dict[str, Any]:
         init = self._next_init_method()
         kwargs = self._kwargs(impl_id)
+        if self.pmc:
+            return self._run_child_pmc(impl_id, init, kwargs)
         if not self.isolate:
             os.environ["DDLB_CHILD_INIT_METHOD"] = init
             try:
@@ -436,3 +483,30 @@ class PrimitiveBenchmarkRunner:
         fig.savefig(path)
         plt.close(fig)
         return path
+
+
+def _worker_main(argv: List[str]) -> int:
+    """``python -m ddlb_amd.benchmark --worker KWARGS.json ROW.json``: one benchmark child as a
+    standalone program (the form a profiler launcher can wrap)."""
+    if len(argv) != 3 or argv[0] != "--worker":
+        raise SystemExit("usage: python -m ddlb_amd.benchmark --worker KWARGS.json ROW.json")
+    with open(argv[1]) as f:
+        kwargs = json.load(f)
+    try:
+        row = run_single(**kwargs)
+    except Exception as e:
+        row = {"error": f"{type(e).__name__}: {e}", "valid": False}
+    finally:
+        try:
+            from ddlb_amd.communicator import Communicator
+
+            Communicator.reset()
+        except Exception:
+            pass
+    with open(argv[2], "w") as f:
+        json.dump(row, f, default=str)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(_worker_main(sys.argv[1:]))

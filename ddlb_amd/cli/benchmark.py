@@ -74,7 +74,8 @@ def run_benchmark(config: Dict[str, Any], isolate: bool = True, plot: bool = Fal
             profile_iterations=int(bench["profile_iterations"]),
             child_timeout_s=float(bench["child_timeout_s"]), resume=bool(bench["resume"]),
             isolate=isolate, validate_every_iteration=bool(bench.get("validate_every_iteration",
-                                                                     False)))
+                                                                     False)),
+            pmc=bench.get("pmc"), pmc_dir=bench.get("pmc_dir") or "results/pmc")
         df = runner.run()
         if plot and rank == 0 and len(df):
             runner.plot_results(df, path=os.path.splitext(csv_path)[0] + f"_{mm}x{kk}x{nn}.png")
@@ -120,6 +121,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--validate-every-iteration", action="store_true",
                    help="debug/race screen: validate every timed iteration")
     p.add_argument("--plot", action="store_true", help="save a bar chart next to the CSV")
+    p.add_argument("--pmc", default=None,
+                   help="comma list of hardware counters (or 'default') collected by rocprofv3 "
+                        "over the 5-iteration profiler window of every child; per-kernel means "
+                        "land in the CSV's pmc column (one pass: <= 8 SQ, 4 TCC, 2 GRBM, ...)")
+    p.add_argument("--pmc-dir", default="results/pmc", help="rocprofv3 output directory root")
     return p
 
 
@@ -146,6 +152,7 @@ def main(argv: Optional[List[str]] = None) -> None:
         "barrier_at_each_iteration": args.barrier, "profile_iterations": args.profile_iterations,
         "child_timeout_s": args.child_timeout, "resume": args.resume,
         "validate_every_iteration": args.validate_every_iteration,
+        "pmc": args.pmc, "pmc_dir": args.pmc_dir,
     }}
     run_benchmark(config, isolate=not args.no_isolate, plot=args.plot)
 

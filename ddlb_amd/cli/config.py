@@ -29,6 +29,8 @@ DEFAULTS: Dict[str, Any] = {
     "output_csv": None,
     "profile_iterations": 5,      # reference hard-codes the 5-iteration profiler window
     "child_timeout_s": 1800.0,
+    "pmc": None,                  # opt-in rocprofv3 counters over the profiler window (utils/pmc)
+    "pmc_dir": "results/pmc",
     "resume": False,
 }
 

@@ -103,6 +103,8 @@ class NativeContext:
         if not communicator.is_gpu:
             raise RuntimeError("the native data plane needs a ROCm GPU")
         self.C = load()
+        if os.environ.get("DDLB_CRASH_BT", "0") == "1":
+            self.C.install_crash_handler()  # native frames on SIGSEGV / SIGABRT (diagnostics)
         self.comm = communicator
         self.rank = communicator.rank
         self.world = communicator.world_size
@@ -261,7 +263,8 @@ class BoundPlan:
                 "hipGraph replay needs at least 4 hardware queues per process: with "
                 f"GPU_MAX_HW_QUEUES={os.environ.get('GPU_MAX_HW_QUEUES')} the HIP runtime of this "
                 "image crashes in hipGraphLaunch (profiles/r02/r2_17_*)")
-        if on and self.plan.meta.get("copy_streams", 1) > 1:
+        if (on and self.plan.meta.get("copy_streams", 1) > 1
+                and os.environ.get("DDLB_GRAPH_CS2", "0") != "1"):  # diagnostic override
             raise RuntimeError(
                 "hipGraph replay: plans with copy_streams > 1 (one peer's pulls split over several "
                 "copy streams) segfaulted in this HIP runtime (profiles/r02/r2_22_cs2_graph.txt); "

@@ -21,7 +21,7 @@ CSV_COLUMNS: List[str] = [
     "dtype", "Throughput (TFLOPS)", "Throughput std (TFLOPS)", "world_size", "hostname",
     "time_measurement_backend", "barrier_at_each_iteration", "option", "valid",
 ]
-EXTRA_COLUMNS: List[str] = ["per_gpu_tflops", "algbw_GBps", "gpu_arch", "error"]
+EXTRA_COLUMNS: List[str] = ["per_gpu_tflops", "algbw_GBps", "gpu_arch", "error", "pmc"]
 
 SUMMARY_COLUMNS = ["m", "n", "k", "config", "Throughput (TFLOPS)", "Throughput std (TFLOPS)",
                    "mean_time (ms)", "std_time", "min_time", "max_time"]

@@ -332,3 +332,30 @@ def test_t8_mx_fp8(tile, shape, gen):
     again = gemm(a, w, mode="mx", tile=tile)
     torch.cuda.synchronize()
     assert torch.equal(out, again)
+
+
+def _tight_bound(ref, k):
+    """max|err| <= 2^-7 max|ref| + k 2^-12: output rounding plus f32 accumulation fit far inside;
+    one dropped 16-byte K chunk per tile (error sigma ~0.9, max ~5 at k = 8192) does not — the
+    reference's atol = 1e-3 k (8.2 at k = 8192) would let that through."""
+    return 2.0 ** -7 * float(ref.abs().max()) + k * 2.0 ** -12
+
+
+@pytest.mark.parametrize("tile", ["auto", "pt4", "t4", "t8", "pt8", "r256", "i256", "pi256",
+                                  "256x256", "128x128"])
+@pytest.mark.parametrize("dt", [(torch.bfloat16, "auto"), (torch.float16, "auto"),
+                                (torch.float8_e4m3fn, "mx"), (torch.float8_e4m3fn, "auto")],
+                         ids=lambda d: f"{str(d[0])[6:]}-{d[1]}")
+def test_gemm_long_k_tight(dt, tile, gen):
+    """Every fast kernel at K = 8192 (the long-K shapes of BASELINE configs #2-#4) against the
+    tight bound, with 512 x 512 outputs (several tiles, both wave groups, every K-tile kind)."""
+    from ddlb_amd.ops.gemm import gemm
+
+    dtype, mode = dt
+    M, N, K = 512, 512, 8192
+    a, w = _rand((M, K), dtype, gen), _rand((N, K), dtype, gen)
+    out = gemm(a, w, tile=tile, mode=mode)
+    torch.cuda.synchronize()
+    ref = _ref(a, w)
+    err = float((out.float() - ref).abs().max())
+    assert err <= _tight_bound(ref, K), (err, _tight_bound(ref, K))
