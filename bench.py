@@ -124,6 +124,8 @@ WORLD1 = [
 ]
 WORLD1_VENDOR = [
     ("compute_only(hipblaslt)", "compute_only", dict(size="unsharded", gemm="torch")),
+    # F.linear on the [n, k] weight: hipBLASLt's fastest layout, the like-for-like comparison
+    ("compute_only(hipblaslt,nt)", "compute_only", dict(size="unsharded", gemm="torch_nt")),
     ("pytorch(rccl+hipblaslt)", "pytorch", dict(backend="nccl", empty_cache=False)),
 ]
 # tp_rowwise (GEMM + sequence-parallel reduce-scatter; BASELINE config #3)
@@ -157,6 +159,7 @@ ROW_WORLD1 = [
 ]
 ROW_WORLD1_VENDOR = [
     ("row/compute_only(hipblaslt)", "compute_only", dict(gemm="torch")),
+    ("row/compute_only(hipblaslt,nt)", "compute_only", dict(gemm="torch_nt")),
     ("row/pytorch(rccl+hipblaslt)", "pytorch", dict(backend="nccl", empty_cache=False)),
 ]
 

@@ -269,6 +269,8 @@ class BoundPlan:
                 "hipGraph replay: plans with copy_streams > 1 (one peer's pulls split over several "
                 "copy streams) segfaulted in this HIP runtime (profiles/r02/r2_22_cs2_graph.txt); "
                 "use graph=False")
+        if os.environ.get("DDLB_CRASH_BT", "0") == "1":
+            self.ctx.C.install_crash_handler()  # (re)install right before the capture
         self.ex.enable_graph(on)
 
     def run(self, stream: Optional[int] = None) -> int:

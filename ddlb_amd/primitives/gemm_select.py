@@ -3,7 +3,10 @@
 ``hip``   : our CDNA4 MFMA kernels (:mod:`ddlb_amd.ops.gemm`); weights are stored ``[n, k]``
             (K-contiguous, the layout both MFMA operands want — the same layout
             ``te.Linear`` keeps its weight in).
-``torch`` : ``torch.matmul`` (hipBLASLt / rocBLAS on GPU, ATen on CPU) — the vendor baseline.
+``torch`` : ``torch.matmul`` (hipBLASLt / rocBLAS on GPU, ATen on CPU) — the vendor baseline, with
+            the reference's ``[k, n]`` weight (``TPColumnwise/pytorch.py:97``).
+``torch_nt``: ``F.linear`` on the ``[n, k]`` weight — hipBLASLt's fastest layout (the one our
+            kernels use), so the vendor comparison is like for like.
 ``auto``  : ``hip`` on a GPU, ``torch`` on the CPU. On a GPU ``auto`` never silently falls back:
             a missing extension raises (the driver checks the native library really ran).
 """
@@ -30,8 +33,8 @@ class GemmBackend:
             self._hip = _g
 
     def prepare_weight(self, b):
-        """``b`` is ``[k, n]``; the HIP kernel consumes ``[n, k]``."""
-        if self.choice == "hip":
+        """``b`` is ``[k, n]``; the HIP kernel (and F.linear) consume ``[n, k]``."""
+        if self.choice in ("hip", "torch_nt"):
             return b.t().contiguous()
         return b
 
@@ -47,6 +50,8 @@ class GemmBackend:
 
         if a.dtype == torch.float8_e4m3fn:
             a, w = a.to(torch.bfloat16), w.to(torch.bfloat16)
+        if self.choice == "torch_nt":
+            return torch.nn.functional.linear(a, w)
         if out is not None:
             return torch.matmul(a, w, out=out)
         return torch.matmul(a, w)

@@ -17,7 +17,7 @@ from ddlb_amd.primitives.gemm_select import GemmBackend
 
 class ComputeOnlyTPColumnwise(TPColumnwise):
     DEFAULT_OPTIONS = {"size": "sharded", "gemm": "auto"}
-    ALLOWED_VALUES = {"size": ["sharded", "unsharded"], "gemm": ["auto", "hip", "torch"]}
+    ALLOWED_VALUES = {"size": ["sharded", "unsharded"], "gemm": ["auto", "hip", "torch", "torch_nt"]}
 
     def __init__(self, *args, **kwargs):
         super().__init__(*args, **kwargs)

@@ -14,7 +14,7 @@ from ddlb_amd.primitives.tp_rowwise.base import TPRowwise
 
 class ComputeOnlyTPRowwise(TPRowwise):
     DEFAULT_OPTIONS = {"size": "sharded", "gemm": "auto"}
-    ALLOWED_VALUES = {"size": ["sharded", "unsharded"], "gemm": ["auto", "hip", "torch"]}
+    ALLOWED_VALUES = {"size": ["sharded", "unsharded"], "gemm": ["auto", "hip", "torch", "torch_nt"]}
 
     def __init__(self, *args, **kwargs):
         super().__init__(*args, **kwargs)

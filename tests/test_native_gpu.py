@@ -489,8 +489,10 @@ def test_flag_gated_persistent_gemm_world1(comm, graph):
               first_shard=1, tile_order=1, reserve_cus=32)
     ctx = NativeContext(comm)
     bound = ctx.bind(plan)
-    if graph:
-        bound.enable_graph(True)
+    if graph:  # a copy-fed gated GEMM is never captured: refused, then run eagerly
+        assert not bound.ex.graph_capturable()
+        with pytest.raises(RuntimeError, match="not captured"):
+            bound.enable_graph(True)
     A = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
     W = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
     bound.buffer("src").view(torch.bfloat16).view(M, K).copy_(A)
@@ -541,7 +543,7 @@ def test_in_kernel_allgather_world1(comm, graph, mode):
     plan.wait_signal(0, [ACK + 4], method=SIG_IN_LAUNCH if mode & 16 else sig)
     ctx = NativeContext(comm)
     bound = ctx.bind(plan)
-    if graph:
+    if graph:  # the in-kernel all-gather sets its own gate flags: captured
         bound.enable_graph(True)
     A = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
     W = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
