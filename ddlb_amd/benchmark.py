@@ -345,7 +345,7 @@ class PrimitiveBenchmarkRunner:
         with open(jout) as f:
             row = json.load(f)
         try:
-            row["pmc"] = json.dumps(pmc_mod.summarize(out_dir), sort_keys=True)
+            row["pmc"] = json.dumps(pmc_mod.summarize(out_dir, top=8), sort_keys=True)
         except Exception as e:  # the measurement stands without counters
             row["pmc"] = f"unavailable: {type(e).__name__}: {e}"
         return row

@@ -79,8 +79,9 @@ def rocprof_cmd(counters: Sequence[str], out_dir: str, name: str = "pmc") -> Lis
     return [exe, "--pmc", *counters, "--selected-regions", "-d", out_dir, "-o", name, "--"]
 
 
-def summarize(out_dir: str, match: str = "") -> Dict[str, Dict[str, float]]:
-    """Per kernel (short name): mean of every counter over the recorded dispatches."""
+def summarize(out_dir: str, match: str = "", top: int = 0) -> Dict[str, Dict[str, float]]:
+    """Per kernel (short name): mean of every counter over the recorded dispatches; ``top`` > 0
+    keeps the kernels with the most ``GRBM_GUI_ACTIVE`` (else ``SQ_WAVE_CYCLES``) only."""
     vals: Dict[str, Dict[str, List[float]]] = collections.defaultdict(
         lambda: collections.defaultdict(list))
     for root, _, files in os.walk(out_dir):
@@ -98,7 +99,13 @@ def summarize(out_dir: str, match: str = "") -> Dict[str, Dict[str, float]]:
                         vals[short_name(kn)][cn].append(float(v))
             finally:
                 con.close()
-    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in vals.items()}
+    out = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in vals.items()}
+    if top > 0 and len(out) > top:
+        def weight(item):
+            cs = item[1]
+            return cs.get("GRBM_GUI_ACTIVE", cs.get("SQ_WAVE_CYCLES", 0.0))
+        out = dict(sorted(out.items(), key=weight, reverse=True)[:top])
+    return out
 
 
 def short_name(name: str) -> str:

@@ -86,3 +86,15 @@ def test_standalone_worker_cpu(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     row = json.loads(jout.read_text())
     assert row["valid"] is True and row["mean_time (ms)"] > 0
+
+
+def test_summarize_top(tmp_path):
+    db = tmp_path / "pmc_results.db"
+    con = sqlite3.connect(db)
+    con.execute("create table counters_collection (kernel_name text, counter_name text, "
+                "value real)")
+    con.executemany("insert into counters_collection values (?, ?, ?)",
+                    [(f"k{i}", "GRBM_GUI_ACTIVE", float(i)) for i in range(12)])
+    con.commit()
+    con.close()
+    assert set(pmc.summarize(str(tmp_path), top=3)) == {"k11", "k10", "k9"}
