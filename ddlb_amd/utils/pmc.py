@@ -4,8 +4,11 @@ The reference's only profiling hook is the 5-iteration ``cudaProfilerStart/Stop`
 external ``nsys --capture-range=cudaProfilerApi`` records (``ddlb/benchmark.py:89-104``). Here the
 same window is delimited with ``roctxProfilerResume/Pause`` (``ddlb_amd.utils.profiling``), and
 ``--pmc SQ_WAVES,...`` makes the runner start each benchmark child under
-``rocprofv3 --pmc <counters> --selected-regions``: the counters cover exactly the window's five
-``run()`` calls, and their per-kernel means come back in the CSV row (``pmc`` column, JSON).
+``rocprofv3 --pmc <counters> --selected-regions`` and the per-kernel means come back in the CSV row
+(``pmc`` column, JSON; the 8 kernels with the most GPU-active cycles). Measured on this image
+(``profiles/r03/r3_8_cli_pmc_default_set.txt``): rocprofv3 counted every dispatch of the child, not
+only the window's five ``run()`` calls, so a row's means also include the warmup / timed runs of
+the same kernels (and its validation kernels, which the per-kernel split keeps apart).
 
 rocprofv3 does not split counters over passes, and asking one pass for more than the hardware
 blocks hold makes it hang (``error code 38``) — so the set is checked against the per-pass limits
