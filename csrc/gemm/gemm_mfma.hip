@@ -30,6 +30,8 @@
 #include <hip/hip_fp16.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 #include "gemm.h"
 #include "gemm_entry.h"
 
@@ -82,6 +84,8 @@ int choose_tile(int64_t M, int64_t N, int64_t K, int din) {
 hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mode,
                        hipStream_t s) {
   GemmArgs p = p_in;
+  static const int raster_env = getenv("DDLB_RASTER_G") ? atoi(getenv("DDLB_RASTER_G")) : 0;
+  if (raster_env > 0) p.raster_g = raster_env;  // A/B knob of the tile raster (tile_map.h)
   if (p.a_grp <= 0) { p.a_grp = p.M > 0 ? p.M : 1; p.a_gstride = p.a_grp; }
   if (p.c_grp <= 0) { p.c_grp = p.M > 0 ? p.M : 1; p.c_gstride = p.c_grp; }
   if (p.M == 0 || p.N == 0) return hipSuccess;

@@ -50,9 +50,10 @@ static void check_tile_index(int ntiles, int order, int nshards, int nsub, int f
   }
 }
 
-static void check_tile_mn(int tm_n, int tn_n, int order) {
+static void check_tile_mn(int tm_n, int tn_n, int order, int g = 8) {
   GemmArgs p;
   p.tile_order = order;
+  p.raster_g = g;
   std::vector<int> seen(tm_n * tn_n, 0);
   for (int w = 0; w < tm_n * tn_n; ++w) {
     int tm = -1, tn = -1;
@@ -62,8 +63,8 @@ static void check_tile_mn(int tm_n, int tn_n, int order) {
     if (tm >= 0 && tm < tm_n && tn >= 0 && tn < tn_n) ++seen[tm * tn_n + tn];
   }
   for (int i = 0; i < tm_n * tn_n; ++i)
-    CHECK(seen[i] == 1, "tile_mn not bijective: %dx%d order %d cell %d x%d", tm_n, tn_n, order, i,
-          seen[i]);
+    CHECK(seen[i] == 1, "tile_mn not bijective: %dx%d order %d G %d cell %d x%d", tm_n, tn_n, order,
+          g, i, seen[i]);
 }
 
 static void check_ag_units(int np, int nsub, int parts, int rank) {
@@ -123,7 +124,8 @@ int main() {
         }
   for (int tm : {1, 3, 8, 13, 64, 256})
     for (int tn : {1, 2, 4, 5, 6, 32})
-      for (int order : {0, 1}) check_tile_mn(tm, tn, order);
+      for (int order : {0, 1})
+        for (int g : {1, 2, 4, 8, 16, 0}) check_tile_mn(tm, tn, order, g);
   for (int np : {2, 3, 4, 8})
     for (int nsub : {1, 2, 8})
       for (int parts : {1, 3, 8})
