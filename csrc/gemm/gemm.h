@@ -54,7 +54,7 @@ struct GemmArgs {
   // i.e. the order chunked pulls from all peers arrive in. nsub = 1: plain shard order.
   int nsub = 1;
   int reserve_cus = 0;              // flag-gated persistent GEMMs: CUs left free (see launch_pt4)
-  int raster_g = 8;                 // m-blocks per raster group of tile_mn (tile_map.h)
+  int raster_g = 4;                 // m-blocks per raster group of tile_mn (tile_map.h)
   // In-kernel all-gather (flag-gated pt4 only): workgroups [0, ag_ctas) of the launch pull the
   // peers' row blocks of A over xGMI into A (the same rows), count each (producer, block)
   // segment's ag_parts pieces and set its flag when the last lands, and ACK each producer once

@@ -47,13 +47,15 @@ __host__ __device__ inline int tile_index_virtual(const GemmArgs& p, int vid, in
 }
 
 // Tile id -> (tm, tn). Row-major, except that without a shard order and with more than 4 column
-// tiles, ids are rastered in groups of G = raster_g m-blocks (default 8, column-major inside a
-// group): the 32 tiles an XCD runs together (consecutive ids after xcd_remap) then cover 8 m-blocks
-// x 4 n-blocks, i.e. 12 A / B panels in its L2 instead of 1 + 32 (guide §5, L2 reuse per XCD).
-// Bijective for every G >= 1.
+// tiles, ids are rastered in groups of G = raster_g m-blocks (default 4, column-major inside a
+// group): the 32 tiles an XCD runs together (consecutive ids after xcd_remap) then cover 4 m-blocks
+// x 8 n-blocks, i.e. 12 A / B panels in its L2 instead of 1 + 32 (guide §5, L2 reuse per XCD).
+// Measured (profiles/r03/r3_9_raster_*.txt, pt4, one box): 16384x8192x8192 G = 2 / 4 / 8 / 16:
+// 1.430 / 1.395 / 1.465 / 1.451 ms; 8192^3 0.704 / 0.688 / 0.688 / 0.703 ms. Bijective for every
+// G >= 1.
 __host__ __device__ inline void tile_mn(const GemmArgs& p, int wg, int tiles_m, int tiles_n,
                                         int& tm, int& tn) {
-  const int G = p.raster_g > 0 ? p.raster_g : 8;
+  const int G = p.raster_g > 0 ? p.raster_g : 4;
   if (p.tile_order || tiles_n <= 4) {
     tm = wg / tiles_n;
     tn = wg % tiles_n;
