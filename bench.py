@@ -86,6 +86,8 @@ CANDIDATES = [
     # RCCL's kernels on a CU-masked comm stream (csrc/comm: hipExtStreamCreateWithCUMask), the
     # stage GEMMs sized to the complement; buffers registered with ncclCommRegister
     ("coll_pipeline/rccl/s4/cumask", "native", dict(_COLL4, comm_cus=32, register=True)),
+    ("coll_pipeline/rccl/s8/cumask", "native", dict(_COLL4, s=8, comm_cus=32, register=True)),
+    ("coll_pipeline/rccl/s4/cumask64", "native", dict(_COLL4, comm_cus=64)),
     ("coll_pipeline/rccl/s4/128/c16", "native", dict(_COLL4, tile="128x128",
                                                       _env={"NCCL_MAX_NCHANNELS": "16"})),
     ("p2p_pipeline/rccl", "native", dict(algorithm="p2p_pipeline", backend="rccl")),
@@ -654,6 +656,12 @@ def main(argv=None) -> int:
         sys.stderr.write("bench.py: --gpus > 1 must be launched with torch.distributed.run\n")
         return 2
     job = Job(a)
+    # warm the page cache for the children: the first `import torch` on a fresh box takes 1-2
+    # minutes, which would otherwise land inside the first candidate's timeout (importing torch
+    # does not initialise the GPU in this parent)
+    t0 = time.time()
+    import torch  # noqa: F401
+    job.log(f"import torch {time.time() - t0:.1f} s")
     tune = {}
     pool = candidate_pool(a.primitive, a.dtype, world)
     every = candidate_pool(a.primitive, a.dtype, 1) + candidate_pool(a.primitive, a.dtype, 2)
