@@ -111,12 +111,32 @@ def _compile(src_rel: str, force: bool, verbose: bool) -> str:
     return obj
 
 
+def source_digest() -> str:
+    """sha256 over every source and header the extension is built from (in build order)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for rel in SOURCES + HEADERS:
+        with open(os.path.join(CSRC, rel), "rb") as f:
+            h.update(rel.encode() + b"\0" + f.read())
+    return h.hexdigest()
+
+
+STAMP = os.path.join(PKG, "_C.sources.sha256")  # digest of the sources the in-tree .so came from
+
+
 def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
+    """Compile what changed and link ``ddlb_amd/_C*.so``. The digest of the sources the .so was
+    built from is kept next to it; a .so whose digest differs from the tree's is rebuilt from
+    scratch even when file times look fresh (a checkout or copy can reset mtimes)."""
     os.makedirs(BUILD, exist_ok=True)
+    digest = source_digest()
+    out = ext_path()
+    stamp_ok = os.path.exists(out) and os.path.exists(STAMP) and open(STAMP).read().strip() == digest
+    force = force or not stamp_ok
     jobs = jobs or min(len(SOURCES), max(1, os.cpu_count() or 4), 8)
     with ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, force, verbose), SOURCES))
-    out = ext_path()
     if not force and os.path.exists(out) and all(
             os.path.getmtime(out) >= os.path.getmtime(o) for o in objs):
         return out
@@ -131,6 +151,8 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
     os.replace(out + ".tmp", out)
+    with open(STAMP, "w") as f:
+        f.write(digest + "\n")
     return out
 
 
