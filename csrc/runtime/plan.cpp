@@ -280,6 +280,21 @@ std::vector<float> PlanExecutor::timeline() {
   return out;
 }
 
+// DDLB_GRAPH_DEBUG=1: a stderr line per capture / instantiate / launch step and per captured op
+// (op code, stream, graph node count), flushed, to locate a crash inside the runtime.
+static bool graph_debug() {
+  static const bool on = getenv("DDLB_GRAPH_DEBUG") != nullptr;
+  return on;
+}
+#define GDBG(...)                                  \
+  do {                                             \
+    if (graph_debug()) {                           \
+      fprintf(stderr, "[graph] " __VA_ARGS__);     \
+      fputc('\n', stderr);                         \
+      fflush(stderr);                              \
+    }                                              \
+  } while (0)
+
 void PlanExecutor::join_others(int64_t stream, hipStream_t main) {
   hipStream_t s = S(stream, main);
   for (size_t j = 0; j < streams_.size(); ++j) {
@@ -332,10 +347,12 @@ void PlanExecutor::enqueue(hipStream_t main) {
     if (graph_on_ && o[0] == OP_WAIT_SIGNAL) join_others(o[1], main);
     touched_[(size_t)o[1]] = true;
     const size_t idx = i / kOpWords;
+    if (graph_on_) GDBG("  op %zu code %lld stream %lld", idx, (long long)o[0], (long long)o[1]);
     const bool tr = trace_on_ && idx < labels_.size();
     if (tr) roctx().push(labels_[idx].c_str());
     if (!timeline_on_) {
       exec(&ops_[i], main);
+      if (graph_on_) GDBG("  op %zu enqueued", idx);
       if (tr) roctx().pop();
       continue;
     }
@@ -349,10 +366,12 @@ void PlanExecutor::enqueue(hipStream_t main) {
   if (any_side_) {  // join
     for (size_t i = 1; i < streams_.size(); ++i)
       if (used_[i]) {
+        if (graph_on_) GDBG("  join stream %zu", i);
         DDLB_HIP(hipEventRecord(fork_join_[streams_.size() + i], streams_[i]));
         DDLB_HIP(hipStreamWaitEvent(main, fork_join_[streams_.size() + i], 0));
       }
   }
+  if (graph_on_) GDBG("  enqueue done");
   if (compute_) {
     DDLB_HIP(hipEventRecord(compute_join_, compute_));
     DDLB_HIP(hipStreamWaitEvent(main, compute_join_, 0));
@@ -368,6 +387,7 @@ unsigned PlanExecutor::run(uintptr_t main_stream) {
   }
   if (graph_exec_ == nullptr) {
     // capture on a private stream (the caller's may be the legacy null stream)
+    GDBG("begin capture (%zu ops, %zu streams)", ops_.size() / kOpWords, streams_.size());
     DDLB_HIP(hipStreamBeginCapture(cap_stream_, hipStreamCaptureModeRelaxed));
     try {
       enqueue(cap_stream_);
@@ -378,9 +398,33 @@ unsigned PlanExecutor::run(uintptr_t main_stream) {
       throw;
     }
     DDLB_HIP(hipStreamEndCapture(cap_stream_, &graph_));
+    if (graph_debug()) {
+      size_t nn = 0;
+      hipGraphGetNodes(graph_, nullptr, &nn);
+      std::vector<hipGraphNode_t> nodes(nn);
+      hipGraphGetNodes(graph_, nodes.data(), &nn);
+      int counts[16] = {0};
+      for (auto n : nodes) {
+        hipGraphNodeType t;
+        if (hipGraphNodeGetType(n, &t) == hipSuccess && (int)t >= 0 && (int)t < 16) ++counts[(int)t];
+      }
+      GDBG("end capture: %zu nodes (kernel %d memcpy %d memset %d host %d graph %d empty %d "
+           "wait_event %d event_record %d)", nn, counts[hipGraphNodeTypeKernel],
+           counts[hipGraphNodeTypeMemcpy], counts[hipGraphNodeTypeMemset],
+           counts[hipGraphNodeTypeHost], counts[hipGraphNodeTypeGraph],
+           counts[hipGraphNodeTypeEmpty], counts[hipGraphNodeTypeWaitEvent],
+           counts[hipGraphNodeTypeEventRecord]);
+    }
     DDLB_HIP(hipGraphInstantiate(&graph_exec_, graph_, nullptr, nullptr, 0));
+    GDBG("instantiated");
   }
+  GDBG("launch epoch %u", epoch_);
   DDLB_HIP(hipGraphLaunch(graph_exec_, main));
+  GDBG("launched");
+  if (graph_debug()) {
+    DDLB_HIP(hipStreamSynchronize(main));
+    GDBG("synchronized");
+  }
   return epoch_;
 }
 

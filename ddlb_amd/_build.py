@@ -85,19 +85,37 @@ def _torch_lib_dir() -> str:
     return os.path.join(os.path.dirname(spec.origin), "lib") if spec and spec.origin else ""
 
 
-def _stale(obj: str, src: str) -> bool:
-    if not os.path.exists(obj):
-        return True
-    t = os.path.getmtime(obj)
-    deps = [src] + [os.path.join(CSRC, h) for h in HEADERS]
-    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+def _digest(rels) -> str:
+    import hashlib
+
+    h = hashlib.sha256()
+    for rel in rels:
+        with open(os.path.join(CSRC, rel), "rb") as f:
+            h.update(rel.encode() + b"\0" + f.read())
+    return h.hexdigest()
 
 
-def _compile(src_rel: str, force: bool, verbose: bool) -> str:
+def _stamp_ok(path: str, digest: str) -> bool:
+    stamp = path + ".sha256"
+    if not (os.path.exists(path) and os.path.exists(stamp)):
+        return False
+    with open(stamp) as f:
+        return f.read().strip() == digest
+
+
+def _write_stamp(path: str, digest: str) -> None:
+    with open(path + ".sha256", "w") as f:
+        f.write(digest + "\n")
+
+
+def _compile(src_rel: str, force: bool, verbose: bool):
+    """-> (object path, recompiled?). An object is rebuilt when the digest of its source plus
+    every header differs from the one recorded next to it (content, not file times)."""
     src = os.path.join(CSRC, src_rel)
     obj = os.path.join(BUILD, src_rel.replace("/", "_") + ".o")
-    if not force and not _stale(obj, src):
-        return obj
+    digest = _digest([src_rel] + HEADERS)
+    if not force and _stamp_ok(obj, digest):
+        return obj, False
     cmd = [_hipcc(), "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}",
            "-Wno-unused-result", "-DNDEBUG"]
     if src.endswith(".cpp"):
@@ -108,37 +126,27 @@ def _compile(src_rel: str, force: bool, verbose: bool) -> str:
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src_rel}:\n{r.stderr[-6000:]}")
-    return obj
+    _write_stamp(obj, digest)
+    return obj, True
 
 
 def source_digest() -> str:
     """sha256 over every source and header the extension is built from (in build order)."""
-    import hashlib
-
-    h = hashlib.sha256()
-    for rel in SOURCES + HEADERS:
-        with open(os.path.join(CSRC, rel), "rb") as f:
-            h.update(rel.encode() + b"\0" + f.read())
-    return h.hexdigest()
-
-
-STAMP = os.path.join(PKG, "_C.sources.sha256")  # digest of the sources the in-tree .so came from
+    return _digest(SOURCES + HEADERS)
 
 
 def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
-    """Compile what changed and link ``ddlb_amd/_C*.so``. The digest of the sources the .so was
-    built from is kept next to it; a .so whose digest differs from the tree's is rebuilt from
-    scratch even when file times look fresh (a checkout or copy can reset mtimes)."""
+    """Compile what changed and link ``ddlb_amd/_C*.so``. Objects and the .so carry the digest
+    of the sources they were built from (``<file>.sha256``): whatever differs from the tree's
+    content is rebuilt, so a checkout or copy that resets file times cannot leave a stale .so."""
     os.makedirs(BUILD, exist_ok=True)
-    digest = source_digest()
     out = ext_path()
-    stamp_ok = os.path.exists(out) and os.path.exists(STAMP) and open(STAMP).read().strip() == digest
-    force = force or not stamp_ok
+    digest = source_digest()
     jobs = jobs or min(len(SOURCES), max(1, os.cpu_count() or 4), 8)
     with ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, force, verbose), SOURCES))
-    if not force and os.path.exists(out) and all(
-            os.path.getmtime(out) >= os.path.getmtime(o) for o in objs):
+        res = list(ex.map(lambda s: _compile(s, force, verbose), SOURCES))
+    objs = [o for o, _ in res]
+    if not any(rebuilt for _, rebuilt in res) and _stamp_ok(out, digest):
         return out
     tl = _torch_lib_dir()
     cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", out + ".tmp",
@@ -151,8 +159,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
     os.replace(out + ".tmp", out)
-    with open(STAMP, "w") as f:
-        f.write(digest + "\n")
+    _write_stamp(out, digest)
     return out
 
 
