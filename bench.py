@@ -105,7 +105,8 @@ CANDIDATES = [
     # gated GEMM after every copy stream, see PlanExecutor::graph_capturable)
     ("coll_pipeline/ipc/memcpy/s8/fused", "native", dict(_COLL_IPC, s=8, fused=True)),
     # each peer's chunks split over 2 copy streams (2 copy engines per link)
-    ("coll_pipeline/ipc/memcpy/s8/cs2", "native", dict(_COLL_IPC, s=8, copy_streams=2)),
+    ("coll_pipeline/ipc/memcpy/s8/cs2/graph", "native",
+     dict(_COLL_IPC, s=8, copy_streams=2, graph=True)),
     ("coll_pipeline/ipc/kernel/s4", "native", dict(_COLL_IPC, multicast_protocol="kernel",
                                                    copy_blocks=128, tile="128x128")),
     ("coll_pipeline/ipc/memcpy/s8", "native", dict(_COLL_IPC, s=8)),

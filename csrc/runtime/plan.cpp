@@ -7,6 +7,7 @@
 #include <unistd.h>
 
 #include <chrono>
+#include <functional>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
@@ -190,6 +191,11 @@ bool PlanExecutor::graph_capturable() const {
   //    copy stream instead serialises copy-then-GEMM and removes the overlap it exists for
   //    (ADVICE r2). Such plans run eagerly, where the enqueue order puts the copies first.
   //  * a CU split (set_cu_split): masked streams are not carried into graph nodes.
+  //  * a cycle of dependencies among the side streams (s -> t and, later, t -> s, through event
+  //    edges or the joins before cross-process waits; no cycle of nodes needed):
+  //    hipStreamEndCapture of this HIP runtime segfaults on it (scripts/diag_graph_edges.py
+  //    `cycle`, profiles/r03/r3_15_*). Cycles through the capture's origin stream (the fork /
+  //    join every plan has) are fine.
   if (comm_cus_ > 0) return false;
   for (size_t i = 0; i < ops_.size(); i += kOpWords) {
     const int64_t k = ops_[i];
@@ -198,15 +204,49 @@ bool PlanExecutor::graph_capturable() const {
       return false;
     if (k == OP_GEMM && ops_[i + 19] != 0 && ops_[i + 29] == 0) return false;
   }
-  return true;
+  return !side_stream_cycle();
+}
+
+bool PlanExecutor::side_stream_cycle() const {
+  // the stream relations a capture of this plan creates, as enqueue() issues them in graph mode
+  const size_t ns = streams_.size();
+  std::vector<std::vector<char>> adj(ns, std::vector<char>(ns, 0));
+  std::vector<int64_t> rec_on(events_.size(), -1);
+  std::vector<char> effect(ns, 0);
+  auto edge = [&](int64_t a, int64_t b) {
+    if (a >= 1 && b >= 1 && a != b && (size_t)a < ns && (size_t)b < ns) adj[a][b] = 1;
+  };
+  for (size_t i = 0; i < ops_.size(); i += kOpWords) {
+    const int64_t k = ops_[i], st = ops_[i + 1];
+    if (k == OP_RECORD && (size_t)ops_[i + 2] < rec_on.size()) rec_on[(size_t)ops_[i + 2]] = st;
+    if (k == OP_WAIT && (size_t)ops_[i + 2] < rec_on.size()) edge(rec_on[(size_t)ops_[i + 2]], st);
+    if (k == OP_WAIT_SIGNAL)
+      for (size_t j = 0; j < ns; ++j)
+        if (effect[j]) edge((int64_t)j, st);
+    if (k != OP_WAIT_SIGNAL && k != OP_WAIT && k != OP_RECORD && (size_t)st < ns) effect[st] = 1;
+  }
+  // cycle check (colour DFS over at most a few dozen streams)
+  std::vector<int> colour(ns, 0);
+  std::function<bool(size_t)> dfs = [&](size_t u) {
+    colour[u] = 1;
+    for (size_t v = 0; v < ns; ++v) {
+      if (!adj[u][v]) continue;
+      if (colour[v] == 1 || (colour[v] == 0 && dfs(v))) return true;
+    }
+    colour[u] = 2;
+    return false;
+  };
+  for (size_t u = 1; u < ns; ++u)
+    if (colour[u] == 0 && dfs(u)) return true;
+  return false;
 }
 
 void PlanExecutor::enable_graph(bool on) {
   if (on && timeline_on_) throw std::runtime_error("hipGraph replay: turn the plan timeline off");
   if (on && !graph_capturable())
     throw std::runtime_error("hipGraph replay: plans with RCCL calls, copy-engine-fed "
-                             "flag-gated GEMMs or a CU split are not captured (see "
-                             "PlanExecutor::graph_capturable)");
+                             "flag-gated GEMMs, a CU split or a cycle among side streams are not "
+                             "captured (see PlanExecutor::graph_capturable)");
   if (on) {  // the device run counter continues from the host one (see graph_capturable)
     DDLB_HIP(hipSetDevice(device_));
     DDLB_HIP(hipDeviceSynchronize());
@@ -345,7 +385,11 @@ void PlanExecutor::enqueue(hipStream_t main) {
     // stream (the deadlock-freedom argument of the eager enqueue order, kept under any node
     // order the graph may pick); flag-gated GEMMs fed by other streams are not captured at all
     if (graph_on_ && o[0] == OP_WAIT_SIGNAL) join_others(o[1], main);
-    touched_[(size_t)o[1]] = true;
+    // only ops with an effect a peer can depend on count: waits and event records add none, and
+    // joining a wait-only stream would create side-stream -> side-stream capture relations that,
+    // together with the plan's own side-stream edges (copy_streams > 1), form a cycle on which
+    // this HIP runtime's hipStreamEndCapture segfaults (scripts/diag_graph_edges.py cs2_exact)
+    if (o[0] != OP_WAIT_SIGNAL && o[0] != OP_WAIT && o[0] != OP_RECORD) touched_[(size_t)o[1]] = true;
     const size_t idx = i / kOpWords;
     if (graph_on_) GDBG("  op %zu code %lld stream %lld", idx, (long long)o[0], (long long)o[1]);
     const bool tr = trace_on_ && idx < labels_.size();

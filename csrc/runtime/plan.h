@@ -123,8 +123,9 @@ class PlanExecutor {
   // stream that already has ops, so ANY execution order of the captured graph keeps all ops
   // enqueued before the wait ahead of it (what makes the plan deadlock-free in one queue)
   std::vector<hipEvent_t> sync_ev_;
-  std::vector<bool> touched_;
+  std::vector<bool> touched_;  // graph capture: stream has an effectful op (not a wait / record)
   void join_others(int64_t stream, hipStream_t main);
+  bool side_stream_cycle() const;  // see graph_capturable
   RcclComm* comm_ = nullptr;
   bool timeline_on_ = false;
   hipEvent_t tl_start_ = nullptr;

@@ -263,12 +263,6 @@ class BoundPlan:
                 "hipGraph replay needs at least 4 hardware queues per process: with "
                 f"GPU_MAX_HW_QUEUES={os.environ.get('GPU_MAX_HW_QUEUES')} the HIP runtime of this "
                 "image crashes in hipGraphLaunch (profiles/r02/r2_17_*)")
-        if (on and self.plan.meta.get("copy_streams", 1) > 1
-                and os.environ.get("DDLB_GRAPH_CS2", "0") != "1"):  # diagnostic override
-            raise RuntimeError(
-                "hipGraph replay: plans with copy_streams > 1 (one peer's pulls split over several "
-                "copy streams) segfaulted in this HIP runtime (profiles/r02/r2_22_cs2_graph.txt); "
-                "use graph=False")
         if os.environ.get("DDLB_CRASH_BT", "0") == "1":
             self.ctx.C.install_crash_handler()  # (re)install right before the capture
         self.ex.enable_graph(on)

@@ -166,8 +166,7 @@ def maybe_enable_graph(bound, option) -> bool:
     from ddlb_amd.parallel.context import graph_replay_supported
 
     if (option == "auto" and len(bound.plan.ops) >= GRAPH_MIN_OPS
-            and bound.ex.graph_capturable() and graph_replay_supported()
-            and bound.plan.meta.get("copy_streams", 1) <= 1):
+            and bound.ex.graph_capturable() and graph_replay_supported()):
         bound.enable_graph(True)
         return True
     return False

@@ -13,6 +13,10 @@ once and byte-checked in a child process of its own (a crash only ends that chil
   copy streams, two stages of split copies + edges + GEMM, ACK signal, ACK wait) on local buffers,
   with the waited flags preset so every wait is already satisfied
 * ``cs2_noedge``: cs2_exact with each stage's s3 -> s2 edge replaced by s3 -> s0
+* ``cycle``: no signals at all, only copies and event edges s1 -> s2 then s2 -> s1 (a cycle of
+  stream relations, no cycle of nodes): crashed hipStreamEndCapture; now refused by
+  ``graph_capturable()`` (the child exits 1 with the refusal), the cs2 variants capture since the
+  executor no longer joins wait-only streams before a cross-process wait
 
     python scripts/diag_graph_edges.py            # every variant, one child each
 """
@@ -26,7 +30,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 VARIANTS = ["side_main", "side_side_kernel", "side_side_tail", "side_side", "cs2_noedge",
-            "cs2_exact"]
+            "cs2_exact", "cycle"]
 NB = 1 << 20
 
 
@@ -65,6 +69,15 @@ def build(variant: str):
     plan = Plan(0, 1, nstreams=3)
     src = plan.buffer("src", 3 * NB)
     dst = plan.buffer("dst", 3 * NB)
+    if variant == "cycle":
+        plan.copy(1, dst, src, NB, method=COPY_ENGINE)
+        plan.edge(1, 2)
+        plan.copy(2, dst + NB, src + NB, NB, method=COPY_ENGINE)
+        plan.edge(2, 1)
+        plan.copy(1, dst + 2 * NB, src + 2 * NB, NB, method=COPY_ENGINE)
+        plan.edge(1, 0)
+        plan.edge(2, 0)
+        return plan
     plan.copy(1, dst, src, NB, method=COPY_ENGINE)
     plan.copy(2, dst + NB, src + NB, NB,
               method=COPY_KERNEL if variant == "side_side_kernel" else COPY_ENGINE)
@@ -100,7 +113,8 @@ def child(variant: str) -> int:
         bufs["dst"].zero_()
         ex.run(stream)
         torch.cuda.synchronize()
-    n = {"side_side_tail": 3 * NB}.get(variant, 4 * NB if variant.startswith("cs2") else 2 * NB)
+    n = {"side_side_tail": 3 * NB, "cycle": 3 * NB}.get(
+        variant, 4 * NB if variant.startswith("cs2") else 2 * NB)
     ok = torch.equal(bufs["dst"][:n], bufs["src"][:n])
     print(f"{variant}: replayed, bytes {'ok' if ok else 'WRONG'}", flush=True)
     return 0 if ok else 1

@@ -170,7 +170,12 @@ def _ipc_cfgs():
                                                      multicast_protocol="kernel")),
             ("row/coll/graph", "row", dict(algorithm="coll_pipeline", s=2)),
             ("row/p2p/graph", "row", dict(algorithm="p2p_pipeline")),
-            ("row/p2p/direct/graph", "row", dict(algorithm="p2p_pipeline", fused=True))):
+            ("row/p2p/direct/graph", "row", dict(algorithm="p2p_pipeline", fused=True)),
+            # split pulls: side-to-side event edges inside the capture (r3_15)
+            ("col/coll/memcpy/cs2/graph", "col", dict(algorithm="coll_pipeline", s=2,
+                                                      copy_streams=2)),
+            ("col/p2p/memcpy/cs2/graph", "col", dict(algorithm="p2p_pipeline", copy_streams=2)),
+            ("row/coll/cs2/graph", "row", dict(algorithm="coll_pipeline", copy_streams=2))):
         cfgs.append((label, prim, dict(opts, backend="ipc", graph=True)))
     for alg in ("default", "coll_pipeline", "p2p_pipeline"):  # pulls split over 2 copy streams
         cfgs.append((f"col/{alg}/memcpy/cs2", "col", dict(algorithm=alg, backend="ipc", s=2,
@@ -619,3 +624,36 @@ def test_bench_preflight_shared_gpu():
     for ph in ("ipc", "ipc_ksig", "ipc_kernel", "ipc_sdma", "ipc_push"):
         assert pre[ph].startswith("ok"), (ph, pre, r.stderr[-3000:])
     assert set(pre) >= {"rccl", "torch_nccl"}
+
+
+def test_side_stream_cycle_is_not_captured():
+    """A cycle of dependencies among side streams (s1 -> s2, later s2 -> s1; no cycle of nodes)
+    makes this HIP runtime's hipStreamEndCapture segfault (r3_15): graph_capturable() detects it
+    and enable_graph refuses, the plan still runs eagerly. The cs2 pipeline's op sequence (side
+    edges plus the joins before cross-process waits) captures and replays: checked in a child
+    process, since a regression would segfault."""
+    import importlib.util
+
+    from ddlb_amd.ops import load
+
+    spec = importlib.util.spec_from_file_location(
+        "diag_graph_edges", os.path.join(ROOT, "scripts", "diag_graph_edges.py"))
+    diag = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(diag)
+    C = load()
+    cyc = diag.build("cycle")
+    ex = C.PlanExecutor(0, cyc.nstreams, max(cyc.nevents, 1), list(cyc.stream_priority))
+    NB = diag.NB
+    src = torch.randint(0, 255, (3 * NB,), dtype=torch.uint8, device="cuda")
+    dst = torch.zeros_like(src)
+    ex.load(cyc.encode(lambda ref: (src if ref.buf == "src" else dst).data_ptr() + ref.off))
+    assert not ex.graph_capturable()
+    with pytest.raises(RuntimeError, match="cycle"):
+        ex.enable_graph(True)
+    ex.run(torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(dst, src)
+    for variant in ("cs2_exact", "side_side"):
+        r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "scripts", "diag_graph_edges.py"),
+                            "--child", variant], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0 and "bytes ok" in r.stdout, (variant, r.returncode, r.stderr[-800:])
