@@ -1,0 +1,13 @@
+# Re-entry validation after the container rebuild: GPU suite, smoke, N=1 bench, kernel stats of the bench
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/r3_17
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -v -rs --timeout 170 --timeout-method thread > $O/gpu_tests.log 2>&1; rc=$?; tail -4 $O/gpu_tests.log; grep -a "FAILED\|Timeout" $O/gpu_tests.log | tail -20; [ $rc -le 1 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo smoke failed; tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+timeout -k 10 500 python bench.py --steps 20 --warmup 5 > $O/bench.log 2>&1 || { echo bench failed; tail -20 $O/bench.log; exit 1; }
+grep -a "\[bench" $O/bench.log | cut -c1-200; grep metric $O/bench.log | cut -c1-900
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -- python bench.py --steps 50 --warmup 5 > $O/prof_bench.log 2>&1; echo "prof rc=$?"
+find $O/prof -name "*kernel_stats.csv" | head -3

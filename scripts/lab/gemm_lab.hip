@@ -1558,6 +1558,18 @@ __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
   } while (0)
 #define T4_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
   const bool g1 = wr == 1;
+  // STAMP: per-wave cycle buckets (s_memtime, scalar): 0 LDS-read phase up to lgkmcnt(0), 1 vmcnt
+  // waits, 2 barriers, 3 MFMA issue, 4 C stores, 5 whole stream
+  unsigned long long st[16] = {}, tprev = 0;
+  auto T = [&](int bucket) __attribute__((always_inline)) {
+    if constexpr (STAMP) {
+      __builtin_amdgcn_sched_barrier(0);
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
+      if (bucket >= 0) st[bucket] += t - tprev;
+      tprev = t;
+    }
+  };
   // stage cursors: qa = K-tile h+1 (A units staged in phase A), qb = h+2 (B units in phase B)
   Cur q0{0, 0}, q1{0, 0};
   adv(q1);
@@ -1572,6 +1584,8 @@ __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
   wait_vm<6>();
   T4_BAR();
   if (g1) T4_BAR();
+  T(-1);
+  const unsigned long long t_start = tprev;
   // KIND: 0 normal, 1 last K-tile of a tile, 2 first K-tile after a tile's last, 3 second
   // (3 only with interleaved stores, SKIP & 256: Q00/Q01 of the finished tile are stored inside
   // phase B of its last K-tile, Q11/Q10 inside phase A of the next tile's first K-tile; the
@@ -1584,15 +1598,20 @@ __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
     loadB(cur, 0);  // phase A
     loadB(cur, 1);
     loadA(cur, 0);
+    T(0);
     stage(0, UA0, qa, b ^ 1);
     stage(1, UA1, qa, b ^ 1);
+    T(1);
     T4_LGKM0();
+    T(2);
     if constexpr (ILS) {
       if (g1) wait_vm<KIND == 2 || KIND == 3 ? 8 + 2 * NS : 8>();
     } else {
       if (g1) wait_vm<KIND == 2 ? 8 + 4 * NS : 8>();
     }
+    T(6);
     T4_BAR();
+    T(7);
     if constexpr ((SKIP & 2048) == 0) __builtin_amdgcn_s_setprio((SKIP & 4096) ? 0 : 1);
     if constexpr (ILS && KIND == 2) {
       mm_st(0, 0, 1, 1, ti - 1);
@@ -1601,23 +1620,32 @@ __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
       mm(0, 1);
     }
     if constexpr ((SKIP & 2048) == 0) __builtin_amdgcn_s_setprio((SKIP & 4096) ? 1 : 0);
+    T(11);
     if constexpr (!ILS && KIND == 1) { store_q(0, 0, ti); store_q(0, 1, ti); }
+    T(13);
     if constexpr (ILS) {
       if (!g1) wait_vm<KIND == 2 ? 8 + 4 * NS : (KIND == 3 ? 8 + 2 * NS : 8)>();
     } else {
       if (!g1) wait_vm<KIND == 1 ? 8 + 2 * NS : (KIND == 2 ? 8 + 4 * NS : 8)>();
     }
+    T(6);
     T4_BAR();
+    T(8);
     loadA(cur, 1);  // phase B
+    T(3);
     stage(2, UB0, qb, b);
     stage(3, UB1, qb, b);
+    T(4);
     T4_LGKM0();
+    T(5);
     if constexpr (ILS) {
       if (g1) wait_vm<KIND == 2 ? 6 + 2 * NS : 6>();
     } else {
       if (g1) wait_vm<KIND == 1 ? 6 + 2 * NS : 6>();
     }
+    T(6);
     T4_BAR();
+    T(9);
     if constexpr ((SKIP & 2048) == 0) __builtin_amdgcn_s_setprio((SKIP & 4096) ? 0 : 1);
     if constexpr (ILS && KIND == 1) {
       mm_st(1, 1, 0, 0, ti);
@@ -1626,13 +1654,17 @@ __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
       mm(1, 0);
     }
     if constexpr ((SKIP & 2048) == 0) __builtin_amdgcn_s_setprio((SKIP & 4096) ? 1 : 0);
+    T(12);
     if constexpr (!ILS && KIND == 1) { store_q(1, 1, ti); store_q(1, 0, ti); }
+    T(13);
     if constexpr (ILS) {
       if (!g1) wait_vm<KIND == 1 || KIND == 2 ? 6 + 2 * NS : 6>();
     } else {
       if (!g1) wait_vm<KIND == 1 ? 6 + 4 * NS : 6>();
     }
+    T(6);
     T4_BAR();
+    T(10);
     qa = qb;
     adv(qb);
   };
@@ -1653,6 +1685,16 @@ __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
 #undef T4_BAR
 #undef T4_LGKM0
   wait_vm<0>();
+  if constexpr (STAMP) {
+    T(-1);
+    st[14] = tprev - t_start;
+    if (lane == 0) {
+      unsigned long long* o = p.stamps + ((size_t)blockIdx.x * 8 + wave) * 16;
+#pragma unroll
+      for (int j = 0; j < 15; ++j) o[j] = st[j];
+      o[15] = (unsigned long long)my_tiles;
+    }
+  }
 }
 
 
@@ -2079,7 +2121,7 @@ int main(int argc, char** argv) {
   CHECK(hipDeviceSynchronize());
   unsigned long long* stamps;
   const int grid = std::min(ncu, (M / 256) * (N / 256));
-  CHECK(hipMalloc(&stamps, ((size_t)grid * 8 * 5 + 8) * 8));
+  CHECK(hipMalloc(&stamps, ((size_t)grid * 8 * 16 + 8) * 8));
 
   Variant vs[] = {
       {"ring2 dmaAC", ring2_kernel<4, false, 2>, 4, 512, 0},
@@ -2170,24 +2212,32 @@ int main(int argc, char** argv) {
     const float med = t[t.size() / 2];
     printf("  %-20s %8.4f ms  %7.1f TFLOP/s\n", vs[v].name, med, flop / (med * 1e-3) / 1e12);
   }
-  if (only) return 0;
-  // stamps for NS=4
-  Args s = a;
-  s.stamps = stamps;
-  CHECK(hipMemset(stamps, 0, ((size_t)grid * 8 * 5 + 8) * 8));
-  hipLaunchKernelGGL((ring2_kernel<4, true, 2>), dim3(grid), dim3(512), 0, 0, s);
-  CHECK(hipDeviceSynchronize());
-  std::vector<unsigned long long> h((size_t)grid * 8 * 5 + 8);
-  CHECK(hipMemcpy(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost));
-  double sum[5] = {0, 0, 0, 0, 0};
-  for (size_t i = 0; i < (size_t)grid * 8 * 5; ++i) sum[i % 5] += (double)h[i];
-  const double nw = grid * 8.0, steps = (double)(M / 256) * (N / 256) * (K / 32) / grid;
-  printf("\nstamps (ring2 NS=4, cycles per step per wave): vmwait %.0f barrier %.0f  partA %.0f  partC %.0f  epilogue(amortized) %.0f\n",
-         sum[4] / nw / steps, sum[0] / nw / steps, sum[1] / nw / steps, sum[2] / nw / steps, sum[3] / nw / steps);
-  {
-    const double cyc = (double)h[(size_t)grid * 8 * 5 + 1], ns = (double)h[(size_t)grid * 8 * 5 + 3] * 10.0;
-    printf("block 0 wave 0: %.0f cycles in %.1f us -> %.2f GHz\n", cyc, ns / 1e3, cyc / ns);
+  if (getenv("LAB_STAMP")) {
+    // pt4 (nt stores) with s_memtime buckets: per K-tile cycles per wave, by wave group
+    Args s = a;
+    s.stamps = stamps;
+    for (int i = 0; i < 50; ++i) hipLaunchKernelGGL((pt4_kernel<false, 16>), dim3(grid), dim3(512), 0, 0, a);
+    CHECK(hipMemset(stamps, 0, ((size_t)grid * 8 * 16 + 8) * 8));
+    hipLaunchKernelGGL((pt4_kernel<true, 16>), dim3(grid), dim3(512), 0, 0, s);
+    CHECK(hipDeviceSynchronize());
+    std::vector<unsigned long long> h((size_t)grid * 8 * 16);
+    CHECK(hipMemcpy(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost));
+    const char* names[15] = {"A:ds_read issue", "A:glds issue", "A:lgkm wait", "B:ds_read issue",
+                             "B:glds issue", "B:lgkm wait", "vm waits", "bar after load A",
+                             "bar after mfma A", "bar after load B", "bar after mfma B",
+                             "mfma A issue", "mfma B issue", "C stores", "total"};
+    for (int g = 0; g < 2; ++g) {
+      double sum[15] = {}, kt = 0;
+      for (int b = 0; b < grid; ++b)
+        for (int w = g * 4; w < g * 4 + 4; ++w) {
+          const unsigned long long* o = &h[((size_t)b * 8 + w) * 16];
+          for (int j = 0; j < 15; ++j) sum[j] += (double)o[j];
+          kt += (double)o[15] * (K / 64);
+        }
+      printf("pt4 stamps, waves %d-%d, cycles per K-tile per wave:\n", g * 4, g * 4 + 3);
+      for (int j = 0; j < 15; ++j) printf("    %-18s %6.0f\n", names[j], sum[j] / kt);
+    }
+    printf("ideal: 4 x 32 MFMA x 16 cyc = 2048 per K-tile per SIMD (1024 issue per wave)\n");
   }
-  printf("ideal MFMA cycles per step per wave: %d (x2 waves per SIMD)\n", 32 * 16);
   return 0;
 }
