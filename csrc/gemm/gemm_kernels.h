@@ -754,22 +754,24 @@ template <> struct Store8<DT_F32> {
 // line leaves this XCD's L2 as it is written (write-through) instead of staying there as a dirty
 // streaming line. GEMM lab, one box (profiles/r02/s4/r2s4_17_*): pt4 flagship 0.1060 -> 0.1040 ms,
 // 16384x8192x1024 0.2347 -> 0.2177 ms vs plain nt stores.
+// soff: a wave-uniform part of the offset (SGPR soffset), so a kernel can keep the per-lane part
+// fixed and move only scalars per store (pt4).
 template <int OUT>
 __device__ __forceinline__ void store8_wt(__amdgpu_buffer_rsrc_t rc, unsigned off, const f32x4 a,
-                                          const f32x4 b) {
+                                          const f32x4 b, unsigned soff = 0) {
   typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
   constexpr int AUX = 18;  // sc1 | nt
   if constexpr (OUT == DT_F32) {
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, a), rc, off, 0, AUX);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, b), rc, off + 16, 0, AUX);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, a), rc, off, soff, AUX);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, b), rc, off + 16, soff, AUX);
   } else if constexpr (OUT == DT_BF16) {
     bf16x8 o = {(__bf16)a.x, (__bf16)a.y, (__bf16)a.z, (__bf16)a.w,
                 (__bf16)b.x, (__bf16)b.y, (__bf16)b.z, (__bf16)b.w};
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), rc, off, 0, AUX);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), rc, off, soff, AUX);
   } else {
     f16x8 o = {(_Float16)a.x, (_Float16)a.y, (_Float16)a.z, (_Float16)a.w,
                (_Float16)b.x, (_Float16)b.y, (_Float16)b.z, (_Float16)b.w};
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), rc, off, 0, AUX);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), rc, off, soff, AUX);
   }
 }
 
@@ -1512,22 +1514,31 @@ __global__ __launch_bounds__(512) void gemm_tn_t4_kernel(const GemmArgs p) {
 //   LAST of a tile:     A end g0 8+2NS / g1 8,   B end g0 6+4NS / g1 6+2NS
 //   FIRST after a LAST: A end 8+4NS (both),      B end 6
 // (stores count in issue order with the LDS-DMA; the counts keep exactly the ops issued after
-// the unit the next phase reads in flight). The A / B sources are per-lane 32-bit offsets inside
-// a tile's panels plus wave-uniform panel bases, so switching tiles costs two scalar pointers and
-// the kernel stays within 256 VGPRs. Plain A rows only (no shard table / grouped A / flags: t4).
-// Measured (scripts/lab, profiles/r01/s2/lab/t8_vs_ring2.txt): flagship 0.1127 vs t4 0.1160 ms.
+// the unit the next phase reads in flight).
+// Load phases carry no VALU (round 3, profiles/r03/r3_20..r3_22: the un-prioritized loading wave
+// pays ~90 cycles per VALU at the head of a segment, MI355X_MICROARCH.md "Two waves per SIMD"
+// item 6; lab flagship 0.1093 -> 0.1039 ms, 8192^3 0.7555 -> 0.7286):
+//  * LDS = [A units of buffers 0 / 1 | B units of buffers 0 / 1], unit (X, buf, q) at
+//    X * 64K + buf * 32K + q * 16K: a fragment read is a fixed per-lane VGPR plus a compile-time
+//    offset below 64 KB (the ds_read offset field); the buffer parity is static because every
+//    tile has an even number of K-tiles and its body is unrolled by two (a run-time parity
+//    branch between two instantiations made the register allocator spill ~250 VGPRs);
+//  * LDS-DMA through buffer descriptors: per-tile panel base in SGPRs, K offset in soffset, the
+//    per-lane source offsets fixed (pt4_ok keeps a 256-row panel below 2 GiB);
+//  * CMODE 2 C stores through SGPR soffsets and one fixed per-lane voffset;
+//  * a tile's first MFMA of every accumulator takes an inline-zero C operand (no v_mov zeroing).
 // GATED: the arrival-flag form (a separate instantiation, so the ungated kernel's code and
 // schedule are exactly those measured without flags).
 // CMODE: 0 = grouped C rows, plain nt stores; 1 = C row-block table (direct store); 2 = grouped C
-// rows, write-through nt buffer stores (C's byte extent below 2 GiB: 32-bit offsets)
+// rows in groups of a multiple of 256, write-through nt buffer stores (C's byte extent below
+// 2 GiB: 32-bit offsets)
 template <class Mma, int OUT, bool GATED, int CMODE = 0>
 __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
-  constexpr int ROWB = 128, UNIT = 128 * ROWB, STAGE = 4 * UNIT;
-  constexpr int UA0 = 0, UA1 = UNIT, UB0 = 2 * UNIT, UB1 = 3 * UNIT;
+  constexpr int ROWB = 128, UNIT = 128 * ROWB;
   constexpr int NS = 4 * Store8<OUT>::kStores;
   constexpr int OSZ = out_size<OUT>();
   constexpr bool PAIR = is_pair<Mma>::value;
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  __shared__ __attribute__((aligned(1024))) char smem[8 * UNIT];
   // CMODE 2: C through one wave-uniform descriptor (launch_pt4 checks the extent fits)
   const __amdgpu_buffer_rsrc_t crc =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.c, 0, 0x7FFFFFF0, 0x00020000);
@@ -1536,7 +1547,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   const int wr = wave >> 2, wc = wave & 3;
   const int tiles_n = p.N / 256, ntiles = (p.M / 256) * tiles_n;
   const int esz = Mma::kElem;
-  const int nk = p.K * esz / ROWB;
+  const int nk = p.K * esz / ROWB;  // even (pt4_ok)
   int bid = (int)blockIdx.x, nblk = (int)gridDim.x;
   if constexpr (GATED) {
     if (p.ag_ctas > 0) {  // in-kernel all-gather: the first ag_ctas workgroups copy
@@ -1565,8 +1576,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
       offB[q][i] = (unsigned)(lc * p.ldb * esz + ch);
     }
   }
-  const char* baseA = nullptr;
-  const char* baseB = nullptr;
+  __amdgpu_buffer_rsrc_t rsA = crc, rsB = crc;  // set at the first stage
   int src_tile = -1;
   auto origin = [&](int ti, int64_t& m0, int64_t& n0) __attribute__((always_inline)) {
     const int wg = tile_index_virtual(p, bid + ti * nblk, ntiles);
@@ -1575,28 +1585,41 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     m0 = (int64_t)tm_ * 256;
     n0 = (int64_t)tn_ * 256;
   };
+  // Tile origins are computed once per tile, at its start, for the tile itself (stores) and for
+  // the next one (staging runs up to two K-tiles ahead, arrival gate): the index maps' integer
+  // divisions would otherwise be inlined at every stage / store site (code size, I-cache).
+  int64_t cm0 = 0, cn0 = 0, nm0 = 0, nn0 = 0;
+  origin(0, nm0, nn0);
   struct Cur { int ti, kt; };
   auto adv = [&](Cur& c) __attribute__((always_inline)) {
     if (c.ti == my_tiles - 1 && c.kt == nk - 1) return;
     if (++c.kt == nk) { c.kt = 0; ++c.ti; }
   };
-  auto stage = [&](int which, int unit_off, Cur c, int buf) __attribute__((always_inline)) {
-    if (c.ti != src_tile) {
-      int64_t m0, n0;
-      origin(c.ti, m0, n0);
-      baseA = (const char*)p.a + m0 * p.lda * esz;
-      baseB = (const char*)p.b + n0 * p.ldb * esz;
+  // LDS unit (X = 0 A / 1 B, buffer, half q)
+  auto uoff = [](int X, int buf, int q) constexpr { return X * 65536 + buf * 32768 + q * 16384; };
+  auto stage = [&](int X, int q, int buf, Cur c) __attribute__((always_inline)) {
+    if (c.ti != src_tile) {  // always the next tile (nm0, nn0)
+      rsA = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.a + nm0 * p.lda * esz), 0,
+                                              0x7FFFFFF0, 0x00020000);
+      rsB = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.b + nn0 * p.ldb * esz), 0,
+                                              0x7FFFFFF0, 0x00020000);
       src_tile = c.ti;
     }
-    const char* base = (which < 2 ? baseA : baseB) + (int64_t)c.kt * ROWB;
-    const unsigned* off = which < 2 ? offA[which] : offB[which - 2];
-    char* dst = smem + buf * STAGE + unit_off + wave * 16 * ROWB;
-    glds16(base + off[0], dst);
-    glds16(base + off[1], dst + 8 * ROWB);
+    const unsigned* off = X == 0 ? offA[q] : offB[q];
+    char* dst = smem + uoff(X, buf, q) + wave * 16 * ROWB;
+    const unsigned soff = (unsigned)(c.kt * ROWB);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(X == 0 ? rsA : rsB, (LDS_AS void*)dst, 16, off[0],
+                                             soff, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(X == 0 ? rsA : rsB, (LDS_AS void*)(dst + 8 * ROWB),
+                                             16, off[1], soff, 0, 0);
   };
   const int frow = lane & 15, fq = lane >> 4, sw = (frow >> 1) & 7;
   const int c0 = ((0 + fq) ^ sw) * 16, c1 = ((4 + fq) ^ sw) * 16;
-  const int aoff = (wr * 64 + frow) * ROWB, boff = (wc * 32 + frow) * ROWB;
+  unsigned rA0 = (wr * 64 + frow) * ROWB + c0, rA1 = (wr * 64 + frow) * ROWB + c1;
+  unsigned rB0 = 65536 + (wc * 32 + frow) * ROWB + c0, rB1 = 65536 + (wc * 32 + frow) * ROWB + c1;
+  // opaque bases: otherwise the B base's 64K can be re-associated into a read's constant, which
+  // then no longer fits the ds_read offset field (a VGPR per read)
+  asm volatile("" : "+v"(rA0), "+v"(rA1), "+v"(rB0), "+v"(rB1));
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -1604,38 +1627,44 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   i32x4 aR[4][2], bR[2][2][2];
   i32x8 aP[4], bP[2][2];
-  auto loadA = [&](const char* base, int mq) __attribute__((always_inline)) {
-    const char* r = base + (mq ? UA1 : UA0) + aoff;
+  auto loadA = [&](auto bufc, int mq) __attribute__((always_inline)) {
+    constexpr int BUF = decltype(bufc)::value;
 #pragma unroll
     for (int f = 0; f < 4; ++f) {
+      const int o = uoff(0, BUF, mq) + f * 16 * ROWB;
       if constexpr (PAIR) {
-        aP[f].lo = *(const i32x4*)(r + f * 16 * ROWB + c0);
-        aP[f].hi = *(const i32x4*)(r + f * 16 * ROWB + c1);
+        aP[f].lo = *(const i32x4*)(smem + rA0 + o);
+        aP[f].hi = *(const i32x4*)(smem + rA1 + o);
       } else {
-        aR[f][0] = *(const i32x4*)(r + f * 16 * ROWB + c0);
-        aR[f][1] = *(const i32x4*)(r + f * 16 * ROWB + c1);
+        aR[f][0] = *(const i32x4*)(smem + rA0 + o);
+        aR[f][1] = *(const i32x4*)(smem + rA1 + o);
       }
     }
   };
-  auto loadB = [&](const char* base, int nq) __attribute__((always_inline)) {
-    const char* r = base + (nq ? UB1 : UB0) + boff;
+  auto loadB = [&](auto bufc, int nq) __attribute__((always_inline)) {
+    constexpr int BUF = decltype(bufc)::value;
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
+      const int o = uoff(0, BUF, nq) + g * 16 * ROWB;  // rB0 / rB1 carry the B region's 64K
       if constexpr (PAIR) {
-        bP[nq][g].lo = *(const i32x4*)(r + g * 16 * ROWB + c0);
-        bP[nq][g].hi = *(const i32x4*)(r + g * 16 * ROWB + c1);
+        bP[nq][g].lo = *(const i32x4*)(smem + rB0 + o);
+        bP[nq][g].hi = *(const i32x4*)(smem + rB1 + o);
       } else {
-        bR[nq][g][0] = *(const i32x4*)(r + g * 16 * ROWB + c0);
-        bR[nq][g][1] = *(const i32x4*)(r + g * 16 * ROWB + c1);
+        bR[nq][g][0] = *(const i32x4*)(smem + rB0 + o);
+        bR[nq][g][1] = *(const i32x4*)(smem + rB1 + o);
       }
     }
   };
-  auto mm = [&](int mq, int nq) __attribute__((always_inline)) {
+  // zero: the tile's first K-tile; each accumulator's first MFMA takes an inline-zero C operand
+  auto mm = [&](int mq, int nq, bool zero) __attribute__((always_inline)) {
     if constexpr (PAIR) {
 #pragma unroll
       for (int f = 0; f < 4; ++f)
 #pragma unroll
-        for (int g = 0; g < 2; ++g) Mma::step8(acc[mq * 4 + f][nq * 2 + g], bP[nq][g], aP[f]);
+        for (int g = 0; g < 2; ++g) {
+          if (zero) acc[mq * 4 + f][nq * 2 + g] = f32x4{0.f, 0.f, 0.f, 0.f};
+          Mma::step8(acc[mq * 4 + f][nq * 2 + g], bP[nq][g], aP[f]);
+        }
 #pragma unroll
       for (int f = 0; f < 4; ++f)  // pin the pure scaled MFMAs in this section (see t8)
 #pragma unroll
@@ -1646,34 +1675,34 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
 #pragma unroll
         for (int f = 0; f < 4; ++f)
 #pragma unroll
-          for (int g = 0; g < 2; ++g)
+          for (int g = 0; g < 2; ++g) {
+            if (zero && kk == 0) acc[mq * 4 + f][nq * 2 + g] = f32x4{0.f, 0.f, 0.f, 0.f};
             Mma::step(acc[mq * 4 + f][nq * 2 + g], bR[nq][g][kk], aR[f][kk]);
+          }
     }
   };
   int ti = 0;
+  // CMODE 2: the lane's part of a C offset (fixed) and the wave-uniform part per fragment row
+  const unsigned c_lane = (unsigned)(((wr * 128 + frow) * p.ldc + wc * 64 + fq * 8) * OSZ);
+  // (no fused activation: pt4_ok routes those GEMMs to t4, keeping pt4's code small)
   auto store_q = [&](int mq, int nq) __attribute__((always_inline)) {
-    int64_t m0, n0;
-    origin(ti, m0, n0);
+    const int64_t m0 = cm0, n0 = cn0;
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int f = 0; f < 4; ++f) {
       const int i = mq * 4 + f;
-      const int64_t row = m0 + wr * 128 + mq * 64 + f * 16 + frow;
-      char* dst = c_row<OSZ, CMODE == 1 ? 1 : 0>(p, row) +
-                  (n0 + wc * 64 + nq * 32 + fq * 8) * OSZ;
-      // one store site (two branch-local stores get merged by the optimizer, which drops the
-      // non-temporal hint)
-      f32x4 v0 = acc[i][nq * 2], v1 = acc[i][nq * 2 + 1];
-      if (p.act != ACT_NONE) {
-        v0 = act4(v0, p.act);
-        v1 = act4(v1, p.act);
-      }
-      if constexpr (CMODE == 2)
-        store8_wt<OUT>(crc, (unsigned)(dst - (char*)p.c), v0, v1);
-      else
+      const f32x4 v0 = acc[i][nq * 2], v1 = acc[i][nq * 2 + 1];
+      if constexpr (CMODE == 2) {
+        // grouped C rows: a tile's 256 rows stay contiguous (launch_pt4: c_grp % 256 == 0)
+        const int64_t prow = m0 + mq * 64 + f * 16;  // cm0: already the physical row
+        const unsigned soff = (unsigned)((prow * p.ldc + n0 + nq * 32) * OSZ);
+        store8_wt<OUT>(crc, c_lane, v0, v1, soff);
+      } else {
+        const int64_t row = m0 + wr * 128 + mq * 64 + f * 16 + frow;
+        char* dst = c_row<OSZ, CMODE == 1 ? 1 : 0>(p, row) +
+                    (n0 + wc * 64 + nq * 32 + fq * 8) * OSZ;
         Store8<OUT>::st(dst, v0, v1);
-      acc[i][nq * 2] = f32x4{0.f, 0.f, 0.f, 0.f};
-      acc[i][nq * 2 + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -1685,51 +1714,47 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   } while (0)
 #define T4_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
   const bool g1 = wr == 1;  // wave-uniform (wave came through readfirstlane)
-  if constexpr (GATED) {  // arrival gate of the first tile, before any staging
-    int64_t m0, n0;
-    origin(0, m0, n0);
-    wait_flag(p, m0, m0 + 255);
-  }
+  if constexpr (GATED) wait_flag(p, nm0, nm0 + 255);  // arrival gate of the first tile
   Cur q0{0, 0}, q1{0, 0};
   adv(q1);
-  stage(2, UB0, q0, 0);
-  stage(3, UB1, q0, 0);
-  stage(0, UA0, q0, 0);
-  stage(1, UA1, q0, 0);
-  stage(2, UB0, q1, 1);
-  stage(3, UB1, q1, 1);
+  stage(1, 0, 0, q0);
+  stage(1, 1, 0, q0);
+  stage(0, 0, 0, q0);
+  stage(0, 1, 0, q0);
+  stage(1, 0, 1, q1);
+  stage(1, 1, 1, q1);
   Cur qa = q1, qb = q1;  // K-tile h+1 (A units, phase A) and h+2 (B units, phase B)
   adv(qb);
   wait_vm<6>();
   T4_BAR();
   if (g1) T4_BAR();
-  // KIND: 0 normal, 1 last K-tile of a tile, 2 first K-tile after a tile's last
-  auto iter = [&](int h, auto kind_tag) __attribute__((always_inline)) {
+  // KIND: 0 normal, 1 last K-tile of a tile, 2 first K-tile after a tile's last; BUF: the
+  // buffer this K-tile reads (A units of the next K-tile go to the other one, B units of the
+  // one after next to this one)
+  auto iter = [&](auto bufc, auto kind_tag) __attribute__((always_inline)) {
     constexpr int KIND = decltype(kind_tag)::value;
-    const int b = h & 1;
-    const char* cur = smem + b * STAGE;
+    constexpr int BUF = decltype(bufc)::value;
+    constexpr bool Z = KIND == 2;
     if (GATED && qa.kt == 0) {
       // Arrival gate: this iteration stages the first A K-tile of tile qa.ti. Thread 0 spins on
       // the flags of its rows and acquires; one extra barrier, executed by every wave at this
       // same point (qa is workgroup-uniform), orders all waves' A staging after it. Both wave
       // groups insert it at the same place, so their one-barrier stagger is unchanged; an extra
       // barrier only adds ordering (LDS RAW / WAR distances grow).
-      int64_t m0, n0;
-      origin(qa.ti, m0, n0);
-      wait_flag_t0(p, m0, m0 + 255);
+      wait_flag_t0(p, nm0, nm0 + 255);  // qa.ti is the next tile (or tile 0)
       T4_BAR();
     }
-    loadB(cur, 0);  // phase A
-    loadB(cur, 1);
-    loadA(cur, 0);
-    stage(0, UA0, qa, b ^ 1);
-    stage(1, UA1, qa, b ^ 1);
+    loadB(bufc, 0);  // phase A
+    loadB(bufc, 1);
+    loadA(bufc, 0);
+    stage(0, 0, BUF ^ 1, qa);
+    stage(0, 1, BUF ^ 1, qa);
     T4_LGKM0();
     if (g1) wait_vm<KIND == 2 ? 8 + 4 * NS : 8>();
     T4_BAR();
     __builtin_amdgcn_s_setprio(1);
-    mm(0, 0);
-    mm(0, 1);
+    mm(0, 0, Z);
+    mm(0, 1, Z);
     __builtin_amdgcn_s_setprio(0);
     if constexpr (KIND == 1) {
       store_q(0, 0);
@@ -1737,15 +1762,15 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     }
     if (!g1) wait_vm<KIND == 1 ? 8 + 2 * NS : (KIND == 2 ? 8 + 4 * NS : 8)>();
     T4_BAR();
-    loadA(cur, 1);  // phase B
-    stage(2, UB0, qb, b);
-    stage(3, UB1, qb, b);
+    loadA(bufc, 1);  // phase B
+    stage(1, 0, BUF, qb);
+    stage(1, 1, BUF, qb);
     T4_LGKM0();
     if (g1) wait_vm<KIND == 1 ? 6 + 2 * NS : 6>();
     T4_BAR();
     __builtin_amdgcn_s_setprio(1);
-    mm(1, 1);
-    mm(1, 0);
+    mm(1, 1, Z);
+    mm(1, 0, Z);
     __builtin_amdgcn_s_setprio(0);
     if constexpr (KIND == 1) {
       store_q(1, 1);
@@ -1756,18 +1781,25 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     qa = qb;
     adv(qb);
   };
-  int h = 0;
-  for (ti = 0; ti < my_tiles; ++ti) {
-    int t = 0;
-    if (ti > 0) {
-      iter(h, std::integral_constant<int, 2>{});
-      ++h;
-      ++t;
+  using B0 = std::integral_constant<int, 0>;
+  using B1 = std::integral_constant<int, 1>;
+  using K0 = std::integral_constant<int, 0>;
+  using K1 = std::integral_constant<int, 1>;
+  auto tile_body = [&](auto first_kind) __attribute__((always_inline)) {
+    cm0 = nm0;  // this tile (C rows: physical, grouped C rows keep a tile contiguous)
+    cn0 = nn0;
+    if constexpr (CMODE == 2) cm0 = map_row(cm0, p.c_grp, p.c_gstride);
+    if (ti + 1 < my_tiles) origin(ti + 1, nm0, nn0);
+    iter(B0{}, first_kind);  // K-tile 0
+    for (int t = 1; t + 2 < nk; t += 2) {
+      iter(B1{}, K0{});
+      iter(B0{}, K0{});
     }
-    for (; t < nk - 1; ++t, ++h) iter(h, std::integral_constant<int, 0>{});
-    iter(h, std::integral_constant<int, 1>{});
-    ++h;
-  }
+    iter(B1{}, K1{});  // K-tile nk - 1 (nk even)
+  };
+  ti = 0;
+  tile_body(K0{});
+  for (ti = 1; ti < my_tiles; ++ti) tile_body(std::integral_constant<int, 2>{});
   if (!g1) T4_BAR();
 #undef T4_BAR
 #undef T4_LGKM0
@@ -2259,11 +2291,14 @@ hipError_t launch_t4(const GemmArgs& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-// pt4 needs >= 2 K-tiles per tile (its FIRST and LAST K-tile kinds are distinct), plain A rows
-// and 32-bit panel offsets
+// pt4 needs an even number (>= 2) of K-tiles per tile (its FIRST and LAST K-tile kinds are
+// distinct, its body is unrolled by buffer parity), plain A rows, 32-bit panel offsets (a
+// 256-row panel, the reach of its LDS-DMA buffer descriptors, stays below 1 GiB) and no fused
+// activation (t4 carries those)
 bool pt4_ok(const GemmArgs& p, int esz) {
-  return p.M % 256 == 0 && p.N % 256 == 0 && p.a_table == nullptr &&
-         p.a_grp == p.M && (int64_t)p.K * esz / 128 >= 2 && p.lda * esz <= (1 << 22) &&
+  const int64_t nk = (int64_t)p.K * esz / 128;
+  return p.M % 256 == 0 && p.N % 256 == 0 && p.a_table == nullptr && p.act == ACT_NONE &&
+         p.a_grp == p.M && nk >= 2 && nk % 2 == 0 && p.lda * esz <= (1 << 22) &&
          p.ldb * esz <= (1 << 22);
 }
 
@@ -2287,7 +2322,8 @@ hipError_t launch_pt4(const GemmArgs& p, hipStream_t s) {
   grid = (grid / 8) * 8;  // blockIdx % 8 == XCD group for every virtual tile id
   if (grid > tiles) grid = tiles;
   if (grid < 1) grid = 1;
-  const bool wt = c_fits_wt(p, out_size<OUT>());
+  // write-through stores address C from a per-tile scalar row (the tile's rows contiguous)
+  const bool wt = c_fits_wt(p, out_size<OUT>()) && p.c_grp % 256 == 0;
   if (p.flags != nullptr && wt)
     hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, true, 2>), dim3(grid + q.ag_ctas), dim3(512),
                        0, s, q);

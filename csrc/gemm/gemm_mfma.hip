@@ -122,7 +122,8 @@ hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mo
     const int esz = dtype_size(din);
     if (p.flags == nullptr || p.a_table != nullptr || mode == GEMM_MODE_GENERIC ||
         !gemm_fast_path_ok(p, din, dout) || p.M % 256 || p.N % 256 || p.a_grp != p.M ||
-        (int64_t)p.K * esz / 128 < 2 || p.lda * esz > (1 << 22) || p.ldb * esz > (1 << 22) ||
+        (int64_t)p.K * esz / 128 < 2 || ((int64_t)p.K * esz / 128) % 2 != 0 || p.act != ACT_NONE ||
+        p.lda * esz > (1 << 22) || p.ldb * esz > (1 << 22) ||
         p.nsub < 1 || p.nshards % p.nsub || p.nshards / p.nsub > 32 || p.ag_parts < 1 ||
         p.ag_tab == nullptr || p.flag_rows * p.lda * esz / p.ag_parts >= (int64_t(1) << 30))
       return hipErrorNotSupported;  // (a copy unit is addressed by one 32-bit buffer descriptor)

@@ -195,10 +195,10 @@ def check_columnwise(d: int, m: int, n: int, k: int, cfg: AlgoConfig, ein: int =
         raise ValueError("fused=True (one arrival-flag-gated GEMM) applies to backend=ipc, "
                          "order=AG_before, p2p_pipeline / coll_pipeline")
     if (cfg.fused and cfg.protocol == "kernel" and cfg.algorithm == "coll_pipeline" and d > 1
-            and (m % 256 or n % 256 or k * ein % 128 or k * ein < 256)):
+            and (m % 256 or n % 256 or k * ein % 256 or k * ein < 256 or cfg.act)):
         raise ValueError("the in-kernel all-gather (coll_pipeline, fused, kernel copies) runs on "
-                         "the persistent 256x256 GEMM: m and n multiples of 256, k rows of "
-                         "whole 128-byte K-tiles")
+                         "the persistent 256x256 GEMM: m and n multiples of 256, k rows of an "
+                         "even number of 128-byte K-tiles, no fused activation")
     if d > 17:
         raise ValueError("at most 17 ranks per node are supported by the flag/reduce ops")
 

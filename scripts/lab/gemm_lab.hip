@@ -1595,8 +1595,9 @@ __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
     constexpr int KIND = decltype(kind_tag)::value;
     const int b = h & 1;
     const char* cur = smem + b * STAGE;
+    // SKIP & 65536 (timing only, wrong results): balanced reads, phase A B0 + A0, phase B B1 + A1
     loadB(cur, 0);  // phase A
-    loadB(cur, 1);
+    if constexpr ((SKIP & 65536) == 0) loadB(cur, 1);
     loadA(cur, 0);
     T(0);
     stage(0, UA0, qa, b ^ 1);
@@ -1632,6 +1633,7 @@ __global__ __launch_bounds__(512) void pt4_kernel(const Args p) {
     T4_BAR();
     T(8);
     loadA(cur, 1);  // phase B
+    if constexpr ((SKIP & 65536) != 0) loadB(cur, 1);
     T(3);
     stage(2, UB0, qb, b);
     stage(3, UB1, qb, b);
@@ -2055,6 +2057,529 @@ __global__ __launch_bounds__(256) void q4_kernel(const Args p) {  // 2 no loop b
 }
 
 // fp32 reference: C[m][n] = sum_k A[m][k] * B[n][k]
+// ---------------------------------------------------------------------------------------------
+// pt4v: pt4 (nt | sc1 write-through C stores, as the product's CMODE 2) with VALU-free load
+// phases. Stamps (r3_20/r3_21) showed phase A's load segment ~550 cycles longer than phase B's
+// with equal read counts: its head carried the buffer-parity VGPR address arithmetic (a 16-bit
+// ds offset cannot reach the second 64 KB buffer) and the LDS-DMA 64-bit address math, and VALU
+// at the head of a segment costs the un-prioritized wave ~90 cycles each (MI355X_MICROARCH.md,
+// two waves per SIMD, item 6). V bits:
+//   1: LDS = [A units of both buffers | B units of both buffers]: every fragment read is a fixed
+//      per-lane VGPR + compile-time offset (< 64 KB); the K-tile body is instantiated per parity
+//   2: LDS-DMA through buffer descriptors: per-tile SGPR base, K offset in soffset, fixed
+//      per-lane voffset (no per-stage VALU)
+//   4: C stores through SGPR soffsets (fixed per-lane voffset)
+//   8: a tile's first MFMA of each accumulator takes a zero C operand (no v_mov zeroing)
+template <int V>
+__device__ constexpr int pt4v_uoff(int X, int buf, int q) {
+  return (V & 1) ? X * 65536 + buf * 32768 + q * 16384 : buf * 65536 + X * 32768 + q * 16384;
+}
+
+template <bool STAMP, int V>
+__global__ __launch_bounds__(512) void pt4v_kernel(const Args p) {
+  constexpr int ROWB = 128, UNIT = 128 * ROWB;
+  constexpr int NS = 4;
+  __shared__ __attribute__((aligned(1024))) char smem[8 * UNIT];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int tiles_n = p.N / 256, ntiles = (p.M / 256) * tiles_n;
+  const int nk = p.K / 64;
+  const int my_tiles =
+      ((int)blockIdx.x < ntiles) ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  if (my_tiles == 0) return;
+  const int drow = lane >> 3, dpc = lane & 7;
+  unsigned offA[2][2], offB[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int ur = wave * 16 + i * 8 + drow;
+    const int ch = (dpc ^ ((ur >> 1) & 7)) * 16;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int lr = (ur >> 6) * 128 + q * 64 + (ur & 63);
+      offA[q][i] = (unsigned)(lr * p.lda * 2 + ch);
+      const int lc = (ur >> 5) * 64 + q * 32 + t8_perm(ur & 31);
+      offB[q][i] = (unsigned)(lc * p.ldb * 2 + ch);
+    }
+  }
+  const char* baseA = nullptr;
+  const char* baseB = nullptr;
+  __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)p.a, 0, 0x7FFFFFF0, 0x00020000);
+  __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)p.b, 0, 0x7FFFFFF0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t crc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.c, 0, 0x7FFFFFF0, 0x00020000);
+  int src_tile = -1;
+  auto origin = [&](int ti, int64_t& m0, int64_t& n0) __attribute__((always_inline)) {
+    const int wg = xcd_remap((int)blockIdx.x + ti * (int)gridDim.x, ntiles);
+    m0 = (int64_t)(wg / tiles_n) * 256;
+    n0 = (int64_t)(wg % tiles_n) * 256;
+  };
+  struct Cur { int ti, kt; };
+  auto adv = [&](Cur& c) __attribute__((always_inline)) {
+    if (c.ti == my_tiles - 1 && c.kt == nk - 1) return;
+    if (++c.kt == nk) { c.kt = 0; ++c.ti; }
+  };
+  auto stage = [&](int which, int buf, Cur c) __attribute__((always_inline)) {
+    if (c.ti != src_tile) {
+      int64_t m0, n0;
+      origin(c.ti, m0, n0);
+      baseA = (const char*)p.a + m0 * p.lda * 2;
+      baseB = (const char*)p.b + n0 * p.ldb * 2;
+      if constexpr ((V & 2) != 0) {
+        rsA = __builtin_amdgcn_make_buffer_rsrc((void*)baseA, 0, 0x7FFFFFF0, 0x00020000);
+        rsB = __builtin_amdgcn_make_buffer_rsrc((void*)baseB, 0, 0x7FFFFFF0, 0x00020000);
+      }
+      src_tile = c.ti;
+    }
+    const int X = which < 2 ? 0 : 1, q = which & 1;
+    const unsigned* off = X == 0 ? offA[q] : offB[q];
+    char* dst = smem + pt4v_uoff<V>(X, buf, q) + wave * 16 * ROWB;
+    if constexpr ((V & 2) != 0) {
+      const unsigned soff = (unsigned)(c.kt * ROWB);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(X == 0 ? rsA : rsB, (LDS_AS void*)dst, 16, off[0],
+                                               soff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(X == 0 ? rsA : rsB, (LDS_AS void*)(dst + 8 * ROWB),
+                                               16, off[1], soff, 0, 0);
+    } else {
+      const char* base = (X == 0 ? baseA : baseB) + (int64_t)c.kt * ROWB;
+      glds16(base + off[0], dst);
+      glds16(base + off[1], dst + 8 * ROWB);
+    }
+  };
+  const int frow = lane & 15, fq = lane >> 4, sw = (frow >> 1) & 7;
+  const int c0 = ((0 + fq) ^ sw) * 16, c1 = ((4 + fq) ^ sw) * 16;
+  const int aoff = (wr * 64 + frow) * ROWB, boff = (wc * 32 + frow) * ROWB;
+  const unsigned rA0 = aoff + c0, rA1 = aoff + c1;
+  const unsigned rB0 = ((V & 1) ? 0 : 0) + boff + c0, rB1 = boff + c1;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  i32x4 aR[4][2], bR[2][2][2];
+  auto loadA = [&](auto bufc, int mq) __attribute__((always_inline)) {
+    constexpr int BUF = decltype(bufc)::value;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const int o = pt4v_uoff<V>(0, BUF, mq) + f * 16 * ROWB;
+      aR[f][0] = *(const i32x4*)(smem + rA0 + o);
+      aR[f][1] = *(const i32x4*)(smem + rA1 + o);
+    }
+  };
+  auto loadB = [&](auto bufc, int nq) __attribute__((always_inline)) {
+    constexpr int BUF = decltype(bufc)::value;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const int o = pt4v_uoff<V>(1, BUF, nq) + g * 16 * ROWB;
+      bR[nq][g][0] = *(const i32x4*)(smem + rB0 + o);
+      bR[nq][g][1] = *(const i32x4*)(smem + rB1 + o);
+    }
+  };
+  auto mm = [&](int mq, int nq, bool zero) __attribute__((always_inline)) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          f32x4& a = acc[mq * 4 + f][nq * 2 + g];
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8, bR[nq][g][kk]), __builtin_bit_cast(bf16x8, aR[f][kk]),
+              (zero && kk == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : a, 0, 0, 0);
+        }
+  };
+  int ti = 0;
+  const unsigned c_lane = (unsigned)(((wr * 128 + frow) * p.ldc + wc * 64 + fq * 8) * 2);
+  auto store_frag = [&](int mq, int nq, int f, int sti) __attribute__((always_inline)) {
+    const int i = mq * 4 + f;
+    int64_t m0, n0;
+    origin(sti, m0, n0);
+    const f32x4 v0 = acc[i][nq * 2], v1 = acc[i][nq * 2 + 1];
+    bf16x8 o = {(__bf16)v0.x, (__bf16)v0.y, (__bf16)v0.z, (__bf16)v0.w,
+                (__bf16)v1.x, (__bf16)v1.y, (__bf16)v1.z, (__bf16)v1.w};
+    typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
+    if constexpr ((V & 4) != 0) {
+      const unsigned soff = (unsigned)(((m0 + mq * 64 + f * 16) * p.ldc + n0) * 2 + nq * 64);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), crc, c_lane, soff, 18);
+    } else {
+      char* crow = (char*)p.c + (m0 + wr * 128 + mq * 64 + f * 16 + frow) * p.ldc * 2;
+      const char* dst = crow + (n0 + wc * 64 + nq * 32 + fq * 8) * 2;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), crc,
+                                             (unsigned)(dst - (const char*)p.c), 0, 18);
+    }
+    if constexpr ((V & 8) == 0) {
+      acc[i][nq * 2] = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc[i][nq * 2 + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto store_q = [&](int mq, int nq, int sti) __attribute__((always_inline)) {
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) store_frag(mq, nq, f, sti);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+#define T4_BAR()                         \
+  do {                                   \
+    __builtin_amdgcn_sched_barrier(0);   \
+    __builtin_amdgcn_s_barrier();        \
+    __builtin_amdgcn_sched_barrier(0);   \
+  } while (0)
+#define T4_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+  const bool g1 = wr == 1;
+  unsigned long long st[16] = {}, tprev = 0;
+  auto T = [&](int bucket) __attribute__((always_inline)) {
+    if constexpr (STAMP) {
+      __builtin_amdgcn_sched_barrier(0);
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
+      if (bucket >= 0) st[bucket] += t - tprev;
+      tprev = t;
+    }
+  };
+  Cur q0{0, 0}, q1{0, 0};
+  adv(q1);
+  stage(2, 0, q0);
+  stage(3, 0, q0);
+  stage(0, 0, q0);
+  stage(1, 0, q0);
+  stage(2, 1, q1);
+  stage(3, 1, q1);
+  Cur qa = q1, qb = q1;
+  adv(qb);
+  wait_vm<6>();
+  T4_BAR();
+  if (g1) T4_BAR();
+  T(-1);
+  const unsigned long long t_start = tprev;
+  auto iter = [&](auto bufc, auto kind_tag) __attribute__((always_inline)) {
+    constexpr int KIND = decltype(kind_tag)::value;
+    constexpr int BUF = decltype(bufc)::value;
+    constexpr bool Z = (V & 8) != 0 && KIND == 2;
+    if constexpr ((V & 16) != 0) {  // timing only: phase A reads A0 + A1, phase B B0 + B1
+      loadA(bufc, 0);
+#pragma unroll
+      for (int f = 0; f < 4; ++f) asm volatile("" ::"v"(aR[f][0]), "v"(aR[f][1]));
+      loadA(bufc, 1);
+    } else {
+      loadB(bufc, 0);  // phase A
+      loadB(bufc, 1);
+      loadA(bufc, 0);
+    }
+    T(0);
+    stage(0, BUF ^ 1, qa);
+    stage(1, BUF ^ 1, qa);
+    T(1);
+    T4_LGKM0();
+    T(2);
+    if (g1) wait_vm<KIND == 2 ? 8 + 4 * NS : 8>();
+    T(6);
+    T4_BAR();
+    T(7);
+    __builtin_amdgcn_s_setprio(1);
+    mm(0, 0, Z);
+    mm(0, 1, Z);
+    __builtin_amdgcn_s_setprio(0);
+    T(11);
+    if constexpr (KIND == 1) { store_q(0, 0, ti); store_q(0, 1, ti); }
+    T(13);
+    if (!g1) wait_vm<KIND == 1 ? 8 + 2 * NS : (KIND == 2 ? 8 + 4 * NS : 8)>();
+    T(6);
+    T4_BAR();
+    T(8);
+    if constexpr ((V & 16) != 0) {
+      loadB(bufc, 0);
+      loadB(bufc, 1);
+    } else {
+      loadA(bufc, 1);  // phase B
+    }
+    T(3);
+    stage(2, BUF, qb);
+    stage(3, BUF, qb);
+    T(4);
+    T4_LGKM0();
+    T(5);
+    if (g1) wait_vm<KIND == 1 ? 6 + 2 * NS : 6>();
+    T(6);
+    T4_BAR();
+    T(9);
+    __builtin_amdgcn_s_setprio(1);
+    mm(1, 1, Z);
+    mm(1, 0, Z);
+    __builtin_amdgcn_s_setprio(0);
+    T(12);
+    if constexpr (KIND == 1) { store_q(1, 1, ti); store_q(1, 0, ti); }
+    T(13);
+    if (!g1) wait_vm<KIND == 1 ? 6 + 4 * NS : 6>();
+    T(6);
+    T4_BAR();
+    T(10);
+    qa = qb;
+    adv(qb);
+  };
+  // buffer parity is static by position: every tile has an even number (>= 4) of K-tiles, so
+  // each tile starts in buffer 0 and its body is unrolled by two (a run-time parity branch
+  // between two instantiations made the register allocator spill ~250 VGPRs)
+  using B0 = std::integral_constant<int, 0>;
+  using B1 = std::integral_constant<int, 1>;
+  using K0 = std::integral_constant<int, 0>;
+  using K1 = std::integral_constant<int, 1>;
+  auto tile_body = [&](auto first_kind) __attribute__((always_inline)) {
+    iter(B0{}, first_kind);
+    iter(B1{}, K0{});
+    for (int t = 2; t < nk - 2; t += 2) {
+      iter(B0{}, K0{});
+      iter(B1{}, K0{});
+    }
+    iter(B0{}, K0{});
+    iter(B1{}, K1{});
+  };
+  ti = 0;
+  tile_body(K0{});
+  for (ti = 1; ti < my_tiles; ++ti) tile_body(std::integral_constant<int, 2>{});
+  if (!g1) T4_BAR();
+#undef T4_BAR
+#undef T4_LGKM0
+  wait_vm<0>();
+  if constexpr (STAMP) {
+    T(-1);
+    st[14] = tprev - t_start;
+    if (lane == 0) {
+      unsigned long long* o = p.stamps + ((size_t)blockIdx.x * 8 + wave) * 16;
+#pragma unroll
+      for (int j = 0; j < 15; ++j) o[j] = st[j];
+      o[15] = (unsigned long long)my_tiles;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// pt4k: pt4v15 with the K-tile split by K HALVES instead of M / N halves: phase A reads the first
+// 32 K of every fragment (8 A + 4 B ds_reads, 32 MFMAs), phase B the second 32 (the same), so the
+// two load phases are equal (pt4: 16 / 8 reads). LDS regions (X, buf, h) of 256 rows x 64 B
+// (X * 64K + buf * 32K + h * 16K; chunks swizzled by swz64); a region is restaged as soon as both
+// wave groups have read it: phase A of K-tile t stages the h = 1 regions of t + 1, phase B the
+// h = 0 regions of t + 2 (6 intervals of DMA lead for both). vmcnt: 8 per wait, + 16 (the tile's
+// C stores, all issued after its last MFMA B) at the two waits behind them.
+template <bool STAMP>
+__global__ __launch_bounds__(512) void pt4k_kernel(const Args p) {
+  constexpr int ROWB = 128, HB = 64;  // bytes per K-tile row / per K-half row
+  constexpr int NSQ = 16;             // C store instructions per wave per tile (bf16)
+  __shared__ __attribute__((aligned(1024))) char smem[131072];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int tiles_n = p.N / 256, ntiles = (p.M / 256) * tiles_n;
+  const int nk = p.K / 64;
+  const int my_tiles =
+      ((int)blockIdx.x < ntiles) ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  if (my_tiles == 0) return;
+  // DMA: a wave fills rows wave * 32 .. + 31 of a region, 16 rows x 64 B per instruction
+  const int drow = lane >> 2, dch = lane & 3;
+  unsigned offA[2], offB[2];  // [i]; K half h adds h * 64 in the instruction's offset field
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = wave * 32 + i * 16 + drow;
+    const int col = (r & ~31) + t8_perm(r & 31);
+    const int ch = (dch ^ swz64(r)) * 16;
+    offA[i] = (unsigned)(r * p.lda * 2 + ch);
+    offB[i] = (unsigned)(col * p.ldb * 2 + ch);
+  }
+  __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)p.a, 0, 0x7FFFFFF0, 0x00020000);
+  __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)p.b, 0, 0x7FFFFFF0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t crc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.c, 0, 0x7FFFFFF0, 0x00020000);
+  int src_tile = -1;
+  auto origin = [&](int ti, int64_t& m0, int64_t& n0) __attribute__((always_inline)) {
+    const int wg = xcd_remap((int)blockIdx.x + ti * (int)gridDim.x, ntiles);
+    m0 = (int64_t)(wg / tiles_n) * 256;
+    n0 = (int64_t)(wg % tiles_n) * 256;
+  };
+  struct Cur { int ti, kt; };
+  auto adv = [&](Cur& c) __attribute__((always_inline)) {
+    if (c.ti == my_tiles - 1 && c.kt == nk - 1) return;
+    if (++c.kt == nk) { c.kt = 0; ++c.ti; }
+  };
+  auto reg = [](int X, int buf, int h) constexpr { return X * 65536 + buf * 32768 + h * 16384; };
+  // both regions (A and B) of K-half h of K-tile c into buffer buf: 4 instructions per wave
+  auto stage = [&](int buf, auto hc, Cur c) __attribute__((always_inline)) {
+    constexpr int h = decltype(hc)::value;
+    if (c.ti != src_tile) {
+      int64_t m0, n0;
+      origin(c.ti, m0, n0);
+      rsA = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.a + m0 * p.lda * 2), 0,
+                                              0x7FFFFFF0, 0x00020000);
+      rsB = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.b + n0 * p.ldb * 2), 0,
+                                              0x7FFFFFF0, 0x00020000);
+      src_tile = c.ti;
+    }
+    const unsigned soff = (unsigned)(c.kt * ROWB);
+#pragma unroll
+    for (int X = 0; X < 2; ++X) {
+      // the instruction offset (h * 64, the K half) moves the LDS destination too: start that
+      // much lower so the 64-byte rows land in place
+      char* dst = smem + reg(X, buf, h) + wave * 32 * HB - h * HB;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(X == 0 ? rsA : rsB,
+                                                 (LDS_AS void*)(dst + i * 16 * HB), 16,
+                                                 X == 0 ? offA[i] : offB[i], soff, h * HB, 0);
+    }
+  };
+  const int frow = lane & 15, fq = lane >> 4;
+  const int fch = (fq ^ swz64(frow)) * 16;
+  unsigned rA = (wr * 128 + frow) * HB + fch, rB = 65536 + (wc * 64 + frow) * HB + fch;
+  // opaque bases: otherwise the B base's 64K is re-associated into the per-read constant, which
+  // then no longer fits the ds_read offset field (a VGPR per read, spilled)
+  asm volatile("" : "+v"(rA), "+v"(rB));
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  i32x4 aR[8], bR[4];
+  auto load = [&](auto bufc, auto hc) __attribute__((always_inline)) {
+    constexpr int BUF = decltype(bufc)::value, H = decltype(hc)::value;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) bR[g] = *(const i32x4*)(smem + rB + reg(0, BUF, H) + g * 16 * HB);
+#pragma unroll
+    for (int f = 0; f < 8; ++f) aR[f] = *(const i32x4*)(smem + rA + reg(0, BUF, H) + f * 16 * HB);
+  };
+  auto mm = [&](bool zero) __attribute__((always_inline)) {
+#pragma unroll
+    for (int f = 0; f < 8; ++f)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            __builtin_bit_cast(bf16x8, bR[g]), __builtin_bit_cast(bf16x8, aR[f]),
+            zero ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[f][g], 0, 0, 0);
+  };
+  int ti = 0;
+  const unsigned c_lane = (unsigned)(((wr * 128 + frow) * p.ldc + wc * 64 + fq * 8) * 2);
+  auto store_tile = [&]() __attribute__((always_inline)) {
+    int64_t m0, n0;
+    origin(ti, m0, n0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int f = 0; f < 8; ++f)
+#pragma unroll
+      for (int nq = 0; nq < 2; ++nq) {
+        const f32x4 v0 = acc[f][nq * 2], v1 = acc[f][nq * 2 + 1];
+        bf16x8 o = {(__bf16)v0.x, (__bf16)v0.y, (__bf16)v0.z, (__bf16)v0.w,
+                    (__bf16)v1.x, (__bf16)v1.y, (__bf16)v1.z, (__bf16)v1.w};
+        typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
+        const unsigned soff = (unsigned)(((m0 + f * 16) * p.ldc + n0) * 2 + nq * 64);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), crc, c_lane, soff, 18);
+      }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+#define T4_BAR()                         \
+  do {                                   \
+    __builtin_amdgcn_sched_barrier(0);   \
+    __builtin_amdgcn_s_barrier();        \
+    __builtin_amdgcn_sched_barrier(0);   \
+  } while (0)
+#define T4_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+  const bool g1 = wr == 1;
+  unsigned long long st[16] = {}, tprev = 0;
+  auto T = [&](int bucket) __attribute__((always_inline)) {
+    if constexpr (STAMP) {
+      __builtin_amdgcn_sched_barrier(0);
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
+      if (bucket >= 0) st[bucket] += t - tprev;
+      tprev = t;
+    }
+  };
+  using H0 = std::integral_constant<int, 0>;
+  using H1 = std::integral_constant<int, 1>;
+  Cur q0{0, 0}, q1{0, 0};
+  adv(q1);
+  stage(0, H0{}, q0);  // "D_B(-2)": K-tile 0, h = 0
+  stage(0, H1{}, q0);  // "D_A(-1)": K-tile 0, h = 1
+  stage(1, H0{}, q1);  // "D_B(-1)": K-tile 1, h = 0
+  Cur qa = q1, qb = q1;  // qa: K-tile t + 1 (phase A stages its h = 1), qb: t + 2 (h = 0)
+  adv(qb);
+  wait_vm<8>();
+  T4_BAR();
+  if (g1) T4_BAR();
+  T(-1);
+  const unsigned long long t_start = tprev;
+  auto iter = [&](auto bufc, auto kind_tag) __attribute__((always_inline)) {
+    constexpr int KIND = decltype(kind_tag)::value;
+    constexpr int BUF = decltype(bufc)::value;
+    constexpr bool Z = KIND == 2;
+    load(bufc, H0{});  // phase A: K half 0
+    T(0);
+    stage(BUF ^ 1, H1{}, qa);
+    T(1);
+    T4_LGKM0();
+    T(2);
+    if (g1) wait_vm<KIND == 2 ? 8 + NSQ : 8>();
+    T(6);
+    T4_BAR();
+    T(7);
+    __builtin_amdgcn_s_setprio(1);
+    mm(Z);
+    __builtin_amdgcn_s_setprio(0);
+    T(11);
+    if (!g1) wait_vm<KIND == 2 ? 8 + NSQ : 8>();
+    T(6);
+    T4_BAR();
+    T(8);
+    load(bufc, H1{});  // phase B: K half 1
+    T(3);
+    stage(BUF, H0{}, qb);
+    T(4);
+    T4_LGKM0();
+    T(5);
+    if (g1) wait_vm<8>();
+    T(6);
+    T4_BAR();
+    T(9);
+    __builtin_amdgcn_s_setprio(1);
+    mm(false);
+    __builtin_amdgcn_s_setprio(0);
+    T(12);
+    if constexpr (KIND == 1) store_tile();
+    T(13);
+    if (!g1) wait_vm<KIND == 1 ? 8 + NSQ : 8>();
+    T(6);
+    T4_BAR();
+    T(10);
+    qa = qb;
+    adv(qb);
+  };
+  using B0 = std::integral_constant<int, 0>;
+  using B1 = std::integral_constant<int, 1>;
+  using K0 = std::integral_constant<int, 0>;
+  using K1 = std::integral_constant<int, 1>;
+  auto tile_body = [&](auto first_kind) __attribute__((always_inline)) {
+    iter(B0{}, first_kind);
+    for (int t = 1; t + 2 < nk; t += 2) {
+      iter(B1{}, K0{});
+      iter(B0{}, K0{});
+    }
+    iter(B1{}, K1{});
+  };
+  ti = 0;
+  tile_body(K0{});
+  for (ti = 1; ti < my_tiles; ++ti) tile_body(std::integral_constant<int, 2>{});
+  if (!g1) T4_BAR();
+#undef T4_BAR
+#undef T4_LGKM0
+  wait_vm<0>();
+  if constexpr (STAMP) {
+    T(-1);
+    st[14] = tprev - t_start;
+    if (lane == 0) {
+      unsigned long long* o = p.stamps + ((size_t)blockIdx.x * 8 + wave) * 16;
+#pragma unroll
+      for (int j = 0; j < 15; ++j) o[j] = st[j];
+      o[15] = (unsigned long long)my_tiles;
+    }
+  }
+}
+
 __global__ void ref_kernel(const __hip_bfloat16* A, const __hip_bfloat16* B, float* C, int M, int N,
                            int K) {
   __shared__ float as[16][65], bs[16][65];
@@ -2134,6 +2659,14 @@ int main(int argc, char** argv) {
       {"pt4 noDMA", pt4_kernel<false, 1>, 2, 512, 0},
       {"pt4 noMFMA", pt4_kernel<false, 4>, 2, 512, 0},
       {"pt4 nt", pt4_kernel<false, 16>, 2, 512, 0},
+      {"pt4 nt bal", pt4_kernel<false, 16 | 65536>, 2, 512, 0},
+      {"pt4v0", pt4v_kernel<false, 0>, 2, 512, 0},
+      {"pt4v1", pt4v_kernel<false, 1>, 2, 512, 0},
+      {"pt4v3", pt4v_kernel<false, 3>, 2, 512, 0},
+      {"pt4v7", pt4v_kernel<false, 7>, 2, 512, 0},
+      {"pt4v15", pt4v_kernel<false, 15>, 2, 512, 0},
+      {"pt4v15 AfirstBsecond", pt4v_kernel<false, 31>, 2, 512, 0},
+      {"pt4k", pt4k_kernel<false>, 2, 512, 0},
       {"pt4 nt stag2", pt4_kernel<false, 16 | 64>, 2, 512, 0},
       {"pt4 nt stag6", pt4_kernel<false, 16 | 128>, 2, 512, 0},
       {"pt4 nt stag4ph", pt4_kernel<false, 16 | 192>, 2, 512, 0},
@@ -2218,7 +2751,18 @@ int main(int argc, char** argv) {
     s.stamps = stamps;
     for (int i = 0; i < 50; ++i) hipLaunchKernelGGL((pt4_kernel<false, 16>), dim3(grid), dim3(512), 0, 0, a);
     CHECK(hipMemset(stamps, 0, ((size_t)grid * 8 * 16 + 8) * 8));
-    hipLaunchKernelGGL((pt4_kernel<true, 16>), dim3(grid), dim3(512), 0, 0, s);
+    if (getenv("LAB_STAMP")[0] == 'b')
+      hipLaunchKernelGGL((pt4_kernel<true, 16 | 65536>), dim3(grid), dim3(512), 0, 0, s);
+    else if (getenv("LAB_STAMP")[0] == 'v')
+      hipLaunchKernelGGL((pt4v_kernel<true, 15>), dim3(grid), dim3(512), 0, 0, s);
+    else if (getenv("LAB_STAMP")[0] == 'w')
+      hipLaunchKernelGGL((pt4v_kernel<true, 0>), dim3(grid), dim3(512), 0, 0, s);
+    else if (getenv("LAB_STAMP")[0] == 'k')
+      hipLaunchKernelGGL((pt4k_kernel<true>), dim3(grid), dim3(512), 0, 0, s);
+    else if (getenv("LAB_STAMP")[0] == 'x')
+      hipLaunchKernelGGL((pt4v_kernel<true, 31>), dim3(grid), dim3(512), 0, 0, s);
+    else
+      hipLaunchKernelGGL((pt4_kernel<true, 16>), dim3(grid), dim3(512), 0, 0, s);
     CHECK(hipDeviceSynchronize());
     std::vector<unsigned long long> h((size_t)grid * 8 * 16);
     CHECK(hipMemcpy(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost));
