@@ -40,7 +40,22 @@ struct Args {
   int64_t lda, ldb, ldc;
   int M, N, K;
   unsigned long long* stamps;  // optional per-wave cycle breakdown
+  int raster = 0;              // pt4v / pt4d: tile raster groups of this many m-blocks (product tile_mn)
 };
+
+// the product's tile raster (csrc/gemm/tile_map.h tile_mn, G m-blocks per group)
+__device__ __forceinline__ void lab_tile_mn(int wg, int tiles_m, int tiles_n, int G, int64_t& m0,
+                                            int64_t& n0) {
+  if (G <= 0 || tiles_n <= 4) {
+    m0 = (int64_t)(wg / tiles_n) * 256;
+    n0 = (int64_t)(wg % tiles_n) * 256;
+    return;
+  }
+  const int per = G * tiles_n, grp = wg / per, first = grp * G;
+  const int gs = tiles_m - first < G ? tiles_m - first : G, in = wg - grp * per;
+  m0 = (int64_t)(first + in % gs) * 256;
+  n0 = (int64_t)(in / gs) * 256;
+}
 
 __device__ __forceinline__ void glds16(const void* g, void* lds) {
   __builtin_amdgcn_global_load_lds((const GLB_AS void*)g, (LDS_AS void*)lds, 16, 0, 0);
@@ -2111,8 +2126,7 @@ __global__ __launch_bounds__(512) void pt4v_kernel(const Args p) {
   int src_tile = -1;
   auto origin = [&](int ti, int64_t& m0, int64_t& n0) __attribute__((always_inline)) {
     const int wg = xcd_remap((int)blockIdx.x + ti * (int)gridDim.x, ntiles);
-    m0 = (int64_t)(wg / tiles_n) * 256;
-    n0 = (int64_t)(wg % tiles_n) * 256;
+    lab_tile_mn(wg, p.M / 256, tiles_n, p.raster, m0, n0);
   };
   struct Cur { int ti, kt; };
   auto adv = [&](Cur& c) __attribute__((always_inline)) {
@@ -2636,8 +2650,7 @@ __global__ __launch_bounds__(512) void pt4d_kernel(const Args p) {
   int src_tile = -1;
   auto origin = [&](int ti, int64_t& m0, int64_t& n0) __attribute__((always_inline)) {
     const int wg = xcd_remap((int)blockIdx.x + ti * (int)gridDim.x, ntiles);
-    m0 = (int64_t)(wg / tiles_n) * 256;
-    n0 = (int64_t)(wg % tiles_n) * 256;
+    lab_tile_mn(wg, p.M / 256, tiles_n, p.raster, m0, n0);
   };
   int64_t cm0 = 0, cn0 = 0, nm0 = 0, nn0 = 0;
   origin(0, nm0, nn0);
@@ -2932,7 +2945,7 @@ int main(int argc, char** argv) {
       {"q4 noDMA noBAR", q4_kernel<0, 3>, 2, 256, 1},
       {"q4 noMFMA", q4_kernel<0, 4>, 2, 256, 1},
   };
-  Args a{A, B, C, K, K, N, M, N, K, nullptr};
+  Args a{A, B, C, K, K, N, M, N, K, nullptr, getenv("LAB_RASTER") ? atoi(getenv("LAB_RASTER")) : 0};
   const char* only = getenv("LAB_ONLY");  // comma-separated variant names: skip the others
   auto skip = [&](const char* name) {
     if (!only) return false;
