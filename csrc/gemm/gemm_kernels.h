@@ -1538,6 +1538,14 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   constexpr int NS = 4 * Store8<OUT>::kStores;
   constexpr int OSZ = out_size<OUT>();
   constexpr bool PAIR = is_pair<Mma>::value;
+  // DEFER: the balanced schedule (ungated kernels): phase A reads the first halves (A rows mq = 0,
+  // B cols nq = 0) and computes A0 x B0 plus the previous K-tile's A1 x B1, phase B the second
+  // halves and A0 x B1 + A1 x B0; units are restaged as soon as both wave groups have read them
+  // (6 intervals of DMA lead for every unit). Both halves' fragments stay live (+32 VGPRs, which
+  // the gated kernels' arrival gate and the per-lane C addressing of CMODE 0 / 1 cannot spare:
+  // those keep the 16 / 8-read schedule).
+  constexpr bool DEFER = !GATED && CMODE == 2;
+  constexpr int NH = DEFER ? 2 : 1;  // fragment register sets
   __shared__ __attribute__((aligned(1024))) char smem[8 * UNIT];
   // CMODE 2: C through one wave-uniform descriptor (launch_pt4 checks the extent fits)
   const __amdgpu_buffer_rsrc_t crc =
@@ -1625,19 +1633,20 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  i32x4 aR[4][2], bR[2][2][2];
-  i32x8 aP[4], bP[2][2];
+  i32x4 aR[NH][4][2], bR[2][2][2];  // [A half (DEFER) / 0][frag][k16], [B half][frag][k16]
+  i32x8 aP[NH][4], bP[2][2];
   auto loadA = [&](auto bufc, int mq) __attribute__((always_inline)) {
     constexpr int BUF = decltype(bufc)::value;
+    const int h = DEFER ? mq : 0;
 #pragma unroll
     for (int f = 0; f < 4; ++f) {
       const int o = uoff(0, BUF, mq) + f * 16 * ROWB;
       if constexpr (PAIR) {
-        aP[f].lo = *(const i32x4*)(smem + rA0 + o);
-        aP[f].hi = *(const i32x4*)(smem + rA1 + o);
+        aP[h][f].lo = *(const i32x4*)(smem + rA0 + o);
+        aP[h][f].hi = *(const i32x4*)(smem + rA1 + o);
       } else {
-        aR[f][0] = *(const i32x4*)(smem + rA0 + o);
-        aR[f][1] = *(const i32x4*)(smem + rA1 + o);
+        aR[h][f][0] = *(const i32x4*)(smem + rA0 + o);
+        aR[h][f][1] = *(const i32x4*)(smem + rA1 + o);
       }
     }
   };
@@ -1657,13 +1666,14 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   };
   // zero: the tile's first K-tile; each accumulator's first MFMA takes an inline-zero C operand
   auto mm = [&](int mq, int nq, bool zero) __attribute__((always_inline)) {
+    const int h = DEFER ? mq : 0;
     if constexpr (PAIR) {
 #pragma unroll
       for (int f = 0; f < 4; ++f)
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
           if (zero) acc[mq * 4 + f][nq * 2 + g] = f32x4{0.f, 0.f, 0.f, 0.f};
-          Mma::step8(acc[mq * 4 + f][nq * 2 + g], bP[nq][g], aP[f]);
+          Mma::step8(acc[mq * 4 + f][nq * 2 + g], bP[nq][g], aP[h][f]);
         }
 #pragma unroll
       for (int f = 0; f < 4; ++f)  // pin the pure scaled MFMAs in this section (see t8)
@@ -1677,7 +1687,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
 #pragma unroll
           for (int g = 0; g < 2; ++g) {
             if (zero && kk == 0) acc[mq * 4 + f][nq * 2 + g] = f32x4{0.f, 0.f, 0.f, 0.f};
-            Mma::step(acc[mq * 4 + f][nq * 2 + g], bR[nq][g][kk], aR[f][kk]);
+            Mma::step(acc[mq * 4 + f][nq * 2 + g], bR[nq][g][kk], aR[h][f][kk]);
           }
     }
   };
@@ -1717,67 +1727,121 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   if constexpr (GATED) wait_flag(p, nm0, nm0 + 255);  // arrival gate of the first tile
   Cur q0{0, 0}, q1{0, 0};
   adv(q1);
-  stage(1, 0, 0, q0);
-  stage(1, 1, 0, q0);
-  stage(0, 0, 0, q0);
-  stage(0, 1, 0, q0);
-  stage(1, 0, 1, q1);
-  stage(1, 1, 1, q1);
-  Cur qa = q1, qb = q1;  // K-tile h+1 (A units, phase A) and h+2 (B units, phase B)
+  if constexpr (DEFER) {
+    stage(0, 0, 0, q0);  // halves 0 of K-tile 0 ("phase B of K-tile -2")
+    stage(1, 0, 0, q0);
+    stage(0, 1, 0, q0);  // halves 1 of K-tile 0 ("phase A of K-tile -1")
+    stage(1, 1, 0, q0);
+    stage(0, 0, 1, q1);  // halves 0 of K-tile 1 ("phase B of K-tile -1")
+    stage(1, 0, 1, q1);
+  } else {
+    stage(1, 0, 0, q0);
+    stage(1, 1, 0, q0);
+    stage(0, 0, 0, q0);
+    stage(0, 1, 0, q0);
+    stage(1, 0, 1, q1);
+    stage(1, 1, 1, q1);
+  }
+  // DEFER: qa = K-tile t+1 (halves 1, phase A), qb = t+2 (halves 0, phase B); otherwise qa = t+1
+  // (A units, phase A), qb = t+2 (B units, phase B)
+  Cur qa = q1, qb = q1;
   adv(qb);
-  wait_vm<6>();
+  wait_vm<DEFER ? 8 : 6>();
   T4_BAR();
   if (g1) T4_BAR();
-  // KIND: 0 normal, 1 last K-tile of a tile, 2 first K-tile after a tile's last; BUF: the
-  // buffer this K-tile reads (A units of the next K-tile go to the other one, B units of the
-  // one after next to this one)
+  // KIND: 0 normal, 1 last K-tile of a tile, 2 first K-tile after a tile's last, 4 the kernel's
+  // first K-tile (DEFER: no deferred product, no stores counted); BUF: the buffer this K-tile
+  // reads. vmcnt counts keep exactly the DMA (and C stores) issued after the units the next phase
+  // reads in flight; stores count in issue order with the DMA.
   auto iter = [&](auto bufc, auto kind_tag) __attribute__((always_inline)) {
     constexpr int KIND = decltype(kind_tag)::value;
     constexpr int BUF = decltype(bufc)::value;
-    constexpr bool Z = KIND == 2;
-    if (GATED && qa.kt == 0) {
-      // Arrival gate: this iteration stages the first A K-tile of tile qa.ti. Thread 0 spins on
-      // the flags of its rows and acquires; one extra barrier, executed by every wave at this
-      // same point (qa is workgroup-uniform), orders all waves' A staging after it. Both wave
-      // groups insert it at the same place, so their one-barrier stagger is unchanged; an extra
-      // barrier only adds ordering (LDS RAW / WAR distances grow).
-      wait_flag_t0(p, nm0, nm0 + 255);  // qa.ti is the next tile (or tile 0)
+    constexpr bool Z = KIND == 2 || KIND == 4;
+    if constexpr (DEFER) {
+      constexpr bool DEF = KIND == 0 || KIND == 1;  // the previous K-tile's A1 x B1
+      loadB(bufc, 0);  // phase A: halves 0
+      loadA(bufc, 0);
+      stage(0, 1, BUF ^ 1, qa);
+      stage(1, 1, BUF ^ 1, qa);
+      T4_LGKM0();
+      if (g1) wait_vm<KIND == 2 ? 8 + 3 * NS : 8>();
+      T4_BAR();
+      __builtin_amdgcn_s_setprio(1);
+      if constexpr (DEF) mm(1, 1, false);
+      mm(0, 0, Z);
+      __builtin_amdgcn_s_setprio(0);
+      if constexpr (KIND == 1) store_q(0, 0);
+      if (!g1) wait_vm<KIND == 2 ? 8 + 3 * NS : (KIND == 1 ? 8 + NS : 8)>();
+      T4_BAR();
+      loadB(bufc, 1);  // phase B: halves 1
+      loadA(bufc, 1);
+      stage(0, 0, BUF, qb);
+      stage(1, 0, BUF, qb);
+      T4_LGKM0();
+      if (g1) wait_vm<KIND == 1 ? 8 + NS : 8>();
+      T4_BAR();
+      __builtin_amdgcn_s_setprio(1);
+      mm(0, 1, Z);
+      mm(1, 0, Z);
+      if constexpr (KIND == 1) mm(1, 1, false);
+      __builtin_amdgcn_s_setprio(0);
+      if constexpr (KIND == 1) {
+        store_q(0, 1);
+        store_q(1, 0);
+        store_q(1, 1);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {  // the next tile's first A1 x B1 is a deferred product
+          acc[4 + f][2] = f32x4{0.f, 0.f, 0.f, 0.f};
+          acc[4 + f][3] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+      if (!g1) wait_vm<KIND == 1 ? 8 + 4 * NS : 8>();
+      T4_BAR();
+    } else {
+      if (GATED && qa.kt == 0) {
+        // Arrival gate: this iteration stages the first A K-tile of tile qa.ti. Thread 0 spins on
+        // the flags of its rows and acquires; one extra barrier, executed by every wave at this
+        // same point (qa is workgroup-uniform), orders all waves' A staging after it. Both wave
+        // groups insert it at the same place, so their one-barrier stagger is unchanged; an extra
+        // barrier only adds ordering (LDS RAW / WAR distances grow).
+        wait_flag_t0(p, nm0, nm0 + 255);  // qa.ti is the next tile (or tile 0)
+        T4_BAR();
+      }
+      loadB(bufc, 0);  // phase A
+      loadB(bufc, 1);
+      loadA(bufc, 0);
+      stage(0, 0, BUF ^ 1, qa);
+      stage(0, 1, BUF ^ 1, qa);
+      T4_LGKM0();
+      if (g1) wait_vm<KIND == 2 ? 8 + 4 * NS : 8>();
+      T4_BAR();
+      __builtin_amdgcn_s_setprio(1);
+      mm(0, 0, Z);
+      mm(0, 1, Z);
+      __builtin_amdgcn_s_setprio(0);
+      if constexpr (KIND == 1) {
+        store_q(0, 0);
+        store_q(0, 1);
+      }
+      if (!g1) wait_vm<KIND == 1 ? 8 + 2 * NS : (KIND == 2 ? 8 + 4 * NS : 8)>();
+      T4_BAR();
+      loadA(bufc, 1);  // phase B
+      stage(1, 0, BUF, qb);
+      stage(1, 1, BUF, qb);
+      T4_LGKM0();
+      if (g1) wait_vm<KIND == 1 ? 6 + 2 * NS : 6>();
+      T4_BAR();
+      __builtin_amdgcn_s_setprio(1);
+      mm(1, 1, Z);
+      mm(1, 0, Z);
+      __builtin_amdgcn_s_setprio(0);
+      if constexpr (KIND == 1) {
+        store_q(1, 1);
+        store_q(1, 0);
+      }
+      if (!g1) wait_vm<KIND == 1 ? 6 + 4 * NS : 6>();
       T4_BAR();
     }
-    loadB(bufc, 0);  // phase A
-    loadB(bufc, 1);
-    loadA(bufc, 0);
-    stage(0, 0, BUF ^ 1, qa);
-    stage(0, 1, BUF ^ 1, qa);
-    T4_LGKM0();
-    if (g1) wait_vm<KIND == 2 ? 8 + 4 * NS : 8>();
-    T4_BAR();
-    __builtin_amdgcn_s_setprio(1);
-    mm(0, 0, Z);
-    mm(0, 1, Z);
-    __builtin_amdgcn_s_setprio(0);
-    if constexpr (KIND == 1) {
-      store_q(0, 0);
-      store_q(0, 1);
-    }
-    if (!g1) wait_vm<KIND == 1 ? 8 + 2 * NS : (KIND == 2 ? 8 + 4 * NS : 8)>();
-    T4_BAR();
-    loadA(bufc, 1);  // phase B
-    stage(1, 0, BUF, qb);
-    stage(1, 1, BUF, qb);
-    T4_LGKM0();
-    if (g1) wait_vm<KIND == 1 ? 6 + 2 * NS : 6>();
-    T4_BAR();
-    __builtin_amdgcn_s_setprio(1);
-    mm(1, 1, Z);
-    mm(1, 0, Z);
-    __builtin_amdgcn_s_setprio(0);
-    if constexpr (KIND == 1) {
-      store_q(1, 1);
-      store_q(1, 0);
-    }
-    if (!g1) wait_vm<KIND == 1 ? 6 + 4 * NS : 6>();
-    T4_BAR();
     qa = qb;
     adv(qb);
   };
@@ -1798,7 +1862,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     iter(B1{}, K1{});  // K-tile nk - 1 (nk even)
   };
   ti = 0;
-  tile_body(K0{});
+  tile_body(std::integral_constant<int, DEFER ? 4 : 0>{});
   for (ti = 1; ti < my_tiles; ++ti) tile_body(std::integral_constant<int, 2>{});
   if (!g1) T4_BAR();
 #undef T4_BAR
