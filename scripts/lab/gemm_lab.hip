@@ -2279,10 +2279,20 @@ __global__ __launch_bounds__(512) void pt4v_kernel(const Args p) {
   if (g1) T4_BAR();
   T(-1);
   const unsigned long long t_start = tprev;
+  // V & 1024: static priority (waves 4-7 at 1 for the whole kernel, no per-phase flips);
+  // V & 4096: no s_setprio at all
+  constexpr bool FLIP = (V & (1024 | 4096)) == 0;
+  if constexpr ((V & 1024) != 0) {
+    if (g1) __builtin_amdgcn_s_setprio(1);
+  }
   auto iter = [&](auto bufc, auto kind_tag) __attribute__((always_inline)) {
     constexpr int KIND = decltype(kind_tag)::value;
     constexpr int BUF = decltype(bufc)::value;
     constexpr bool Z = (V & 8) != 0 && KIND == 2;
+    if constexpr ((V & 2048) != 0) {  // the LDS-DMA pieces first, then the fragment reads
+      stage(0, BUF ^ 1, qa);
+      stage(1, BUF ^ 1, qa);
+    }
     if constexpr ((V & 16) != 0) {  // timing only: phase A reads A0 + A1, phase B B0 + B1
       loadA(bufc, 0);
 #pragma unroll
@@ -2294,8 +2304,10 @@ __global__ __launch_bounds__(512) void pt4v_kernel(const Args p) {
       loadA(bufc, 0);
     }
     T(0);
-    stage(0, BUF ^ 1, qa);
-    stage(1, BUF ^ 1, qa);
+    if constexpr ((V & 2048) == 0) {
+      stage(0, BUF ^ 1, qa);
+      stage(1, BUF ^ 1, qa);
+    }
     T(1);
     T4_LGKM0();
     T(2);
@@ -2303,10 +2315,10 @@ __global__ __launch_bounds__(512) void pt4v_kernel(const Args p) {
     T(6);
     T4_BAR();
     T(7);
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr (FLIP) __builtin_amdgcn_s_setprio(1);
     mm(0, 0, Z);
     mm(0, 1, Z);
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (FLIP) __builtin_amdgcn_s_setprio(0);
     T(11);
     if constexpr (KIND == 1) { store_q(0, 0, ti); store_q(0, 1, ti); }
     T(13);
@@ -2314,6 +2326,10 @@ __global__ __launch_bounds__(512) void pt4v_kernel(const Args p) {
     T(6);
     T4_BAR();
     T(8);
+    if constexpr ((V & 2048) != 0) {
+      stage(2, BUF, qb);
+      stage(3, BUF, qb);
+    }
     if constexpr ((V & 16) != 0) {
       loadB(bufc, 0);
       loadB(bufc, 1);
@@ -2321,8 +2337,10 @@ __global__ __launch_bounds__(512) void pt4v_kernel(const Args p) {
       loadA(bufc, 1);  // phase B
     }
     T(3);
-    stage(2, BUF, qb);
-    stage(3, BUF, qb);
+    if constexpr ((V & 2048) == 0) {
+      stage(2, BUF, qb);
+      stage(3, BUF, qb);
+    }
     T(4);
     T4_LGKM0();
     T(5);
@@ -2330,10 +2348,10 @@ __global__ __launch_bounds__(512) void pt4v_kernel(const Args p) {
     T(6);
     T4_BAR();
     T(9);
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr (FLIP) __builtin_amdgcn_s_setprio(1);
     mm(1, 1, Z);
     mm(1, 0, Z);
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (FLIP) __builtin_amdgcn_s_setprio(0);
     T(12);
     if constexpr (KIND == 1) { store_q(1, 1, ti); store_q(1, 0, ti); }
     T(13);
@@ -2913,6 +2931,9 @@ int main(int argc, char** argv) {
       {"pt4v15 AfirstBsecond", pt4v_kernel<false, 31>, 2, 512, 0},
       {"pt4k", pt4k_kernel<false>, 2, 512, 0},
       {"pt4d", pt4d_kernel<false>, 2, 512, 0},
+      {"pt4v15 staticprio", pt4v_kernel<false, 15 | 1024>, 2, 512, 0},
+      {"pt4v15 noprio", pt4v_kernel<false, 15 | 4096>, 2, 512, 0},
+      {"pt4v15 dmafirst", pt4v_kernel<false, 15 | 2048>, 2, 512, 0},
       {"pt4v15 noST", pt4v_kernel<false, 15 | 64>, 2, 512, 0},
       {"pt4v15 noLDSrd", pt4v_kernel<false, 15 | 128>, 2, 512, 0},
       {"pt4v15 noMFMA", pt4v_kernel<false, 15 | 256>, 2, 512, 0},

@@ -359,3 +359,45 @@ def test_gemm_long_k_tight(dt, tile, gen):
     ref = _ref(a, w)
     err = float((out.float() - ref).abs().max())
     assert err <= _tight_bound(ref, K), (err, _tight_bound(ref, K))
+
+
+@pytest.mark.parametrize("dt", [(torch.bfloat16, torch.bfloat16, "auto"),
+                                (torch.bfloat16, torch.float32, "auto"),
+                                (torch.float8_e4m3fn, torch.bfloat16, "mx")],
+                         ids=lambda d: f"{str(d[0])[6:]}-{str(d[1])[6:]}-{d[2]}")
+@pytest.mark.parametrize("kt", [2, 3, 4, 5, 6, 12])
+def test_pt4_k_tile_counts(dt, kt, gen):
+    """pt4's tile body is unrolled by LDS-buffer parity (an even number of 128-byte K-tiles; odd
+    counts go to t4) and its write-through form runs the DEFER schedule, whose K-tile kinds
+    (first of the kernel, first after a tile, last, deferred A1 x B1) all meet within 2 - 12
+    K-tiles and 8 tiles per persistent block; repeat-identical."""
+    from ddlb_amd.ops.gemm import gemm
+
+    din, dout, mode = dt
+    K = kt * 128 // din.itemsize
+    M, N = 2048 * 8, 256 * 8  # 512 tiles: two per persistent block
+    a, w = _rand((M, K), din, gen), _rand((N, K), din, gen)
+    out = gemm(a, w, tile="pt4", out_dtype=dout, mode=mode)
+    torch.cuda.synchronize()
+    ref = _ref(a, w)
+    err = float((out.float() - ref).abs().max())
+    assert err <= _tight_bound(ref, K), (err, K)
+    again = gemm(a, w, tile="pt4", out_dtype=dout, mode=mode)
+    torch.cuda.synchronize()
+    assert torch.equal(out, again)
+
+
+def test_pt4_flagship_race_screen(gen):
+    """The flagship shape on pt4 (DEFER schedule, 4 tiles per block) 30 times, bit for bit: a
+    new sync structure is screened over many runs (cdna_hip_programming.md §5, 8-phase notes)."""
+    from ddlb_amd.ops.gemm import gemm
+
+    a, w = _rand((65536, 1024), torch.bfloat16, gen), _rand((1024, 1024), torch.bfloat16, gen)
+    first = gemm(a, w, tile="pt4").clone()
+    out = torch.empty_like(first)
+    for _ in range(30):
+        gemm(a, w, out, tile="pt4")
+        torch.cuda.synchronize()
+        assert torch.equal(out, first)
+    ref = _ref(a, w)
+    assert float((first.float() - ref).abs().max()) <= _tight_bound(ref, 1024)
