@@ -290,3 +290,18 @@ def test_in_kernel_allgather_ack_protocol_negative():
     sim = Simulator(plans, make_buffers(plans))
     with pytest.raises(Deadlock):
         sim.run_epoch()
+
+
+def test_in_kernel_allgather_shape_rules():
+    """The gated persistent pt4 kernel that carries the in-kernel all-gather unrolls its tile body
+    by LDS-buffer parity (an even number of 128-byte K-tiles) and has no fused activation: the
+    plan builder refuses other configs instead of failing in the launch."""
+    cfg = AlgoConfig(algorithm="coll_pipeline", backend="ipc", fused=True, s=2, protocol="kernel",
+                     copy_blocks=8)
+    build_tp_columnwise(0, 2, 512, 256, 64, DT_F32, DT_F32, cfg)  # 2 K-tiles of f32
+    with pytest.raises(ValueError, match="even number"):
+        build_tp_columnwise(0, 2, 512, 256, 96, DT_F32, DT_F32, cfg)  # 3 K-tiles
+    act = AlgoConfig(algorithm="coll_pipeline", backend="ipc", fused=True, s=2, protocol="kernel",
+                     copy_blocks=8, act=1)
+    with pytest.raises(ValueError, match="activation"):
+        build_tp_columnwise(0, 2, 512, 256, 64, DT_F32, DT_F32, act)
