@@ -2843,6 +2843,242 @@ __global__ __launch_bounds__(512) void pt4d_kernel(const Args p) {
   wait_vm<0>();
 }
 
+// ---------------------------------------------------------------------------------------------
+// pt4e: pt4d whose second-half fragment reads move into the MFMA phase A (behind the deferred
+// A1 x B1, interleaved with A0 x B0), so load phase B carries only LDS-DMA. Waits move one
+// interval earlier for the halves 1 (5 intervals of DMA lead). Derived from:
+// pt4d: pt4v15 with balanced load phases on 128-byte-row units. Phase A of K-tile t reads the
+// first halves (A rows mq = 0, B cols nq = 0: 8 + 4 ds_reads) and computes A0 x B0 plus the
+// DEFERRED A1 x B1 of K-tile t - 1 (its fragments are still in registers); phase B reads the
+// second halves (8 + 4) and computes A0 x B1 + A1 x B0. A tile's last K-tile does its own A1 x B1
+// in phase B. Fragments of both halves stay live (96 VGPRs). A unit is restaged as soon as both
+// wave groups have read it (phase A(t): halves 1 of K-tile t + 1; phase B(t): halves 0 of t + 2),
+// so every unit gets 6 intervals of DMA lead. KIND 0 normal, 1 last, 2 first after a tile,
+// 4 first of the kernel (no deferred product, no store counts).
+template <bool STAMP>
+__global__ __launch_bounds__(512) void pt4e_kernel(const Args p) {
+  constexpr int ROWB = 128, UNIT = 128 * ROWB;
+  constexpr int NS = 4;  // C store instructions per quadrant per wave (bf16)
+  __shared__ __attribute__((aligned(1024))) char smem[8 * UNIT];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int tiles_n = p.N / 256, ntiles = (p.M / 256) * tiles_n;
+  const int nk = p.K / 64;
+  const int my_tiles =
+      ((int)blockIdx.x < ntiles) ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  if (my_tiles == 0) return;
+  const int drow = lane >> 3, dpc = lane & 7;
+  unsigned offA[2][2], offB[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int ur = wave * 16 + i * 8 + drow;
+    const int ch = (dpc ^ ((ur >> 1) & 7)) * 16;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int lr = (ur >> 6) * 128 + q * 64 + (ur & 63);
+      offA[q][i] = (unsigned)(lr * p.lda * 2 + ch);
+      const int lc = (ur >> 5) * 64 + q * 32 + t8_perm(ur & 31);
+      offB[q][i] = (unsigned)(lc * p.ldb * 2 + ch);
+    }
+  }
+  const __amdgpu_buffer_rsrc_t crc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.c, 0, 0x7FFFFFF0, 0x00020000);
+  __amdgpu_buffer_rsrc_t rsA = crc, rsB = crc;
+  int src_tile = -1;
+  auto origin = [&](int ti, int64_t& m0, int64_t& n0) __attribute__((always_inline)) {
+    const int wg = xcd_remap((int)blockIdx.x + ti * (int)gridDim.x, ntiles);
+    lab_tile_mn(wg, p.M / 256, tiles_n, p.raster, m0, n0);
+  };
+  int64_t cm0 = 0, cn0 = 0, nm0 = 0, nn0 = 0;
+  origin(0, nm0, nn0);
+  struct Cur { int ti, kt; };
+  auto adv = [&](Cur& c) __attribute__((always_inline)) {
+    if (c.ti == my_tiles - 1 && c.kt == nk - 1) return;
+    if (++c.kt == nk) { c.kt = 0; ++c.ti; }
+  };
+  auto uoff = [](int X, int buf, int q) constexpr { return X * 65536 + buf * 32768 + q * 16384; };
+  auto stage = [&](int X, int q, int buf, Cur c) __attribute__((always_inline)) {
+    if (c.ti != src_tile) {
+      rsA = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.a + nm0 * p.lda * 2), 0,
+                                              0x7FFFFFF0, 0x00020000);
+      rsB = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.b + nn0 * p.ldb * 2), 0,
+                                              0x7FFFFFF0, 0x00020000);
+      src_tile = c.ti;
+    }
+    const unsigned* off = X == 0 ? offA[q] : offB[q];
+    char* dst = smem + uoff(X, buf, q) + wave * 16 * ROWB;
+    const unsigned soff = (unsigned)(c.kt * ROWB);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(X == 0 ? rsA : rsB, (LDS_AS void*)dst, 16, off[0],
+                                             soff, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(X == 0 ? rsA : rsB, (LDS_AS void*)(dst + 8 * ROWB),
+                                             16, off[1], soff, 0, 0);
+  };
+  const int frow = lane & 15, fq = lane >> 4, sw = (frow >> 1) & 7;
+  const int c0 = ((0 + fq) ^ sw) * 16, c1 = ((4 + fq) ^ sw) * 16;
+  unsigned rA0 = (wr * 64 + frow) * ROWB + c0, rA1 = (wr * 64 + frow) * ROWB + c1;
+  unsigned rB0 = 65536 + (wc * 32 + frow) * ROWB + c0, rB1 = 65536 + (wc * 32 + frow) * ROWB + c1;
+  asm volatile("" : "+v"(rA0), "+v"(rA1), "+v"(rB0), "+v"(rB1));
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  i32x4 aX[2][4][2], bX[2][2][2];  // [half][frag][k16]
+  auto loadA = [&](auto bufc, int mq) __attribute__((always_inline)) {
+    constexpr int BUF = decltype(bufc)::value;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const int o = uoff(0, BUF, mq) + f * 16 * ROWB;
+      aX[mq][f][0] = *(const i32x4*)(smem + rA0 + o);
+      aX[mq][f][1] = *(const i32x4*)(smem + rA1 + o);
+    }
+  };
+  auto loadB = [&](auto bufc, int nq) __attribute__((always_inline)) {
+    constexpr int BUF = decltype(bufc)::value;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const int o = uoff(0, BUF, nq) + g * 16 * ROWB;
+      bX[nq][g][0] = *(const i32x4*)(smem + rB0 + o);
+      bX[nq][g][1] = *(const i32x4*)(smem + rB1 + o);
+    }
+  };
+  auto mm = [&](int mq, int nq, bool zero) __attribute__((always_inline)) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          f32x4& a = acc[mq * 4 + f][nq * 2 + g];
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8, bX[nq][g][kk]), __builtin_bit_cast(bf16x8, aX[mq][f][kk]),
+              (zero && kk == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : a, 0, 0, 0);
+        }
+  };
+  int ti = 0;
+  const unsigned c_lane = (unsigned)(((wr * 128 + frow) * p.ldc + wc * 64 + fq * 8) * 2);
+  auto store_q = [&](int mq, int nq) __attribute__((always_inline)) {
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const int i = mq * 4 + f;
+      const f32x4 v0 = acc[i][nq * 2], v1 = acc[i][nq * 2 + 1];
+      bf16x8 o = {(__bf16)v0.x, (__bf16)v0.y, (__bf16)v0.z, (__bf16)v0.w,
+                  (__bf16)v1.x, (__bf16)v1.y, (__bf16)v1.z, (__bf16)v1.w};
+      typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
+      const unsigned soff = (unsigned)(((cm0 + mq * 64 + f * 16) * p.ldc + cn0) * 2 + nq * 64);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), crc, c_lane, soff, 18);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+#define T4_BAR()                         \
+  do {                                   \
+    __builtin_amdgcn_sched_barrier(0);   \
+    __builtin_amdgcn_s_barrier();        \
+    __builtin_amdgcn_sched_barrier(0);   \
+  } while (0)
+// lgkmcnt(0) as the builtin (vmcnt / expcnt at their maxima): the compiler's waitcnt pass sees
+// it, so it does not re-wait for the load phase's reads inside the interleaved MFMA phase
+#define T4_LGKM0() __builtin_amdgcn_s_waitcnt(0xC07F)
+  const bool g1 = wr == 1;
+  Cur q0{0, 0}, q1{0, 0};
+  adv(q1);
+  stage(0, 0, 0, q0);  // halves 0 of K-tile 0
+  stage(1, 0, 0, q0);
+  stage(0, 1, 0, q0);  // halves 1 of K-tile 0
+  stage(1, 1, 0, q0);
+  stage(0, 0, 1, q1);  // halves 0 of K-tile 1
+  stage(1, 0, 1, q1);
+  Cur qa = q1, qb = q1;  // qa: K-tile t + 1 (halves 1, phase A), qb: t + 2 (halves 0, phase B)
+  adv(qb);
+  wait_vm<8>();
+  T4_BAR();
+  if (g1) {  // g1's halves 1 of K-tile 0 are read in its first MFMA phase
+    wait_vm<4>();
+    T4_BAR();
+  }
+  auto iter = [&](auto bufc, auto kind_tag) __attribute__((always_inline)) {
+    constexpr int KIND = decltype(kind_tag)::value;
+    constexpr int BUF = decltype(bufc)::value;
+    constexpr bool Z = KIND == 2 || KIND == 4;
+    constexpr bool DEF = KIND == 0 || KIND == 1;  // the previous K-tile's A1 x B1
+    loadB(bufc, 0);  // load phase A: halves 0
+    loadA(bufc, 0);
+    stage(0, 1, BUF ^ 1, qa);
+    stage(1, 1, BUF ^ 1, qa);
+    T4_LGKM0();
+    // the halves 1 of this K-tile are read in the next interval (MFMA A) by this group
+    if (!g1) wait_vm<KIND == 2 ? 8 + 4 * NS : 8>();
+    T4_BAR();
+    __builtin_amdgcn_s_setprio(1);
+    if constexpr (DEF) mm(1, 1, false);  // frees the halves-1 registers
+    __builtin_amdgcn_sched_barrier(0);
+    loadB(bufc, 1);  // halves 1, interleaved with A0 x B0
+    loadA(bufc, 1);
+    mm(0, 0, Z);
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // one ds_read
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(0);
+    if constexpr (KIND == 1) store_q(0, 0);
+    T4_LGKM0();
+    T4_BAR();
+    stage(0, 0, BUF, qb);  // load phase B: LDS-DMA only
+    stage(1, 0, BUF, qb);
+    if (g1) wait_vm<KIND == 1 ? 8 + NS : 8>();
+    T4_BAR();
+    __builtin_amdgcn_s_setprio(1);
+    mm(0, 1, Z);
+    mm(1, 0, Z);
+    if constexpr (KIND == 1) mm(1, 1, false);
+    __builtin_amdgcn_s_setprio(0);
+    if constexpr (KIND == 1) {
+      store_q(0, 1);
+      store_q(1, 0);
+      store_q(1, 1);
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        acc[4 + f][2] = f32x4{0.f, 0.f, 0.f, 0.f};
+        acc[4 + f][3] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    // g0: the halves 0 of the next K-tile (its next load phase); g1: the halves 1 of the next
+    // K-tile, which g0 reads in the interval after this one
+    if (!g1) wait_vm<KIND == 1 ? 8 + 4 * NS : 8>();
+    else wait_vm<KIND == 1 ? 4 + 4 * NS : 4>();
+    T4_BAR();
+    qa = qb;
+    adv(qb);
+  };
+  using B0 = std::integral_constant<int, 0>;
+  using B1 = std::integral_constant<int, 1>;
+  using K0 = std::integral_constant<int, 0>;
+  using K1 = std::integral_constant<int, 1>;
+  auto tile_body = [&](auto first_kind) __attribute__((always_inline)) {
+    cm0 = nm0;
+    cn0 = nn0;
+    if (ti + 1 < my_tiles) origin(ti + 1, nm0, nn0);
+    iter(B0{}, first_kind);
+    for (int t = 1; t + 2 < nk; t += 2) {
+      iter(B1{}, K0{});
+      iter(B0{}, K0{});
+    }
+    iter(B1{}, K1{});
+  };
+  ti = 0;
+  tile_body(std::integral_constant<int, 4>{});
+  for (ti = 1; ti < my_tiles; ++ti) tile_body(std::integral_constant<int, 2>{});
+  if (!g1) T4_BAR();
+#undef T4_BAR
+#undef T4_LGKM0
+  wait_vm<0>();
+}
+
 __global__ void ref_kernel(const __hip_bfloat16* A, const __hip_bfloat16* B, float* C, int M, int N,
                            int K) {
   __shared__ float as[16][65], bs[16][65];
@@ -2931,6 +3167,7 @@ int main(int argc, char** argv) {
       {"pt4v15 AfirstBsecond", pt4v_kernel<false, 31>, 2, 512, 0},
       {"pt4k", pt4k_kernel<false>, 2, 512, 0},
       {"pt4d", pt4d_kernel<false>, 2, 512, 0},
+      {"pt4e", pt4e_kernel<false>, 2, 512, 0},
       {"pt4v15 staticprio", pt4v_kernel<false, 15 | 1024>, 2, 512, 0},
       {"pt4v15 noprio", pt4v_kernel<false, 15 | 4096>, 2, 512, 0},
       {"pt4v15 dmafirst", pt4v_kernel<false, 15 | 2048>, 2, 512, 0},
