@@ -2635,7 +2635,7 @@ __global__ __launch_bounds__(512) void pt4k_kernel(const Args p) {
 // wave groups have read it (phase A(t): halves 1 of K-tile t + 1; phase B(t): halves 0 of t + 2),
 // so every unit gets 6 intervals of DMA lead. KIND 0 normal, 1 last, 2 first after a tile,
 // 4 first of the kernel (no deferred product, no store counts).
-template <bool STAMP>
+template <bool STAMP, bool PRIO = true>
 __global__ __launch_bounds__(512) void pt4d_kernel(const Args p) {
   constexpr int ROWB = 128, UNIT = 128 * ROWB;
   constexpr int NS = 4;  // C store instructions per quadrant per wave (bf16)
@@ -2785,10 +2785,10 @@ __global__ __launch_bounds__(512) void pt4d_kernel(const Args p) {
     T4_LGKM0();
     if (g1) wait_vm<KIND == 2 ? 8 + 3 * NS : 8>();
     T4_BAR();
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
     if constexpr (DEF) mm(1, 1, false);
     mm(0, 0, Z);
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     if constexpr (KIND == 1) store_q(0, 0);
     if (!g1) wait_vm<KIND == 2 ? 8 + 3 * NS : (KIND == 1 ? 8 + NS : 8)>();
     T4_BAR();
@@ -2799,11 +2799,11 @@ __global__ __launch_bounds__(512) void pt4d_kernel(const Args p) {
     T4_LGKM0();
     if (g1) wait_vm<KIND == 1 ? 8 + NS : 8>();
     T4_BAR();
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
     mm(0, 1, Z);
     mm(1, 0, Z);
     if constexpr (KIND == 1) mm(1, 1, false);
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     if constexpr (KIND == 1) {
       store_q(0, 1);
       store_q(1, 0);
@@ -3168,6 +3168,7 @@ int main(int argc, char** argv) {
       {"pt4k", pt4k_kernel<false>, 2, 512, 0},
       {"pt4d", pt4d_kernel<false>, 2, 512, 0},
       {"pt4e", pt4e_kernel<false>, 2, 512, 0},
+      {"pt4d noprio", pt4d_kernel<false, false>, 2, 512, 0},
       {"pt4v15 staticprio", pt4v_kernel<false, 15 | 1024>, 2, 512, 0},
       {"pt4v15 noprio", pt4v_kernel<false, 15 | 4096>, 2, 512, 0},
       {"pt4v15 dmafirst", pt4v_kernel<false, 15 | 2048>, 2, 512, 0},
