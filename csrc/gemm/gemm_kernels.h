@@ -1434,7 +1434,13 @@ __global__ __launch_bounds__(512) void gemm_tn_t4_kernel(const GemmArgs p) {
     __builtin_amdgcn_s_barrier();        \
     __builtin_amdgcn_sched_barrier(0);   \
   } while (0)
-#define T4_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+// compiler-visible lgkmcnt(0) (see pt4)
+#define T4_LGKM0()                            \
+  do {                                        \
+    __builtin_amdgcn_sched_barrier(0);        \
+    __builtin_amdgcn_s_waitcnt(0xC07F);       \
+    __builtin_amdgcn_sched_barrier(0);        \
+  } while (0)
   const bool g1 = wr == 1;  // wave-uniform (wave came through readfirstlane)
   // prologue = the steady-state issue order up to "end of phase B of K-tile -1"
   stage(sB[0], UB0, 0, 0);
@@ -1722,7 +1728,15 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     __builtin_amdgcn_s_barrier();        \
     __builtin_amdgcn_sched_barrier(0);   \
   } while (0)
-#define T4_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+// lgkmcnt(0) through the builtin (vmcnt / expcnt at their maxima, pinned by scheduling
+// barriers): the compiler's waitcnt pass sees it, so it does not re-wait, counted, for reads it
+// believes still in flight at the head of the next MFMA phase
+#define T4_LGKM0()                            \
+  do {                                        \
+    __builtin_amdgcn_sched_barrier(0);        \
+    __builtin_amdgcn_s_waitcnt(0xC07F);       \
+    __builtin_amdgcn_sched_barrier(0);        \
+  } while (0)
   const bool g1 = wr == 1;  // wave-uniform (wave came through readfirstlane)
   if constexpr (GATED) wait_flag(p, nm0, nm0 + 255);  // arrival gate of the first tile
   Cur q0{0, 0}, q1{0, 0};
