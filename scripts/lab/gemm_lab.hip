@@ -1948,6 +1948,12 @@ __global__ __launch_bounds__(256) void q4_kernel(const Args p) {  // 2 no loop b
   const char* baseA = (const char*)p.a + (m0 + (wave >> 1) * 128 + (wave & 1) * 32) * p.lda * 2;
   //                   B unit row -> column (ur>>6)*128 + q*64 + ((ur&63)>>5)*32 + perm(ur&31)
   const char* baseB = (const char*)p.b + (n0 + (wave >> 1) * 128 + (wave & 1) * 32) * p.ldb * 2;
+  // SKIP & 8: LDS-DMA through buffer descriptors on the wave's panel bases (row offsets and the
+  // K offset in soffset, the fixed per-lane swizzled offsets in voffset: no VALU per piece)
+  const __amdgpu_buffer_rsrc_t rqA =
+      __builtin_amdgcn_make_buffer_rsrc((void*)baseA, 0, 0x7FFFFFF0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rqB =
+      __builtin_amdgcn_make_buffer_rsrc((void*)baseB, 0, 0x7FFFFFF0, 0x00020000);
   auto stage_half = [&](int kt, int buf, int half) __attribute__((always_inline)) {
     if ((SKIP & 1) && kt >= 2) return;
     kt = kt < nk ? kt : nk - 1;  // past the end: K-tile nk-1 again into a buffer no one reads
@@ -1956,10 +1962,20 @@ __global__ __launch_bounds__(256) void q4_kernel(const Args p) {  // 2 no loop b
     for (int q = 0; q < 2; ++q)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const char* src = half == 0
-            ? baseA + ((int64_t)(q * 64 + i * 8) * p.lda * 2 + (int64_t)kt * ROWB) + offA[i & 1]
-            : baseB + ((int64_t)(q * 64) * p.ldb * 2 + (int64_t)kt * ROWB) + offB[i];
-        glds16(src, st + (half * 2 + q) * UNIT + i * 8 * ROWB);
+        if constexpr ((SKIP & 8) != 0) {
+          const unsigned soff = half == 0
+              ? (unsigned)((q * 64 + i * 8) * p.lda * 2 + kt * ROWB)
+              : (unsigned)((q * 64) * p.ldb * 2 + kt * ROWB);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(half == 0 ? rqA : rqB,
+                                                   (LDS_AS void*)(st + (half * 2 + q) * UNIT + i * 8 * ROWB),
+                                                   16, (unsigned)(half == 0 ? offA[i & 1] : offB[i]),
+                                                   soff, 0, 0);
+        } else {
+          const char* src = half == 0
+              ? baseA + ((int64_t)(q * 64 + i * 8) * p.lda * 2 + (int64_t)kt * ROWB) + offA[i & 1]
+              : baseB + ((int64_t)(q * 64) * p.ldb * 2 + (int64_t)kt * ROWB) + offB[i];
+          glds16(src, st + (half * 2 + q) * UNIT + i * 8 * ROWB);
+        }
       }
   };
   const int frow = lane & 15, fq = lane >> 4, sw = (frow >> 1) & 7;
@@ -3199,6 +3215,8 @@ int main(int argc, char** argv) {
       {"pt4 wt nt", pt4_kernel<false, 16384 | 16>, 2, 512, 0},
       {"pt4 sc01", pt4_kernel<false, 32768>, 2, 512, 0},
       {"q4", q4_kernel<0>, 2, 256, 1},
+      {"q4 bufdma", q4_kernel<0, 8>, 2, 256, 1},
+      {"q4s1 bufdma", q4_kernel<1, 8>, 2, 256, 1},
       {"q4 noDMA", q4_kernel<0, 1>, 2, 256, 1},
       {"q4 noBAR", q4_kernel<0, 2>, 2, 256, 1},
       {"q4 noDMA noBAR", q4_kernel<0, 3>, 2, 256, 1},
