@@ -2651,7 +2651,7 @@ __global__ __launch_bounds__(512) void pt4k_kernel(const Args p) {
 // wave groups have read it (phase A(t): halves 1 of K-tile t + 1; phase B(t): halves 0 of t + 2),
 // so every unit gets 6 intervals of DMA lead. KIND 0 normal, 1 last, 2 first after a tile,
 // 4 first of the kernel (no deferred product, no store counts).
-template <bool STAMP, bool PRIO = true>
+template <bool STAMP, bool PRIO = true, int STS = 0>
 __global__ __launch_bounds__(512) void pt4d_kernel(const Args p) {
   constexpr int ROWB = 128, UNIT = 128 * ROWB;
   constexpr int NS = 4;  // C store instructions per quadrant per wave (bf16)
@@ -2763,8 +2763,16 @@ __global__ __launch_bounds__(512) void pt4d_kernel(const Args p) {
       bf16x8 o = {(__bf16)v0.x, (__bf16)v0.y, (__bf16)v0.z, (__bf16)v0.w,
                   (__bf16)v1.x, (__bf16)v1.y, (__bf16)v1.z, (__bf16)v1.w};
       typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
-      const unsigned soff = (unsigned)(((cm0 + mq * 64 + f * 16) * p.ldc + cn0) * 2 + nq * 64);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), crc, c_lane, soff, 18);
+      if constexpr (STS == 2) {  // timing only: 32 rows x 32 B per instruction (wrong layout)
+        const int row = wr * 128 + mq * 64 + (f >> 1) * 32 + (lane & 31);
+        const int col = wc * 64 + nq * 32 + (f & 1) * 16 + (lane >> 5) * 8;
+        const unsigned voff = (unsigned)((row * p.ldc + col) * 2);
+        const unsigned soff = (unsigned)((cm0 * p.ldc + cn0) * 2);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), crc, voff, soff, 18);
+      } else {
+        const unsigned soff = (unsigned)(((cm0 + mq * 64 + f * 16) * p.ldc + cn0) * 2 + nq * 64);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), crc, c_lane, soff, 18);
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -3185,6 +3193,7 @@ int main(int argc, char** argv) {
       {"pt4d", pt4d_kernel<false>, 2, 512, 0},
       {"pt4e", pt4e_kernel<false>, 2, 512, 0},
       {"pt4d noprio", pt4d_kernel<false, false>, 2, 512, 0},
+      {"pt4d st32x32", pt4d_kernel<false, true, 2>, 2, 512, 0},
       {"pt4v15 staticprio", pt4v_kernel<false, 15 | 1024>, 2, 512, 0},
       {"pt4v15 noprio", pt4v_kernel<false, 15 | 4096>, 2, 512, 0},
       {"pt4v15 dmafirst", pt4v_kernel<false, 15 | 2048>, 2, 512, 0},
