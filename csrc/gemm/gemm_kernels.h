@@ -1514,11 +1514,14 @@ __global__ __launch_bounds__(512) void gemm_tn_t4_kernel(const GemmArgs p) {
 
 // ---------------------------------------------------------------- pt4: persistent t4
 // t4 streamed across a block's tiles (as pt8 does for t8). A tile's quadrants are stored right
-// after their last MFMAs: Q00 + Q01 after phase A of its last K-tile, Q11 + Q10 after phase B.
-// vmcnt counts (NS = C store instructions per quadrant per wave), per K-tile kind:
-//   normal:             A end 8,        B end 6
-//   LAST of a tile:     A end g0 8+2NS / g1 8,   B end g0 6+4NS / g1 6+2NS
-//   FIRST after a LAST: A end 8+4NS (both),      B end 6
+// after their last MFMAs. Two schedules (see DEFER below):
+//  * 16 / 8 reads (gated, CMODE 0 / 1): Q00 + Q01 after phase A of the tile's last K-tile,
+//    Q11 + Q10 after phase B; vmcnt counts (NS = C store instructions per quadrant per wave):
+//      normal:             A end 8,        B end 6
+//      LAST of a tile:     A end g0 8+2NS / g1 8,   B end g0 6+4NS / g1 6+2NS
+//      FIRST after a LAST: A end 8+4NS (both),      B end 6
+//  * DEFER (12 / 12 reads): Q00 after phase A of the last K-tile, the other three after phase
+//    B; every wait is 8, plus the stores issued after the unit it waits for (iter below).
 // (stores count in issue order with the LDS-DMA; the counts keep exactly the ops issued after
 // the unit the next phase reads in flight).
 // Load phases carry no VALU (round 3, profiles/r03/r3_20..r3_22: the un-prioritized loading wave
@@ -1547,9 +1550,10 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   // DEFER: the balanced schedule (ungated kernels): phase A reads the first halves (A rows mq = 0,
   // B cols nq = 0) and computes A0 x B0 plus the previous K-tile's A1 x B1, phase B the second
   // halves and A0 x B1 + A1 x B0; units are restaged as soon as both wave groups have read them
-  // (6 intervals of DMA lead for every unit). Both halves' fragments stay live (+32 VGPRs, which
-  // the gated kernels' arrival gate and the per-lane C addressing of CMODE 0 / 1 cannot spare:
-  // those keep the 16 / 8-read schedule).
+  // (6 intervals of DMA lead for every unit). Both halves' fragments stay live (+32 VGPRs: the
+  // per-lane C addressing of CMODE 0 / 1 then spills). The gated kernels keep the 16 / 8-read
+  // schedule too: they run the flagship shape, where the lab measured DEFER neutral
+  // (profiles/r03/r3_27, r3_33), and their arrival gate sits at that schedule's A staging.
   constexpr bool DEFER = !GATED && CMODE == 2;
   constexpr int NH = DEFER ? 2 : 1;  // fragment register sets
   __shared__ __attribute__((aligned(1024))) char smem[8 * UNIT];
