@@ -6,6 +6,8 @@ BASELINE.json metric: "ms/iter + effective TFLOP/s, tp_columnwise AG+GEMM m=6553
 
 Contract (driver):  python bench.py --gpus N --steps K --warmup W
   * N>1 is launched by torch.distributed.run, one rank per GPU (RANK/LOCAL_RANK/WORLD_SIZE env);
+    started without a launcher, ``--gpus N`` runs torch.distributed.run itself as a child
+    process and relays rank 0's line (``self_launch``);
   * W untimed warmups, then EXACTLY K timed steps bracketed by barrier + device sync on both
     sides; ms_per_step is the MAX over ranks;
   * rank 0 prints ONE JSON line. ``value`` = whole-job effective TFLOP/s = N * 2*m*n*k / t
@@ -77,6 +79,13 @@ def _graph(opts):
 # "/graph": the whole plan is captured once and replayed with one hipGraphLaunch per run (the IPC
 # pipelines issue ~200 HIP calls per run at d = 8 otherwise, profiles/r02/r2_13_*).
 CANDIDATES = [
+    # RCCL stage all-gathers feeding ONE flag-gated persistent GEMM over all m rows (the
+    # flagship's 1024-tile pt4 kernel at m = 65536; per stage a signal kernel raises the
+    # arrival flags, the own rows run first, ungated): no under-filled stage GEMMs (at d = 8,
+    # s = 8 a stage GEMM has 128 tiles of 256^2 for 256 CUs)
+    ("coll_pipeline/rccl/s8/fused", "native", dict(_COLL4, s=8, fused=True)),
+    ("coll_pipeline/rccl/s4/fused", "native", dict(_COLL4, fused=True)),
+    ("coll_pipeline/rccl/s8/fused/r48", "native", dict(_COLL4, s=8, fused=True, reserve_cus=48)),
     ("coll_pipeline/rccl/s4", "native", _COLL4),
     ("coll_pipeline/rccl/s8", "native", dict(_COLL4, s=8)),
     ("default/rccl", "native", _DEF),
@@ -91,6 +100,8 @@ CANDIDATES = [
     ("coll_pipeline/rccl/s4/128/c16", "native", dict(_COLL4, tile="128x128",
                                                       _env={"NCCL_MAX_NCHANNELS": "16"})),
     ("p2p_pipeline/rccl", "native", dict(algorithm="p2p_pipeline", backend="rccl")),
+    ("p2p_pipeline/rccl/fused", "native", dict(algorithm="p2p_pipeline", backend="rccl",
+                                               fused=True)),
     ("coll_pipeline/ipc/agk32/s8/graph", "native", _graph(_AGK)),
     ("coll_pipeline/ipc/agk64/s8/graph", "native", _graph(dict(_AGK, copy_blocks=64))),
     ("coll_pipeline/ipc/memcpy/s8/graph", "native", _graph(dict(_COLL_IPC, s=8))),
@@ -505,7 +516,7 @@ def autotune(job, pool, a, world: int, tune: dict, pre: dict = None):
     timeouts = {}
     t_tune = time.time()
     for label, impl, opts in order:
-        req = needs(impl, opts)
+        req = needs(impl, opts, getattr(a, "primitive", "tp_columnwise"))
         why = _blocked(req, pre)
         if why is None:
             hung = [ch for ch in req if timeouts.get(ch, 0) >= 2]
@@ -594,6 +605,25 @@ def final_measure(job, chosen, fallbacks, a, tune: dict):
     return chosen, None
 
 
+def self_launch(gpus: int, argv) -> int:
+    """``--gpus N`` without a launcher (no WORLD_SIZE): start ``torch.distributed.run`` with N
+    ranks on this node as a CHILD process (this parent never touched the GPU, and never execs),
+    relay the single JSON line of rank 0 and return the child's exit code. Rank discovery then
+    follows the same env path as a torchrun launch (``/root/reference/ddlb/envs.py:50-67`` reads
+    whatever launcher env is present)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={gpus}", "--master-addr", "127.0.0.1", "--master-port",
+           str(_free_port()), os.path.abspath(__file__), *argv]
+    sys.stderr.write(f"[bench] --gpus {gpus} without a launcher: {' '.join(cmd[1:6])} ...\n")
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    for line in proc.stdout:  # rank 0's JSON line (and anything else on stdout) passes through
+        sys.stdout.write(line)
+        sys.stdout.flush()
+    return proc.wait()
+
+
 def main(argv=None) -> int:
     p = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     p.add_argument("--gpus", type=int, default=1)
@@ -653,8 +683,10 @@ def main(argv=None) -> int:
         return child_main(a)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if a.gpus > 1 and world == 1:
-        sys.stderr.write("bench.py: --gpus > 1 must be launched with torch.distributed.run\n")
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return self_launch(a.gpus, argv if argv is not None else sys.argv[1:])
+    if a.gpus > 1 and world != a.gpus:
+        sys.stderr.write(f"bench.py: --gpus {a.gpus} but the launcher started {world} ranks\n")
         return 2
     job = Job(a)
     # warm the page cache for the children: the first `import torch` on a fresh box takes 1-2

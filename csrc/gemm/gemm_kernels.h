@@ -183,6 +183,8 @@ __device__ __forceinline__ void wait_flag_t0(const GemmArgs& p, int64_t row_firs
     const int s0 = (int)(row_first / p.flag_rows), s1 = (int)(row_last / p.flag_rows);
     const unsigned want = p.epoch_ptr ? *p.epoch_ptr : p.epoch;
     for (int sh = s0; sh <= s1; ++sh) {
+      // tile_order 3: the first producer's blocks are the caller's own rows (never gated)
+      if (p.tile_order == 3 && sh / p.nsub == p.first_shard) continue;
       unsigned* f = const_cast<unsigned*>(p.flags) + sh;
       unsigned spins = 0;
       while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
@@ -1541,7 +1543,9 @@ __global__ __launch_bounds__(512) void gemm_tn_t4_kernel(const GemmArgs p) {
 // CMODE: 0 = grouped C rows, plain nt stores; 1 = C row-block table (direct store); 2 = grouped C
 // rows in groups of a multiple of 256, write-through nt buffer stores (C's byte extent below
 // 2 GiB: 32-bit offsets)
-template <class Mma, int OUT, bool GATED, int CMODE = 0>
+// APAN: A panels through grouped rows or a row-block table (a separate instantiation: deriving
+// the panel base in the plain kernel cost it 6-16 more spilled SGPRs)
+template <class Mma, int OUT, bool GATED, int CMODE = 0, bool APAN = false>
 __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   constexpr int ROWB = 128, UNIT = 128 * ROWB;
   constexpr int NS = 4 * Store8<OUT>::kStores;
@@ -1596,12 +1600,30 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   }
   __amdgpu_buffer_rsrc_t rsA = crc, rsB = crc;  // set at the first stage
   int src_tile = -1;
+  // A panel of a tile (its 256 logical rows are contiguous physical rows, pt4_ok): APAN = grouped
+  // rows (groups of a multiple of 256 rows) or a row-block address table (blocks of a multiple of
+  // 256 rows, e.g. the peers' IPC-mapped shards or a stage-major gather buffer); wave-uniform,
+  // once per tile, with the tile's origin. The arrival gate indexes PHYSICAL rows of grouped A and
+  // LOGICAL rows of a table.
+  auto a_panel = [&](int64_t m0) __attribute__((always_inline)) -> const char* {
+    if (APAN && p.a_table != nullptr) {
+      const unsigned ur = (unsigned)m0, us = (unsigned)p.shard_rows, sh = ur / us;
+      return (const char*)p.a_table[sh] + (int64_t)(ur - sh * us) * p.lda * esz;
+    }
+    return (const char*)p.a + (APAN ? map_row(m0, p.a_grp, p.a_gstride) : m0) * p.lda * esz;
+  };
+  auto flag_row = [&](int64_t m0) __attribute__((always_inline)) -> int64_t {
+    if constexpr (!APAN) return m0;
+    return p.a_table != nullptr ? m0 : map_row(m0, p.a_grp, p.a_gstride);
+  };
+  const char* na = nullptr;  // APAN: the next tile's A panel
   auto origin = [&](int ti, int64_t& m0, int64_t& n0) __attribute__((always_inline)) {
     const int wg = tile_index_virtual(p, bid + ti * nblk, ntiles);
     int tm_, tn_;
     tile_mn(p, wg, p.M / 256, tiles_n, tm_, tn_);
     m0 = (int64_t)tm_ * 256;
     n0 = (int64_t)tn_ * 256;
+    if constexpr (APAN) na = a_panel(m0);
   };
   // Tile origins are computed once per tile, at its start, for the tile itself (stores) and for
   // the next one (staging runs up to two K-tiles ahead, arrival gate): the index maps' integer
@@ -1617,8 +1639,8 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   auto uoff = [](int X, int buf, int q) constexpr { return X * 65536 + buf * 32768 + q * 16384; };
   auto stage = [&](int X, int q, int buf, Cur c) __attribute__((always_inline)) {
     if (c.ti != src_tile) {  // always the next tile (nm0, nn0)
-      rsA = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.a + nm0 * p.lda * esz), 0,
-                                              0x7FFFFFF0, 0x00020000);
+      rsA = __builtin_amdgcn_make_buffer_rsrc((void*)(APAN ? na : a_panel(nm0)), 0, 0x7FFFFFF0,
+                                              0x00020000);
       rsB = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.b + nn0 * p.ldb * esz), 0,
                                               0x7FFFFFF0, 0x00020000);
       src_tile = c.ti;
@@ -1742,7 +1764,10 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     __builtin_amdgcn_sched_barrier(0);        \
   } while (0)
   const bool g1 = wr == 1;  // wave-uniform (wave came through readfirstlane)
-  if constexpr (GATED) wait_flag(p, nm0, nm0 + 255);  // arrival gate of the first tile
+  if constexpr (GATED) {  // arrival gate of the first tile
+    const int64_t f0 = flag_row(nm0);
+    wait_flag(p, f0, f0 + 255);
+  }
   Cur q0{0, 0}, q1{0, 0};
   adv(q1);
   if constexpr (DEFER) {
@@ -1822,7 +1847,8 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
         // same point (qa is workgroup-uniform), orders all waves' A staging after it. Both wave
         // groups insert it at the same place, so their one-barrier stagger is unchanged; an extra
         // barrier only adds ordering (LDS RAW / WAR distances grow).
-        wait_flag_t0(p, nm0, nm0 + 255);  // qa.ti is the next tile (or tile 0)
+        const int64_t f0 = flag_row(nm0);  // qa.ti is the next tile (or tile 0)
+        wait_flag_t0(p, f0, f0 + 255);
         T4_BAR();
       }
       loadB(bufc, 0);  // phase A
@@ -2374,14 +2400,16 @@ hipError_t launch_t4(const GemmArgs& p, hipStream_t s) {
 }
 
 // pt4 needs an even number (>= 2) of K-tiles per tile (its FIRST and LAST K-tile kinds are
-// distinct, its body is unrolled by buffer parity), plain A rows, 32-bit panel offsets (a
-// 256-row panel, the reach of its LDS-DMA buffer descriptors, stays below 1 GiB) and no fused
-// activation (t4 carries those)
+// distinct, its body is unrolled by buffer parity), a tile's 256 A rows contiguous (plain rows,
+// grouped rows in groups of a multiple of 256, or a row-block table of such blocks: one panel
+// base per tile), 32-bit panel offsets (a 256-row panel, the reach of its LDS-DMA buffer
+// descriptors, stays below 1 GiB) and no fused activation (t4 carries those)
 bool pt4_ok(const GemmArgs& p, int esz) {
   const int64_t nk = (int64_t)p.K * esz / 128;
-  return p.M % 256 == 0 && p.N % 256 == 0 && p.a_table == nullptr && p.act == ACT_NONE &&
-         p.a_grp == p.M && nk >= 2 && nk % 2 == 0 && p.lda * esz <= (1 << 22) &&
-         p.ldb * esz <= (1 << 22);
+  const bool a_ok = p.a_table != nullptr ? (p.shard_rows > 0 && p.shard_rows % 256 == 0)
+                                         : (p.a_grp == p.M || p.a_grp % 256 == 0);
+  return p.M % 256 == 0 && p.N % 256 == 0 && a_ok && p.act == ACT_NONE && nk >= 2 &&
+         nk % 2 == 0 && p.lda * esz <= (1 << 22) && p.ldb * esz <= (1 << 22);
 }
 
 template <class Mma, int OUT>
@@ -2406,7 +2434,22 @@ hipError_t launch_pt4(const GemmArgs& p, hipStream_t s) {
   if (grid < 1) grid = 1;
   // write-through stores address C from a per-tile scalar row (the tile's rows contiguous)
   const bool wt = c_fits_wt(p, out_size<OUT>()) && p.c_grp % 256 == 0;
-  if (p.flags != nullptr && wt)
+  // A through grouped rows / a row-block table: the APAN instantiations (no C row table with them)
+  const bool apan = p.a_table != nullptr || p.a_grp != p.M;
+  if (apan && p.c_table != nullptr) return hipErrorNotSupported;
+  if (apan && p.flags != nullptr && wt)
+    hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, true, 2, true>), dim3(grid + q.ag_ctas),
+                       dim3(512), 0, s, q);
+  else if (apan && p.flags != nullptr)
+    hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, true, 0, true>), dim3(grid + q.ag_ctas),
+                       dim3(512), 0, s, q);
+  else if (apan && wt)
+    hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false, 2, true>), dim3(grid), dim3(512), 0, s,
+                       p);
+  else if (apan)
+    hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false, 0, true>), dim3(grid), dim3(512), 0, s,
+                       p);
+  else if (p.flags != nullptr && wt)
     hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, true, 2>), dim3(grid + q.ag_ctas), dim3(512),
                        0, s, q);
   else if (p.flags != nullptr)
@@ -2447,7 +2490,8 @@ hipError_t launch_cfg(const GemmArgs& p, int tile, hipStream_t s) {
       if (t8_ok(p)) return launch_t8<Mma, OUT>(p, s);
       return launch_tiled<Mma, OUT, 256, 256, 2, 4, true>(p, s);
     case TILE_PT4:
-      if (pt4_ok(p, Mma::kElem)) return launch_pt4<Mma, OUT>(p, s);
+      if (pt4_ok(p, Mma::kElem) && !(p.c_table && (p.a_table || p.a_grp != p.M)))
+        return launch_pt4<Mma, OUT>(p, s);
       if (t8_ok(p)) return launch_t4<Mma, OUT>(p, s);
       return launch_tiled<Mma, OUT, 256, 256, 2, 4, true>(p, s);
     case TILE_T4:
@@ -2491,7 +2535,8 @@ hipError_t launch_cfg(const GemmArgs& p, int tile, hipStream_t s) {
 template <int OUT>
 hipError_t launch_mx_cfg(const GemmArgs& p, int tile, hipStream_t s) {
   // whole 256x256 tiles: the 8-phase ping-pong schedule (persistent with >= 2 tiles per CU)
-  if (tile == TILE_PT4 && pt4_ok(p, 1)) return launch_pt4<MmaMX, OUT>(p, s);
+  if (tile == TILE_PT4 && pt4_ok(p, 1) && !(p.c_table && (p.a_table || p.a_grp != p.M)))
+    return launch_pt4<MmaMX, OUT>(p, s);
   if ((tile == TILE_T4 || tile == TILE_PT4) && t8_ok(p)) return launch_t4<MmaMX, OUT>(p, s);
   if ((tile == TILE_T8 || tile == TILE_PT8 || tile == TILE_R256 || tile == TILE_AUTO) && t8_ok(p)) {
     const int tiles = (p.M / 256) * (p.N / 256);

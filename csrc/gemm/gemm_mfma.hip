@@ -90,21 +90,26 @@ hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mo
   if (p.c_grp <= 0) { p.c_grp = p.M > 0 ? p.M : 1; p.c_gstride = p.c_grp; }
   if (p.M == 0 || p.N == 0) return hipSuccess;
   if (p.a_table != nullptr) {
-    // direct-access A: only the tiled and ring kernels read A through the shard table
-    if (p.shard_rows <= 0 || p.flags != nullptr) return hipErrorInvalidValue;
-    if (mode == GEMM_MODE_MX) mode = GEMM_MODE_AUTO;
+    // A through a row-block address table (direct access to the peers' shards, or the blocks of
+    // a stage-major gather buffer): the ping-pong kernels (pt4 / t4 / t8 / pt8, whole 256-row
+    // blocks; pt4 takes one panel base per tile) and the tiled kernels read A through it; the
+    // persistent streaming family does not. Arrival flags then index LOGICAL rows.
+    if (p.shard_rows <= 0) return hipErrorInvalidValue;
     if (tile == TILE_PP256 || tile == TILE_P256 || tile == TILE_PI256 || tile == TILE_PI256W4)
       tile = TILE_I256;
     if (tile == TILE_P128) tile = TILE_I128;
     const bool whole = p.M % 256 == 0 && p.N % 256 == 0 && p.shard_rows % 256 == 0;
     if (tile == TILE_AUTO) {
       tile = choose_tile(p.M, p.N, p.K, din);
-      if (tile == TILE_PT4) tile = TILE_T4;  // pt4 reads A through panel offsets, not shard tables
-      if (tile != TILE_PT8 && tile != TILE_R256 && tile != TILE_T4) tile = TILE_T8;
+      if (tile != TILE_PT4 && tile != TILE_PT8 && tile != TILE_R256 && tile != TILE_T4)
+        tile = TILE_T8;
     }
-    if (tile == TILE_PT4) tile = TILE_T4;
-    if ((tile == TILE_R256 || tile == TILE_T8 || tile == TILE_PT8 || tile == TILE_T4) && !whole)
-      tile = TILE_128x128;
+    const bool ping = tile == TILE_R256 || tile == TILE_T8 || tile == TILE_PT8 ||
+                      tile == TILE_T4 || tile == TILE_PT4;
+    if (ping && !whole) tile = TILE_128x128;
+    // the tiled MX kernel addresses plain rows: block-scaled MFMAs on whole blocks only
+    if (mode == GEMM_MODE_MX && !(ping && whole)) mode = GEMM_MODE_AUTO;
+    if (p.flags != nullptr && !(ping && whole)) return hipErrorNotSupported;
     if (mode == GEMM_MODE_GENERIC || !gemm_fast_path_ok(p, din, dout)) return hipErrorNotSupported;
   }
   if (p.c_table != nullptr) {
@@ -138,8 +143,11 @@ hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mo
     if (tile == TILE_AUTO) tile = choose_tile(p.M, p.N, p.K, din);
     if (p.nsub < 1) p.nsub = 1;
     if (p.tile_order && (p.nshards <= 0 || p.M % p.nshards != 0 || p.nshards % p.nsub != 0 ||
-                         (p.M / p.nshards) % tile_rows(tile) != 0))
+                         (p.M / p.nshards) % tile_rows(tile) != 0)) {
+      // tile_order 3 also means "the own blocks are not gated": never drop it silently
+      if (p.tile_order == 3) return hipErrorNotSupported;
       p.tile_order = 0;
+    }
     if (p.tile_order == 2 && p.N % tile_cols(tile) != 0) p.tile_order = 0;  // whole tiles/shard
     hipError_t e = hipErrorInvalidValue;
     if (din == DT_FP8 && mode == GEMM_MODE_MX) e = launch_fast_mx(p, dout, tile, s);

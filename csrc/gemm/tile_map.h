@@ -27,8 +27,16 @@ __host__ __device__ inline int xcd_remap(int bid, int nwg) {
 // tile_order 2 interleaves the shards.
 // ordered_shard: dispatch position j -> shard; producers rotate fastest (own first), blocks
 // slowest.
+// tile_order 3 (own first): the first producer's nsub blocks (the caller's own rows: a gated
+// GEMM never waits for them, wait_flag_t0), then block-major over the other producers, rotating
+// from first_shard + 1 (the order the stage collectives of an RCCL-fed gated GEMM deliver them).
 __host__ __device__ inline int ordered_shard(const GemmArgs& p, int j) {
   const int np = p.nshards / p.nsub;
+  if (p.tile_order == 3) {
+    if (j < p.nsub || np < 2) return p.first_shard * p.nsub + j;
+    j -= p.nsub;
+    return ((p.first_shard + 1 + j % (np - 1)) % np) * p.nsub + j / (np - 1);
+  }
   return ((p.first_shard + j % np) % np) * p.nsub + j / np;
 }
 

@@ -122,7 +122,7 @@ def _shard_order(rank: int, d: int, ring: bool) -> List[int]:
 class _Flags:
     """Named slot table inside the symmetric ``flags`` buffer (uint32 words)."""
 
-    def __init__(self, plan: Plan, d: int, s: int):
+    def __init__(self, plan: Plan, d: int, s: int, symmetric: bool = True):
         self.d = d
         self.slots: Dict[str, Tuple[int, int]] = {}
         self.words = 0
@@ -132,7 +132,8 @@ class _Flags:
             self.slots[name] = (self.words, count)
             self.words += count
         nbytes = max(256, ((self.words * 4 + 255) // 256) * 256)
-        plan.buffer("flags", nbytes, symmetric=True, zero=True)
+        # local-only flags (RCCL-fed gated GEMMs: set by this rank's own signal kernels)
+        plan.buffer("flags", nbytes, symmetric=symmetric, zero=True)
 
     def ref(self, name: str, idx: int, owner: Optional[int] = None) -> Ref:
         base, count = self.slots[name]
@@ -190,10 +191,10 @@ def check_columnwise(d: int, m: int, n: int, k: int, cfg: AlgoConfig, ein: int =
                                     cfg.algorithm == "direct" or cfg.fused):
         raise ValueError("direction=push applies to backend=ipc, order=AG_before, "
                          "default / coll_pipeline / p2p_pipeline (not fused)")
-    if cfg.fused and (cfg.backend != "ipc" or cfg.order != "AG_before" or
+    if cfg.fused and (cfg.order != "AG_before" or
                       cfg.algorithm not in ("p2p_pipeline", "coll_pipeline")):
-        raise ValueError("fused=True (one arrival-flag-gated GEMM) applies to backend=ipc, "
-                         "order=AG_before, p2p_pipeline / coll_pipeline")
+        raise ValueError("fused=True (one arrival-flag-gated GEMM) applies to order=AG_before, "
+                         "p2p_pipeline / coll_pipeline")
     if (cfg.fused and cfg.protocol == "kernel" and cfg.algorithm == "coll_pipeline" and d > 1
             and (m % 256 or n % 256 or k * ein % 256 or k * ein < 256 or cfg.act)):
         raise ValueError("the in-kernel all-gather (coll_pipeline, fused, kernel copies) runs on "
@@ -272,6 +273,10 @@ def _build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, do
                 plan.wait(S_MAIN, e)
         gemm(S_MAIN, A, C, m)
         _wait(plan, S_MAIN, [flags.ref("ACK", p) for p in range(d) if p != rank], cfg)
+    elif alg == "coll_pipeline" and be == "rccl" and cfg.fused:
+        _col_rccl_fused_coll(plan, rank, d, m, n, k, ein, cfg, A, Bt, C, comm_dt, gdt)
+    elif alg == "p2p_pipeline" and be == "rccl" and cfg.fused:
+        _col_rccl_fused_p2p(plan, rank, d, m, n, k, ein, cfg, A, Bt, C, comm_dt, gdt)
     elif alg == "coll_pipeline" and be == "rccl":
         rows = ml // cfg.s
         for j in range(cfg.s):
@@ -381,6 +386,64 @@ def _build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, do
     else:  # pragma: no cover
         raise ValueError(f"unsupported combination {alg}/{be}")
     return plan, io
+
+
+def _col_rccl_fused_coll(plan, rank, d, m, n, k, ein, cfg, A, Bt, C, comm_dt, gdt) -> None:
+    """coll_pipeline over RCCL feeding ONE persistent flag-gated GEMM over all m rows
+    (``TPColumnwise/fuser.py:59-100`` semantics, SURVEY.md §7.3 hard part #1: at d = 8, s = 8 a
+    stage GEMM is 8192 x n x k, 128 tiles of 256² for 256 CUs; the fused GEMM is the flagship's
+    1024-tile persistent kernel).
+
+    Stage j's ``ncclAllGather`` lands in a stage-major gather buffer G (block (j, p) = rank p's
+    stage-j rows at G row (j*d + p)*rows); a signal kernel on the comm stream then raises
+    ARRIVE[p*s + j] for every peer p. The GEMM reads A through a row-block address table
+    (logical block p*s + j = C rows p*m/d + j*rows: C keeps its canonical layout, no permutation)
+    whose own blocks point at the rank's input shard itself, so the own tiles (dispatched first and
+    never gated, tile_order 3: no signal op for them) run while stage 0 is still in flight. The
+    flags are local (this rank's own signal kernels set them) and the gated GEMM leaves
+    ``reserve_cus`` CUs to RCCL's kernels."""
+    ml = m // d
+    s = cfg.s
+    rows = ml // s
+    blk = rows * k * ein
+    G = plan.buffer("G", m * k * ein)
+    flags = _Flags(plan, d, s, symmetric=False)
+    table = []
+    for p in range(d):
+        for j in range(s):
+            table.append(A + (rank * ml + j * rows) * k * ein if p == rank
+                         else G + (j * d + p) * blk)
+    for j in range(s):
+        plan.allgather(S_COMM, A + (rank * ml + j * rows) * k * ein, G + j * d * blk, rows * k,
+                       comm_dt)
+        # a kernel (release at system scope after the collective's kernel): the gated tiles
+        # acquire the rows RCCL wrote; a stream memop has no such fence
+        for c in _chunks([flags.ref("ARRIVE", p * s + j) for p in range(d) if p != rank]):
+            plan.signal(S_COMM, c, method=SIG_KERNEL)
+    plan.gemm(S_MAIN, A, Bt, C, M=m, N=n, K=k, lda=k, ldb=k, ldc=n, **gdt,
+              a_shards=table, shard_rows=rows, flags=flags.ref("ARRIVE", 0), flag_rows=rows,
+              nshards=d * s, nsub=s, first_shard=rank, tile_order=3,
+              reserve_cus=cfg.reserve_cus)
+
+
+def _col_rccl_fused_p2p(plan, rank, d, m, n, k, ein, cfg, A, Bt, C, comm_dt, gdt) -> None:
+    """p2p_pipeline over RCCL send / recv (``TPColumnwise/fuser.py:102-146``) feeding ONE
+    flag-gated GEMM over all m rows: step j receives shard (r+j)%d into its rows of A and a
+    signal kernel raises ARRIVE[(r+j)%d]; the tiles run shard by shard from the own one
+    (tile_order 1 from ``first_shard`` = rank: the order the steps deliver them)."""
+    ml = m // d
+    flags = _Flags(plan, d, 1, symmetric=False)
+    _signal(plan, S_MAIN, [flags.ref("ARRIVE", rank)], cfg)
+    for j in range(1, d):
+        to, frm = (rank - j) % d, (rank + j) % d
+        plan.group_start(S_COMM)
+        plan.send(S_COMM, A + rank * ml * k * ein, ml * k, comm_dt, to)
+        plan.recv(S_COMM, A + frm * ml * k * ein, ml * k, comm_dt, frm)
+        plan.group_end(S_COMM)
+        plan.signal(S_COMM, [flags.ref("ARRIVE", frm)], method=SIG_KERNEL)
+    plan.gemm(S_MAIN, A, Bt, C, M=m, N=n, K=k, lda=k, ldb=k, ldc=n, **gdt,
+              flags=flags.ref("ARRIVE", 0), flag_rows=ml, nshards=d, first_shard=rank,
+              tile_order=1, reserve_cus=cfg.reserve_cus)
 
 
 def _col_push(plan, rank, d, ml, cfg, flags, arow, crow, gemm, row_bytes) -> None:
@@ -704,6 +767,10 @@ def _build_tp_rowwise(rank: int, d: int, m: int, n: int, k: int, din: int, dout:
         srcs = _row_gather_sources(plan, rank, d, cfg, P + rank * blk, blk, peers, "RCV")
         plan.reduce(S_MAIN, OUT, srcs, ml * n, dout)
         _signal(plan, S_MAIN, [flags.ref("ACK", rank, owner=p) for p in peers], cfg)
+    elif alg == "coll_pipeline" and be == "rccl" and cfg.fused:
+        _col_rccl_fused_coll(plan, rank, d, m, n, k, ein, cfg, A, Bt, C, comm_dt, gdt)
+    elif alg == "p2p_pipeline" and be == "rccl" and cfg.fused:
+        _col_rccl_fused_p2p(plan, rank, d, m, n, k, ein, cfg, A, Bt, C, comm_dt, gdt)
     elif alg == "coll_pipeline" and be == "rccl":
         rows = ml // cfg.s
         for j in range(cfg.s):

@@ -22,7 +22,18 @@ check           what it proves (every rank, every peer, two epochs)
 ``ipc_sdma``    copy-engine pull (``hipMemcpyAsync`` from IPC-mapped peer memory, one stream per
                 peer) of every peer's pattern
 ``ipc_push``    copy-engine push (posted writes into each peer's receive slot) + DONE flag
+``ipc_agk``     the in-kernel all-gather: ONE gated persistent GEMM launch whose copy workgroups
+                pull every peer's row blocks over xGMI (write-through publication, agent-scope
+                gate acquire, ACK stores across the link), validated against fp32
+``ipc_dstore``  the direct-store epilogue: a GEMM whose C row blocks are written straight into
+                every peer's receive slot (tp_rowwise p2p fused), then the d-way reduce, validated
+``rccl_fused``  RCCL stage all-gathers feeding ONE flag-gated GEMM through signal kernels on the
+                comm stream (coll_pipeline backend=rccl fused=True), validated
 ==============  ==================================================================================
+
+The last three run the real plan builders through the primitives at a small shape (every tile
+of the persistent 256x256 kernel, 2 epochs), so a mechanism that corrupts data over the link, not
+only one that hangs, drops its candidate family.
 
 Every check is a :class:`~ddlb_amd.parallel.plan.Plan` executed by the native executor, so the
 same plans run on the CPU simulator in the tests (``tests/test_preflight.py``). A check that hangs
@@ -40,10 +51,49 @@ from typing import Callable, Dict, List, Optional
 from ddlb_amd.parallel.plan import (COPY_ENGINE, DT_F32, DT_U8, SIG_KERNEL, SIG_STREAM, Plan,
                                     Ref)
 
-IPC_PHASES = ("ipc", "ipc_ksig", "ipc_kernel", "ipc_sdma", "ipc_push")
-RCCL_PHASES = ("torch_nccl", "rccl")
+IPC_PHASES = ("ipc", "ipc_ksig", "ipc_kernel", "ipc_sdma", "ipc_push", "ipc_agk", "ipc_dstore")
+RCCL_PHASES = ("torch_nccl", "rccl", "rccl_fused")
+# phases that run a whole primitive (the real plan builder) instead of a data-movement plan:
+# (primitive, options); the shape is PRIMITIVE_SHAPE(d)
+PRIMITIVE_PHASES = {
+    "ipc_agk": ("tp_columnwise", dict(algorithm="coll_pipeline", backend="ipc",
+                                      multicast_protocol="kernel", fused=True, s=2,
+                                      copy_blocks=16)),
+    "ipc_dstore": ("tp_rowwise", dict(algorithm="p2p_pipeline", backend="ipc", fused=True)),
+    "rccl_fused": ("tp_columnwise", dict(algorithm="coll_pipeline", backend="rccl", fused=True,
+                                         s=2)),
+}
 PATTERN_BYTES = 1 << 20      # per rank and phase: 1 MiB (several xGMI packets, small enough)
 RS_COUNT = 4096              # f32 elements per rank of the reduce-scatter check
+
+
+def primitive_shape(d: int):
+    """(m, n, k) of the primitive phases: whole 256-row stage blocks for every rank and stage (the
+    persistent gated 256x256 kernel), k divisible by d (tp_rowwise) in whole pairs of 128-byte
+    K-tiles of bf16."""
+    return 512 * d, 256, 128 * d
+
+
+def run_primitive_check(comm, phase: str, epochs: int = 2) -> None:
+    """One primitive phase: build the real plan, run ``epochs`` times, validate the last output
+    (the reference's rule) and the device spins' health."""
+    import torch
+
+    from ddlb_amd.primitives.registry import resolve
+
+    prim, opts = PRIMITIVE_PHASES[phase]
+    m, n, k = primitive_shape(comm.world_size)
+    cls, o, _ = resolve(prim, "native", dict(opts))
+    impl = cls(m=m, n=n, k=k, dtype="bfloat16", **o)
+    try:
+        for _ in range(epochs):
+            out = impl.run()
+        torch.cuda.synchronize(comm.device)
+        impl.check_health()
+        impl.validate(out)
+        comm.barrier()
+    finally:
+        impl.close()
 
 
 def pattern(owner: int, nbytes: int, epoch: int = 1):
@@ -184,6 +234,10 @@ def run_ipc_checks(comm, phases=IPC_PHASES, progress_path: Optional[str] = None,
     r, d = comm.rank, comm.world_size
     dev = comm.device
     for phase in phases:
+        if phase in PRIMITIVE_PHASES:
+            _run_checked(phase, prog, lambda: run_primitive_check(comm, phase))
+            continue
+
         def one():
             plan = build_ipc_plan(r, d, phase, nbytes)
             bound = ctx.bind(plan)
@@ -256,6 +310,8 @@ def run_rccl_checks(comm, phases=RCCL_PHASES, progress_path: Optional[str] = Non
                 bound.close()
 
         _run_checked("rccl", prog, own)
+    if "rccl_fused" in phases:
+        _run_checked("rccl_fused", prog, lambda: run_primitive_check(comm, "rccl_fused"))
     return prog.res
 
 
@@ -265,26 +321,35 @@ def families_ok(results: Dict[str, str]) -> Dict[str, bool]:
     return ok
 
 
-def needs(impl: str, opts: Dict) -> List[str]:
+def needs(impl: str, opts: Dict, primitive: str = "tp_columnwise") -> List[str]:
     """Preflight checks a benchmark candidate relies on (``bench.py`` drops it if any failed)."""
     if impl == "pytorch":
         return ["torch_nccl"]
     if impl != "native":
         return []
     backend = opts.get("backend", "rccl")
+    alg = opts.get("algorithm", "default")
+    fused = bool(opts.get("fused", False))
     if backend in ("rccl", "nccl"):
-        return ["rccl"]
+        return ["rccl", "rccl_fused"] if fused else ["rccl"]
     out = ["ipc"]
-    if opts.get("graph") in (True, "auto") or opts.get("signal") == "kernel":
+    # a missing "graph" key is the option default "auto" (graph replay whenever capturable, and
+    # graph mode always signals with the kernels); the rowwise IPC plans send READY with the
+    # signal kernel whatever ``signal`` says
+    if (opts.get("graph", "auto") in (True, "auto", "true") or opts.get("signal") == "kernel"
+            or primitive == "tp_rowwise"):
         out.append("ipc_ksig")
     proto = opts.get("multicast_protocol", "memcpy")
-    alg = opts.get("algorithm", "default")
     if alg == "direct" or proto == "kernel":
         out.append("ipc_kernel")   # peer HBM read by CUs (copy kernel, in-kernel AG, LDS-DMA)
     elif opts.get("direction") == "push":
         out.append("ipc_push")
     else:
         out.append("ipc_sdma")
+    if primitive == "tp_columnwise" and fused and alg == "coll_pipeline" and proto == "kernel":
+        out.append("ipc_agk")
+    if primitive == "tp_rowwise" and fused and alg == "p2p_pipeline":
+        out.append("ipc_dstore")
     return out
 
 

@@ -462,6 +462,9 @@ class Simulator:
                             base = a["flags"]
                             ok = True
                             for sh in range(a["nshards"]):
+                                if (a.get("tile_order") == 3
+                                        and sh // a["nsub"] == a["first_shard"]):
+                                    continue  # own rows: never gated (csrc wait_flag_t0)
                                 f = base + 4 * sh
                                 val = int(self._buf(r, f)[f.off:f.off + 4].view(torch.int32)[0])
                                 if val < self.epoch[r]:

@@ -1,7 +1,8 @@
 // Host-side checks of the GEMM's index maps (csrc/gemm/tile_map.h), built with
 // AddressSanitizer + UndefinedBehaviorSanitizer on the host only (tests/test_native_host.py):
-//  * tile_index_virtual is a bijection on [0, ntiles) for tile_order 0 / 1 / 2 and every shard
-//    layout the plans use, and tile_order 2 puts consecutive ids on different shards;
+//  * tile_index_virtual is a bijection on [0, ntiles) for tile_order 0 / 1 / 2 / 3 and every
+//    shard layout the plans use, tile_order 2 puts consecutive ids on different shards, and
+//    tile_order 3 dispatches the first producer's blocks before any other producer's;
 //  * tile_mn is a bijection onto the (tm, tn) grid (grouped raster included);
 //  * the in-kernel all-gather's units cover every (block, producer != rank, part) exactly once,
 //    and each run of np - 1 consecutive units of a block visits every peer;
@@ -47,6 +48,12 @@ static void check_tile_index(int ntiles, int order, int nshards, int nsub, int f
       CHECK(ddlb::tile_index_virtual(p, v, ntiles) / per !=
                 ddlb::tile_index_virtual(p, v + 1, ntiles) / per,
             "tile_order 2: ids %d, %d on one shard", v, v + 1);
+  }
+  if (order == 3) {
+    const int per = ntiles / nshards;
+    for (int v = 0; v < nsub * per; ++v)
+      CHECK(ddlb::tile_index_virtual(p, v, ntiles) / per / nsub == first,
+            "tile_order 3: id %d not in the first producer's blocks", v);
   }
 }
 
@@ -113,7 +120,7 @@ static void check_fill(int grid, int ag, int tiles) {
 
 int main() {
   for (int ntiles : {8, 64, 96, 256, 1024, 2048, 4096})
-    for (int order : {0, 1, 2})
+    for (int order : {0, 1, 2, 3})
       for (int nshards : {1, 2, 3, 4, 6, 8, 16, 24, 32, 64})
         for (int nsub : {1, 2, 4, 8}) {
           if (ntiles % nshards || nshards % nsub) continue;

@@ -50,6 +50,18 @@ def test_bench_world2_cpu():
     assert abs(d["value"] - 2 * d["per_gpu_tflops"]) < 1e-2
 
 
+def test_bench_gpus2_without_launcher_cpu():
+    """``--gpus 2`` started as a plain ``python bench.py`` (no WORLD_SIZE): bench.py runs
+    torch.distributed.run itself as a child and relays exactly one JSON line (the driver's N>1
+    record must not depend on how it launches the script)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *ARGS],
+                       capture_output=True, text=True, timeout=400, env=_env())
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 2 and d["valid"] is True
+    assert "without a launcher" in r.stderr
+
+
 def _prewarm_worker(rank, world, port, q):
     import time
 
@@ -285,3 +297,32 @@ def test_bench_world2_cpu_preflight_fields():
     assert d["preflight"]["ipc"] == "failed: scripted"
     assert d["timing"].startswith("cpu_clock window")
     assert d["harness_mean_ms"] > 0 and d["max_err"] <= d["err_bound"]
+
+
+def test_autotune_drops_candidates_of_failed_primitive_phases():
+    """Mocked failures of the primitive-level preflight phases drop exactly their families: the
+    RCCL-fed fused GEMM (rccl_fused), the in-kernel all-gather (ipc_agk) and, for tp_rowwise, the
+    direct-store epilogue (ipc_dstore)."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    pool = [("rf", "native", {"backend": "rccl", "algorithm": "coll_pipeline", "fused": True}),
+            ("r", "native", {"backend": "rccl", "algorithm": "coll_pipeline"}),
+            ("agk", "native", {"backend": "ipc", "algorithm": "coll_pipeline", "fused": True,
+                               "multicast_protocol": "kernel", "graph": True}),
+            ("k", "native", {"backend": "ipc", "multicast_protocol": "kernel", "graph": True})]
+    job = _FakeJob(pool, {"r": [_ok(1.0)], "k": [_ok(0.9)]})
+    pre = {"rccl": "ok", "rccl_fused": "failed: AssertionError", "ipc": "ok", "ipc_ksig": "ok",
+           "ipc_kernel": "ok", "ipc_agk": "failed: timeout", "torch_nccl": "ok"}
+    tune = {}
+    chosen, _ = bench.autotune(job, pool, _args(), 8, tune, pre)
+    assert chosen[0] == "k"
+    assert tune["rf"].startswith("skipped (rccl_fused") and tune["agk"].startswith("skipped (ipc_agk")
+    row_pool = [("d", "native", {"backend": "ipc", "algorithm": "p2p_pipeline", "fused": True,
+                                 "graph": False}),
+                ("m", "native", {"backend": "ipc", "algorithm": "p2p_pipeline", "graph": False})]
+    job = _FakeJob(row_pool, {"m": [_ok(2.0)]})
+    tune = {}
+    pre = {"ipc": "ok", "ipc_ksig": "ok", "ipc_sdma": "ok", "ipc_dstore": "failed: timeout"}
+    chosen, _ = bench.autotune(job, row_pool, _args(primitive="tp_rowwise"), 8, tune, pre)
+    assert chosen[0] == "m" and tune["d"].startswith("skipped (ipc_dstore")

@@ -401,3 +401,42 @@ def test_pt4_flagship_race_screen(gen):
         assert torch.equal(out, first)
     ref = _ref(a, w)
     assert float((first.float() - ref).abs().max()) <= _tight_bound(ref, 1024)
+
+
+@pytest.mark.parametrize("dt", [(torch.bfloat16, torch.bfloat16, "auto"),
+                                (torch.bfloat16, torch.float32, "auto"),
+                                (torch.float8_e4m3fn, torch.bfloat16, "mx")],
+                         ids=lambda d: f"{str(d[0])[6:]}-{str(d[1])[6:]}-{d[2]}")
+@pytest.mark.parametrize("grp,cgrp", [(256, 0), (512, 512), (1024, 256)])
+def test_pt4_grouped_a_rows(dt, grp, cgrp, gen):
+    """pt4 reading A through grouped rows (groups of a multiple of 256 rows: one panel base per
+    tile, the APAN instantiation) — the IPC / rowwise pipelines' stage GEMMs — with plain or
+    grouped C, against the fp32 reference with the tight bound, repeat-identical 10x."""
+    from ddlb_amd.ops.gemm import gemm
+
+    din, dout, mode = dt
+    d, K, N, stride = 8, 1024, 1024, 4096
+    M = d * grp
+    A = _rand((d * stride, K), din, gen)
+    w = _rand((N, K), din, gen)
+    C = torch.zeros((2 * M if cgrp else M, N), dtype=dout, device=DEV)
+    kw = dict(M=M, a_grp=grp, a_gstride=stride, tile="pt4", out_dtype=dout, mode=mode)
+    if cgrp:
+        kw.update(c_grp=cgrp, c_gstride=2 * cgrp)
+    gemm(A, w, C, **kw)
+    torch.cuda.synchronize()
+    idx = torch.cat([torch.arange(r * stride, r * stride + grp) for r in range(d)]).to(DEV)
+    ref = _ref(A[idx], w)
+    if cgrp:
+        cidx = torch.cat([torch.arange(g * 2 * cgrp, g * 2 * cgrp + cgrp)
+                          for g in range(M // cgrp)]).to(DEV)
+        got = C[cidx]
+    else:
+        got = C
+    err = float((got.float() - ref).abs().max())
+    assert err <= _tight_bound(ref, K), err
+    first = C.clone()
+    for _ in range(10):
+        gemm(A, w, C, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(C, first)

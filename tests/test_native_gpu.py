@@ -569,6 +569,133 @@ def test_in_kernel_allgather_world1(comm, graph, mode):
     ctx.close()
 
 
+def _tight(ref, k):
+    """max|err| <= 2^-7 max|ref| + k 2^-12 (tests/test_gemm_gpu.py _tight_bound)."""
+    return 2.0 ** -7 * float(ref.abs().max()) + k * 2.0 ** -12
+
+
+@pytest.mark.parametrize("tile,dt,mode", [(19, "bf16", 0), (0, "bf16", 0), (18, "bf16", 0),
+                                          (4, "bf16", 0), (19, "fp8", 2), (0, "fp8", 2)])
+def test_a_table_gemm_world1(comm, tile, dt, mode):
+    """A through a row-block address table (the direct-access / RCCL-fused plans): the blocks
+    come from two buffers in a permuted order; pt4 (one panel base per tile), auto, t4, 128x128
+    and MX-fp8 against the fp32 reference with the tight bound, repeat-identical."""
+    from ddlb_amd.parallel.context import NativeContext
+    from ddlb_amd.parallel.plan import DT_BF16, DT_FP8, Plan
+
+    din = DT_FP8 if dt == "fp8" else DT_BF16
+    tdt = torch.float8_e4m3fn if dt == "fp8" else torch.bfloat16
+    es = 1 if dt == "fp8" else 2
+    M, N, K, nb = 16384, 1024, 1024, 8
+    rows = M // nb
+    plan = Plan(0, 1, nstreams=1, stream_priority=[0])
+    x = plan.buffer("x", M // 2 * K * es)
+    y = plan.buffer("y", M // 2 * K * es)
+    bt = plan.buffer("bt", N * K * es)
+    c = plan.buffer("c", M * N * 2)
+    # logical block b -> x block (b // 2) for even b, y block 3 - b // 2 for odd b
+    table = [x + (b // 2) * rows * K * es if b % 2 == 0 else y + (3 - b // 2) * rows * K * es
+             for b in range(nb)]
+    plan.gemm(0, x, bt, c, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, din=din, dout=DT_BF16, tile=tile,
+              mode=mode, a_shards=table, shard_rows=rows)
+    ctx = NativeContext(comm)
+    bound = ctx.bind(plan)
+    X = (torch.rand(M // 2, K, device="cuda") * 2 - 1).to(tdt)
+    Y = (torch.rand(M // 2, K, device="cuda") * 2 - 1).to(tdt)
+    W = (torch.rand(N, K, device="cuda") * 2 - 1).to(tdt)
+    bound.buffer("x").view(tdt).view(M // 2, K).copy_(X)
+    bound.buffer("y").view(tdt).view(M // 2, K).copy_(Y)
+    bound.buffer("bt").view(tdt).view(N, K).copy_(W)
+    A = torch.cat([X.view(4, rows, K), Y.view(4, rows, K).flip(0)], 1).view(M, K)
+    ref = A.float() @ W.float().T
+    out = bound.buffer("c").view(torch.bfloat16).view(M, N)
+    bound.run()
+    torch.cuda.synchronize()
+    first = out.clone()
+    err = float((first.float() - ref).abs().max())
+    assert err <= _tight(ref, K), err
+    for _ in range(10):
+        bound.run()
+    torch.cuda.synchronize()
+    assert torch.equal(out, first)
+    bound.close()
+    ctx.close()
+
+
+@pytest.mark.parametrize("dt,mode", [("bf16", 0), ("fp8", 2)])
+@pytest.mark.parametrize("s", [2, 4])
+def test_rccl_fed_gated_gemm_world1(comm, dt, mode, s):
+    """The RCCL-fed coll_pipeline's fused GEMM in one process: stage j's (world-1) RCCL
+    all-gather lands the "peer" rows in a stage-major gather buffer, a signal kernel on the comm
+    stream raises their ARRIVE flag, and ONE gated persistent pt4 reads A through a row-block
+    table: the own blocks in place (never gated, dispatched first: tile_order 3), the peer
+    blocks from the gather buffer (NaN-filled before every run, so a tile that did not wait
+    fails). Two junk GEMMs hold the comm stream back while the gated GEMM starts."""
+    from ddlb_amd.parallel.context import NativeContext
+    from ddlb_amd.parallel.plan import DT_BF16, DT_FP8, DT_U8, Plan, SIG_KERNEL
+
+    din = DT_FP8 if dt == "fp8" else DT_BF16
+    tdt = torch.float8_e4m3fn if dt == "fp8" else torch.bfloat16
+    es = 1 if dt == "fp8" else 2
+    M, N, K = 32768, 1024, 1024
+    ml = M // 2
+    rows = ml // s
+    plan = Plan(0, 1, nstreams=2, stream_priority=[0, 1])
+    own = plan.buffer("own", ml * K * es)
+    peer = plan.buffer("peer", ml * K * es)  # stands in for the peer's shard (its send buffer)
+    G = plan.buffer("G", ml * K * es)
+    bt = plan.buffer("bt", N * K * es)
+    c = plan.buffer("c", M * N * 2)
+    junk = plan.buffer("junk", M * N * 2)
+    fl = plan.buffer("flags", 256, zero=True)
+    for _ in range(2):
+        plan.gemm(1, own, bt, junk, M=ml, N=N, K=K, lda=K, ldb=K, ldc=N, din=din, dout=DT_BF16)
+    for j in range(s):
+        plan.allgather(1, peer + j * rows * K * es, G + j * rows * K * es, rows * K,
+                       DT_U8 if es == 1 else din)
+        plan.signal(1, [fl + 4 * (s + j)], method=SIG_KERNEL)
+    table = [own + j * rows * K * es for j in range(s)] + [G + j * rows * K * es
+                                                           for j in range(s)]
+    plan.gemm(0, own, bt, c, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, din=din, dout=DT_BF16, tile=19,
+              mode=mode, a_shards=table, shard_rows=rows, flags=fl, flag_rows=rows,
+              nshards=2 * s, nsub=s, first_shard=0, tile_order=3, reserve_cus=32)
+    ctx = NativeContext(comm)
+    bound = ctx.bind(plan)
+    A = (torch.rand(M, K, device="cuda") * 2 - 1).to(tdt)
+    W = (torch.rand(N, K, device="cuda") * 2 - 1).to(tdt)
+    bound.buffer("own").view(tdt).view(ml, K).copy_(A[:ml])
+    bound.buffer("peer").view(tdt).view(ml, K).copy_(A[ml:])
+    bound.buffer("bt").view(tdt).view(N, K).copy_(W)
+    ref = A.float() @ W.float().T
+    out = bound.buffer("c").view(torch.bfloat16).view(M, N)
+    for _ in range(3):
+        bound.buffer("G").view(torch.uint8).fill_(0x7F if es == 1 else 0xFF)  # NaN
+        out.zero_()
+        bound.run()
+        torch.cuda.synchronize()
+        bound.check_health()
+        err = float((out.float() - ref).abs().max())
+        assert err <= _tight(ref, K), err
+    bound.close()
+    ctx.close()
+
+
+@pytest.mark.parametrize("s", [2, 4])
+def test_rccl_fused_plans_world1_native(comm, s):
+    """The coll_pipeline / p2p_pipeline fused=True RCCL options through the primitive at world 1
+    (one GEMM there; the multi-rank schedule is covered by the simulator at d = 2..8)."""
+    from ddlb_amd.primitives.tp_columnwise.native import NativeTPColumnwise
+
+    for alg in ("coll_pipeline", "p2p_pipeline"):
+        impl = NativeTPColumnwise(m=4096, n=1024, k=1024, dtype="bfloat16", algorithm=alg,
+                                  backend="rccl", s=s, fused=True)
+        for _ in range(2):
+            out = impl.run()
+        torch.cuda.synchronize()
+        impl.validate(out)
+        impl.close()
+
+
 @pytest.mark.parametrize("tile,mode", [(0, 0), (18, 0), (4, 0)])
 def test_direct_store_gemm_world1(comm, tile, mode):
     """Direct-store C (c_shards): row block q of one GEMM lands in its own buffer (the peers'

@@ -158,11 +158,59 @@ def test_coll_fused_plan(d, sig, protocol):
 
 def test_fused_rejected_where_meaningless():
     for cfg in (AlgoConfig(algorithm="default", backend="ipc", fused=True),
-                AlgoConfig(algorithm="coll_pipeline", backend="rccl", fused=True),
+                AlgoConfig(algorithm="default", backend="rccl", fused=True),
+                AlgoConfig(algorithm="coll_pipeline", backend="rccl", order="AG_after",
+                           fused=True),
                 AlgoConfig(algorithm="p2p_pipeline", backend="ipc", order="AG_after",
                            fused=True)):
         with pytest.raises(ValueError):
             build_tp_columnwise(0, 2, 16, 8, 8, DT_F32, DT_F32, cfg)
+
+
+@pytest.mark.parametrize("d", [2, 3, 4, 8])
+@pytest.mark.parametrize("s", [1, 2, 8])
+def test_rccl_fused_coll_plan(d, s):
+    """coll_pipeline over RCCL feeding ONE gated GEMM: stage-major gather buffer, A through a
+    row-block table (own blocks read in place), local ARRIVE flags raised by signal kernels after
+    each stage's all-gather, own blocks dispatched first (tile_order 3)."""
+    cfg = AlgoConfig(algorithm="coll_pipeline", backend="rccl", fused=True, s=s)
+    _run_col(d, m=2 * d * s, n=8, k=12, cfg=cfg, epochs=3)
+    rank = 1
+    plan, io = build_tp_columnwise(rank, d, 2 * d * s, 8, 12, DT_F32, DT_F32, cfg)
+    g = [op for op in plan.ops if op.kind == OP_GEMM]
+    assert len(g) == 1 and g[0].args["M"] == 2 * d * s and g[0].args["tile_order"] == 3
+    assert g[0].args["nshards"] == d * s and g[0].args["nsub"] == s
+    assert g[0].args["first_shard"] == rank and g[0].args["shard_rows"] == 2
+    tab = g[0].args["a_shards"]
+    assert [t.buf for t in tab[rank * s:(rank + 1) * s]] == ["A_full"] * s
+    assert all(t.buf == "G" for i, t in enumerate(tab) if i // s != rank)
+    assert not plan.buffers["flags"].symmetric
+    sigs = [op for op in plan.ops if op.kind == OP_SIGNAL and op.stream == 1]
+    assert all(op.args["method"] == SIG_KERNEL for op in sigs) and len(sigs) >= s
+
+
+@pytest.mark.parametrize("d", [2, 3, 4, 8])
+def test_rccl_fused_p2p_plan(d):
+    """p2p_pipeline over RCCL send / recv feeding ONE gated GEMM (shard order from the own)."""
+    cfg = AlgoConfig(algorithm="p2p_pipeline", backend="rccl", fused=True)
+    _run_col(d, m=4 * d, n=8, k=12, cfg=cfg, epochs=3)
+    plan, _ = build_tp_columnwise(0, d, 4 * d, 8, 12, DT_F32, DT_F32, cfg)
+    g = [op for op in plan.ops if op.kind == OP_GEMM]
+    assert len(g) == 1 and g[0].args["nshards"] == d and g[0].args["flags"] is not None
+
+
+def test_rccl_fused_coll_negative_no_signal():
+    """Without the stage signal kernels the gated GEMM can never see the peers' blocks."""
+    from ddlb_amd.parallel.sim import Deadlock
+
+    cfg = AlgoConfig(algorithm="coll_pipeline", backend="rccl", fused=True, s=2)
+    built = [build_tp_columnwise(r, 2, 8, 8, 8, DT_F32, DT_F32, cfg) for r in range(2)]
+    plans = [p for p, _ in built]
+    for p in plans:
+        p.ops = [op for op in p.ops if not (op.kind == OP_SIGNAL and op.stream == 1)]
+    sim = Simulator(plans, make_buffers(plans))
+    with pytest.raises(Deadlock):
+        sim.run_epoch()
 
 
 @pytest.mark.parametrize("d", [1, 2, 3, 4])

@@ -12,7 +12,7 @@ NB = 4096
 
 
 @pytest.mark.parametrize("d", [2, 3, 4, 8])
-@pytest.mark.parametrize("phase", pf.IPC_PHASES)
+@pytest.mark.parametrize("phase", [p for p in pf.IPC_PHASES if p not in pf.PRIMITIVE_PHASES])
 def test_ipc_plan_moves_every_peers_pattern(d, phase):
     plans = [pf.build_ipc_plan(r, d, phase, NB) for r in range(d)]
     bufs = make_buffers(plans)
@@ -59,11 +59,18 @@ def test_rccl_plan(d):
 def test_needs_maps_candidates_to_checks():
     assert pf.needs("pytorch", {}) == ["torch_nccl"]
     assert pf.needs("native", {"backend": "rccl"}) == ["rccl"]
+    assert pf.needs("native", {"backend": "rccl", "fused": True}) == ["rccl", "rccl_fused"]
+    assert pf.needs("native", {"backend": "ipc", "multicast_protocol": "memcpy",
+                               "graph": False}) == ["ipc", "ipc_sdma"]
+    # no "graph" key = the option default "auto": graph replay signals with the kernels
     assert pf.needs("native", {"backend": "ipc", "multicast_protocol": "memcpy"}) == \
-        ["ipc", "ipc_sdma"]
+        ["ipc", "ipc_ksig", "ipc_sdma"]
     agk = pf.needs("native", {"backend": "ipc", "multicast_protocol": "kernel", "fused": True,
-                              "graph": True})
-    assert agk == ["ipc", "ipc_ksig", "ipc_kernel"]
+                              "algorithm": "coll_pipeline", "graph": True})
+    assert agk == ["ipc", "ipc_ksig", "ipc_kernel", "ipc_agk"]
+    dstore = pf.needs("native", {"backend": "ipc", "algorithm": "p2p_pipeline", "fused": True,
+                                 "graph": False}, primitive="tp_rowwise")
+    assert dstore == ["ipc", "ipc_ksig", "ipc_sdma", "ipc_dstore"]
     assert "ipc_kernel" in pf.needs("native", {"backend": "ipc", "algorithm": "direct"})
     assert "ipc_push" in pf.needs("native", {"backend": "ipc", "direction": "push"})
     assert pf.needs("compute_only", {}) == []
@@ -77,3 +84,28 @@ def test_merge_over_ranks():
     assert m["ipc"].startswith("ok")
     assert m["ipc_sdma"].startswith("failed: AssertionError")
     assert m["ipc_kernel"] == "failed: timeout"
+
+
+@pytest.mark.parametrize("d", [2, 3, 4, 8])
+@pytest.mark.parametrize("phase", sorted(pf.PRIMITIVE_PHASES))
+def test_primitive_phases_simulate(d, phase):
+    """The primitive-level phases (in-kernel AG, direct store, RCCL-fed gated GEMM) at their
+    preflight shape: the real plan builders, simulated for d ranks, exact."""
+    from ddlb_amd.parallel.algorithms import build_tp_columnwise, build_tp_rowwise
+    from ddlb_amd.parallel.plan import DT_F32
+    from ddlb_amd.primitives.native_common import algo_config
+    from ddlb_amd.primitives.registry import resolve
+
+    prim, opts = pf.PRIMITIVE_PHASES[phase]
+    m, n, k = pf.primitive_shape(d)
+    cls, o, _ = resolve(prim, "native", dict(opts))
+    merged = {**cls.DEFAULT_OPTIONS, **o}
+    for key, alias in cls.OPTION_ALIASES.items():
+        merged[key] = alias.get(merged[key], merged[key])
+    cfg = algo_config(merged)
+    build = build_tp_columnwise if prim == "tp_columnwise" else build_tp_rowwise
+    for r in range(d):  # the shape passes every builder check at every rank
+        build(r, d, m, n, k, DT_F32, DT_F32, cfg)
+    from test_plans_sim import _run_col, _run_row
+
+    (_run_col if prim == "tp_columnwise" else _run_row)(d, m, n, k, cfg, epochs=2)
