@@ -299,6 +299,11 @@ def child_main(a) -> int:
             res["harness_mean_ms"] = sum(ht) / len(ht)
             impl.check_health()
         res.update(ok=True, ms=float(t.item()), valid=valid)
+        if opts.get("multicast_protocol") == "batch_memcpy":
+            # a batch_memcpy time is a batched submission only if the API call succeeded
+            from ddlb_amd.ops import load
+
+            res["copy_batch"] = load().copy_batch_status()
         impl.close()
         comm.destroy()
     except Exception as e:  # reported to the parent, never raised
@@ -445,6 +450,9 @@ class Job:
             if errs:
                 res["max_err"] = max(errs)
                 res["err_bound"] = min(r["err_bound"] for r in results if "err_bound" in r)
+            cb = [r["copy_batch"] for r in results if "copy_batch" in r]
+            if cb:
+                res["copy_batch"] = cb[0]
             hm = [r["harness_mean_ms"] for r in results if "harness_mean_ms" in r]
             if hm:
                 res["harness_mean_ms"] = max(hm)
@@ -766,6 +774,7 @@ def main(argv=None) -> int:
             "harness_timing": "reference default: cpu_clock, barrier before every iteration, "
                               "MAX over ranks per iteration (ddlb/benchmark.py:161-172)",
             "max_err": final.get("max_err"), "err_bound": final.get("err_bound"),
+            "copy_batch": final.get("copy_batch"),
             "vendor_ms": vendor,
             "preflight": pre,
             "prewarm_ms": a.prewarm_ms,

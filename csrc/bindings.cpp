@@ -143,6 +143,7 @@ PYBIND11_MODULE(_C, m) {
           check(copy_launch(a, max_blocks, (hipStream_t)s), "copy_multi");
         });
   m.def("copy_batch_api_available", &copy_batch_api_available);
+  m.def("copy_batch_status", &copy_batch_status);
   m.def("copy_batch",  // copy-engine copies (dst, src, bytes) submitted as one batch
         [](std::vector<std::tuple<uintptr_t, uintptr_t, int64_t>> segs, uintptr_t s) {
           std::vector<void*> d, sr;
@@ -219,5 +220,6 @@ PYBIND11_MODULE(_C, m) {
       .def("host_times", &PlanExecutor::host_times)
       .def("set_cu_split", &PlanExecutor::set_cu_split)
       .def("cu_split", &PlanExecutor::cu_split)
+      .def("stream_info", &PlanExecutor::stream_info)
       .def("set_trace", &PlanExecutor::set_trace);
 }

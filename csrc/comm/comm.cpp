@@ -75,19 +75,25 @@ RcclMem::RcclMem(std::shared_ptr<RcclComm> comm, size_t bytes, int device)
 RcclMem::~RcclMem() {
   try {
     release();
+    if (ptr_ != nullptr) {
+      hipSetDevice(device_);
+      hipDeviceSynchronize();
+      ncclMemFree(ptr_);
+      ptr_ = nullptr;
+    }
   } catch (...) {
   }
 }
 
+// Deregister from the communicator now (it may be destroyed right after); the memory itself is
+// freed by the destructor, i.e. when the last owner goes — DLPack views handed to torch (e.g.
+// a rowwise plan's output slice returned by run()) hold one, so they stay valid after close().
 void RcclMem::release() {
-  if (ptr_ == nullptr) return;
+  if (ptr_ == nullptr || handle_ == nullptr) return;
   hipSetDevice(device_);
   hipDeviceSynchronize();
-  if (handle_ != nullptr && comm_ && comm_->get() != nullptr)
-    ncclCommDeregister(comm_->get(), handle_);
+  if (comm_ && comm_->get() != nullptr) ncclCommDeregister(comm_->get(), handle_);
   handle_ = nullptr;
-  ncclMemFree(ptr_);
-  ptr_ = nullptr;
 }
 
 SymmetricBuffer::SymmetricBuffer(size_t bytes, int device, bool uncached)

@@ -49,7 +49,8 @@ ncclDataType_t nccl_dtype(int dt);  // DT_* -> ncclDataType_t
 
 // A buffer RCCL may use zero-copy: allocated with ncclMemAlloc and registered with the
 // communicator (ncclCommRegister), the analogue of nvFuser's symmetric-memory allocations
-// (reference TPColumnwise/fuser.py:44-45). Deregistered and freed before the communicator goes.
+// (reference TPColumnwise/fuser.py:44-45). release() deregisters it while the communicator lives;
+// the memory is freed (ncclMemFree) when the last owner, e.g. a DLPack view, lets go.
 class RcclMem {
  public:
   RcclMem(std::shared_ptr<RcclComm> comm, size_t bytes, int device);

@@ -17,13 +17,12 @@ inline int dtype_size(int dt) {
   }
 }
 
+// Codes 5 (pp256), 8 / 9 (p256 / p128), 13 / 14 (pi256 / pi256w4) and 15 (r256) belonged to
+// kernel families retired in round 4 (no `auto` path reached them); they are refused.
 enum Tile : int { TILE_AUTO = 0, TILE_256x256 = 1, TILE_256x128 = 2, TILE_128x256 = 3,
-                  TILE_128x128 = 4, TILE_PP256 = 5, TILE_256x256_W4 = 6, TILE_256x128_W4 = 7,
-                  TILE_P256 = 8, TILE_P128 = 9,     // P*: persistent streaming variants
+                  TILE_128x128 = 4, TILE_256x256_W4 = 6, TILE_256x128_W4 = 7,
                   TILE_I256 = 10, TILE_I128 = 11,    // I*: DMA interleaved into the MFMAs
-                  TILE_I256W4 = 12, TILE_PI256 = 13,
-                  TILE_PI256W4 = 14,
-                  TILE_R256 = 15,     // R: persistent LDS-ring (3 K-steps in flight)
+                  TILE_I256W4 = 12,
                   TILE_T8 = 16,       // T8: 8-phase ping-pong, counted vmcnt (gemm_kernels.h)
                   TILE_PT8 = 17,      // PT8: persistent T8 (tiles streamed, C stores spread)
                   TILE_T4 = 18,       // T4: 2-phase ping-pong (32 MFMAs per section)

@@ -513,211 +513,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_tn_kernel(const GemmArgs p) 
   }
 }
 
-// ---------------------------------------------------------------- persistent streaming kernel
-// Same tile / staging / MFMA body as gemm_tn_kernel, but a fixed grid (one block per CU) walks
-// the tiles, and the (tile, k-step) pairs form ONE continuous stream: the last k-step of tile i
-// already stages k-step 0 of tile i+1, the epilogue of tile i issues its C stores, and the wait
-// before the next compute is a COUNTED vmcnt(NSTORE) — LDS-DMA and stores share the in-order
-// vmcnt queue, so waiting for "at most NSTORE outstanding" retires the (older) DMA while the C
-// stores keep draining under tile i+1's MFMAs. Exactly NSTORE stores must be issued per tile, so
-// this kernel is used only for full tiles (M % BM == 0, N % BN == 0): no store is predicated.
-template <class Mma, int OUT, int BM, int BN, int WM, int WN, bool ILV = false>
-__global__ __launch_bounds__(WM* WN * 64) void gemm_tn_persist_kernel(const GemmArgs p) {
-  constexpr int NW = WM * WN, ROWB = 128;
-  constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, STAGE = A_BYTES + B_BYTES;
-  constexpr int TM = BM / WM, TN = BN / WN, MR = TM / 16, NR = TN / 16;
-  constexpr int LA = BM / 8 / NW, LB = BN / 8 / NW;
-  // vmcnt is a 6-bit counter: with more stores per tile, wait for a few of them too (safe).
-  constexpr int NSTORE = MR * NR < 63 ? MR * NR : 63;
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int tiles_n = p.N / BN, tiles_m = p.M / BM, ntiles = tiles_m * tiles_n;
-  const int esz = Mma::kElem;
-  const int nk = p.K * esz / ROWB;
-  const int my_tiles = ((int)blockIdx.x < ntiles) ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
-  const int total = my_tiles * nk;
-  if (total == 0) return;
-
-  const char* aptr[LA];
-  const char* bptr[LB];
-  int cur_tile = -1;
-  auto set_tile = [&](int i) __attribute__((always_inline)) {  // i-th tile of this block -> source pointers
-    const int wg = tile_index_virtual(p, (int)blockIdx.x + i * (int)gridDim.x, ntiles);
-    const int64_t m0 = (int64_t)(wg / tiles_n) * BM, n0 = (int64_t)(wg % tiles_n) * BN;
-#pragma unroll
-    for (int r = 0; r < LA; ++r) {
-      const int row = (wave * LA + r) * 8 + (lane >> 3);
-      const int chunk = (lane & 7) ^ ((row >> 1) & 7);
-      aptr[r] = (const char*)p.a + map_row(m0 + row, p.a_grp, p.a_gstride) * p.lda * esz +
-                chunk * 16;
-    }
-#pragma unroll
-    for (int r = 0; r < LB; ++r) {
-      const int row = (wave * LB + r) * 8 + (lane >> 3);
-      const int chunk = (lane & 7) ^ ((row >> 1) & 7);
-      bptr[r] = (const char*)p.b + (n0 + row) * p.ldb * esz + chunk * 16;
-    }
-  };
-  auto stage = [&](int buf, int g) __attribute__((always_inline)) {
-    const int ti = g / nk, kt = g - ti * nk;
-    if (ti != cur_tile) {
-      set_tile(ti);
-      cur_tile = ti;
-    }
-    char* base = smem + buf * STAGE;
-    const int64_t koff = (int64_t)kt * ROWB;
-#pragma unroll
-    for (int i = 0; i < LA; ++i) glds16(aptr[i] + koff, base + (wave * LA + i) * 1024);
-#pragma unroll
-    for (int i = 0; i < LB; ++i) glds16(bptr[i] + koff, base + A_BYTES + (wave * LB + i) * 1024);
-  };
-
-  const int wm = wave / WN, wn = wave % WN;
-  const int swz = (lane & 15) >> 1, frow = lane & 15, fq = lane >> 4;
-  f32x4 acc[MR][NR];
-#pragma unroll
-  for (int i = 0; i < MR; ++i)
-#pragma unroll
-    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto compute = [&](int buf) __attribute__((always_inline)) {
-    const char* As = smem + buf * STAGE;
-    const char* Bs = As + A_BYTES;
-#pragma unroll
-    for (int c4 = 0; c4 < 8; c4 += 4) {
-      const int choff = ((c4 + fq) ^ swz) * 16;
-      i32x4 af[MR], bfr[NR];
-#pragma unroll
-      for (int i = 0; i < MR; ++i)
-        af[i] = *(const i32x4*)(As + (wm * TM + i * 16 + frow) * ROWB + choff);
-#pragma unroll
-      for (int j = 0; j < NR; ++j)
-        bfr[j] = *(const i32x4*)(Bs + (wn * TN + j * 16 + frow) * ROWB + choff);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < MR; ++i)
-#pragma unroll
-        for (int j = 0; j < NR; ++j) Mma::step(acc[i][j], bfr[j], af[i]);
-      __builtin_amdgcn_s_setprio(0);
-    }
-  };
-  constexpr int OSZ = out_size<OUT>();
-  auto epilogue = [&](int ti) __attribute__((always_inline)) {
-    const int wg = tile_index_virtual(p, (int)blockIdx.x + ti * (int)gridDim.x, ntiles);
-    const int64_t m0 = (int64_t)(wg / tiles_n) * BM, n0 = (int64_t)(wg % tiles_n) * BN;
-#pragma unroll
-    for (int i = 0; i < MR; ++i) {
-      const int64_t row = m0 + wm * TM + i * 16 + frow;
-      char* crow = c_row<OSZ>(p, row);
-#pragma unroll
-      for (int j = 0; j < NR; ++j) {
-        const int64_t col = n0 + wn * TN + j * 16 + fq * 4;
-        Store4<OUT>::st(crow + col * OSZ, act4(acc[i][j], p.act));
-        acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
-  };
-
-  // interleaved compute (see gemm_tn_kernel::compute_ilv): next step's DMA + second-half
-  // fragment reads issued between the first-half MFMAs
-  auto compute_ilv = [&](int buf, int64_t koff) __attribute__((always_inline)) {
-    constexpr int NDMA = LA + LB, NRD = MR + NR, NQ = MR * NR;
-    constexpr int PER = NQ / NDMA > 0 ? NQ / NDMA : 1;
-    const char* As = smem + buf * STAGE;
-    const char* Bs = As + A_BYTES;
-    char* nbase = smem + (buf ^ 1) * STAGE;
-    const int ch0 = ((0 + fq) ^ swz) * 16, ch1 = ((4 + fq) ^ swz) * 16;
-    i32x4 af0[MR], bf0[NR], af1[MR], bf1[NR];
-#pragma unroll
-    for (int i = 0; i < MR; ++i)
-      af0[i] = *(const i32x4*)(As + (wm * TM + i * 16 + frow) * ROWB + ch0);
-#pragma unroll
-    for (int j = 0; j < NR; ++j)
-      bf0[j] = *(const i32x4*)(Bs + (wn * TN + j * 16 + frow) * ROWB + ch0);
-    auto rd1 = [&](int r) __attribute__((always_inline)) {
-      if (r < MR) af1[r] = *(const i32x4*)(As + (wm * TM + r * 16 + frow) * ROWB + ch1);
-      else bf1[r - MR] = *(const i32x4*)(Bs + (wn * TN + (r - MR) * 16 + frow) * ROWB + ch1);
-    };
-    auto dma = [&](int d) __attribute__((always_inline)) {
-      if (d < LA) glds16(aptr[d] + koff, nbase + (wave * LA + d) * 1024);
-      else glds16(bptr[d - LA] + koff, nbase + A_BYTES + (wave * LB + d - LA) * 1024);
-    };
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      Mma::step(acc[q / NR][q % NR], bf0[q % NR], af0[q / NR]);
-      if ((q % PER) == PER - 1) {
-        const int gg = q / PER;
-        if (gg < NDMA) dma(gg);
-#pragma unroll
-        for (int r = (gg * NRD) / NDMA; r < ((gg + 1) * NRD) / NDMA; ++r) rd1(r);
-      }
-    }
-#pragma unroll
-    for (int d = NQ / PER; d < NDMA; ++d) dma(d);
-#pragma unroll
-    for (int r = ((NQ / PER) * NRD) / NDMA; r < NRD; ++r) rd1(r);
-    IlvPattern<0, (NDMA < NQ / PER ? NDMA : NQ / PER), PER, NRD, NDMA>::emit();
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) Mma::step(acc[q / NR][q % NR], bf1[q % NR], af1[q / NR]);
-    __builtin_amdgcn_s_setprio(0);
-  };
-
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  int cur = 0;
-  for (int g = 0; g < total; ++g) {
-    const bool more = g + 1 < total;
-    if constexpr (ILV) {
-      // last step of the stream: re-stage the current k-step into the idle buffer (never read)
-      const int gn = more ? g + 1 : g;
-      const int ti = gn / nk;
-      if (ti != cur_tile) {
-        set_tile(ti);
-        cur_tile = ti;
-      }
-      compute_ilv(cur, (int64_t)(gn - ti * nk) * ROWB);
-    } else {
-      if (more) stage(cur ^ 1, g + 1);
-      compute(cur);
-    }
-    const bool last_k = (g % nk) == nk - 1;
-    if (last_k) {
-      __builtin_amdgcn_sched_barrier(0);
-      epilogue(g / nk);
-      __builtin_amdgcn_sched_barrier(0);
-      if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSTORE) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    cur ^= 1;
-  }
-  // never leave an LDS-DMA in flight past the end of the workgroup (its LDS is reassigned)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// ---------------------------------------------------------------- ring kernel (default for big grids)
-// Persistent 256x256 tiles, 8 waves (2 x 4, 128x64 outputs per wave), K sliced into 64-BYTE
-// steps (32 bf16/f16, 64 fp8, 16 f32) held in a 4-slot LDS ring filled by LDS-DMA. Three steps
-// are in flight across barriers (counted vmcnt, never 0 inside the stream), and the single
-// barrier of a step sits in the MIDDLE of its MFMAs, so the matrix pipe never waits for fragment
-// reads:
-//   part A : MFMAs of fragment rows 0-3 (A0 x Bc) | half of the DMA of step g+3 | reads of A1
-//   wait   : vmcnt until step g+1's DMA landed, lgkmcnt(0), s_barrier
-//   part C : MFMAs of rows 4-7 (A1 x Bc) | other DMA half | reads of A0 and Bn for step g+1
-// Slot reuse: step g's DMA refills slot (g-1)%4, whose last reads (step g-1's A1, issued in part
-// A of step g-1) retired before barrier g-1. Visibility: reads of slot (g+1)%4 happen after
-// barrier g, which every wave reaches only after its own DMA for step g+1 retired.
-// The B operand is staged with its columns permuted inside each 32-column block so that a lane's
-// two adjacent 16x16 fragments hold 8 CONSECUTIVE output columns: one 16-byte store per pair
-// (half the store instructions of the plain layout). C stores of tile i drain under tile i+1
-// (they are counted in the vmcnt arithmetic). Measured on MI355X (profiles/r01/lab): +7-9 % over
-// the 2-stage interleaved kernels and ~2-3 % over hipBLASLt on 65536x1024x1024 bf16.
-__device__ __forceinline__ int swz64(int row) { return (row >> 1) & 2; }  // conflict-free 64-B rows
-
+// ---------------------------------------------------------------- counted waits, C stores
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -776,351 +572,6 @@ __device__ __forceinline__ void store8_wt(__amdgpu_buffer_rsrc_t rc, unsigned of
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), rc, off, soff, AUX);
   }
 }
-
-template <class Mma, int OUT>
-__global__ __launch_bounds__(512) void gemm_tn_ring_kernel(const GemmArgs p) {
-  constexpr int NS = 4, BM = 256, BN = 256, WN = 4, ROWB = 64;
-  constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB, SLOT = A_BYTES + B_BYTES;
-  constexpr int TM = 128, TN = 64, MR = TM / 16, NR = TN / 16, MH = MR / 2;
-  constexpr int LA = BM / 16 / 8, LB = BN / 16 / 8, NDMA = LA + LB;  // DMAs per wave per step
-  constexpr int DA = NDMA / 2;                                       // ... issued in part A
-  constexpr int NSTORE = MR * NR / 2 * Store8<OUT>::kStores;
-  constexpr int KM = Mma::kMfma;
-  static_assert(NDMA == 4 && MH * NR == 16, "schedule below is written for this geometry");
-  __shared__ __attribute__((aligned(1024))) char smem[NS * SLOT];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int tiles_n = p.N / BN, tiles_m = p.M / BM, ntiles = tiles_m * tiles_n;
-  const int esz = Mma::kElem;
-  const int nk = p.K * esz / ROWB;
-  const int my_tiles =
-      ((int)blockIdx.x < ntiles) ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
-  const int total = my_tiles * nk;
-  if (total == 0) return;
-
-  // DMA lanes: 16 rows x 64 B per instruction, lane -> (row lane>>2, physical chunk lane&3)
-  const int drow = lane >> 2, dchunk = lane & 3;
-  const char* abase[LA];
-  const char* bbase[LB];
-  int dma_tile = -1;
-  auto set_dma_tile = [&](int ti) __attribute__((always_inline)) {
-    const int wg = tile_index_virtual(p, (int)blockIdx.x + ti * (int)gridDim.x, ntiles);
-    const int64_t m0 = (int64_t)(wg / tiles_n) * BM, n0 = (int64_t)(wg % tiles_n) * BN;
-#pragma unroll
-    for (int i = 0; i < LA; ++i) {
-      const int row = (wave * LA + i) * 16 + drow;
-      abase[i] = a_row(p, m0 + row, esz) + ((dchunk ^ swz64(row)) * 16);
-    }
-#pragma unroll
-    for (int i = 0; i < LB; ++i) {
-      const int row = (wave * LB + i) * 16 + drow;
-      const int t32 = row & 31;
-      const int col = (row & ~31) + 8 * ((t32 & 15) >> 2) + 4 * (t32 >> 4) + (t32 & 3);
-      bbase[i] = (const char*)p.b + (n0 + col) * p.ldb * esz + ((dchunk ^ swz64(row)) * 16);
-    }
-  };
-  // Source offset of stream step g. Past the end the last step is re-staged into a slot no one
-  // reads again, which keeps every step's vmcnt arithmetic identical.
-  auto prep = [&](int g) -> int64_t {
-    g = g < total ? g : total - 1;
-    const int ti = g / nk;
-    if (ti != dma_tile) {
-      set_dma_tile(ti);
-      dma_tile = ti;
-    }
-    return (int64_t)(g - ti * nk) * ROWB;
-  };
-  auto dma = [&](int d, int64_t koff, char* base) __attribute__((always_inline)) {
-    if (d < LA) glds16(abase[d] + koff, base + (wave * LA + d) * 1024);
-    else glds16(bbase[d - LA] + koff, base + A_BYTES + (wave * LB + d - LA) * 1024);
-  };
-
-  const int wm = wave / WN, wn = wave % WN;
-  const int frow = lane & 15, fq = lane >> 4;
-  const int rdoff = frow * ROWB + ((fq ^ swz64(frow)) * 16);
-  const int aoff = wm * TM * ROWB + rdoff, boff = A_BYTES + wn * TN * ROWB + rdoff;
-  f32x4 acc[MR][NR];
-#pragma unroll
-  for (int i = 0; i < MR; ++i)
-#pragma unroll
-    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  for (int g = 0; g < NS - 1; ++g) {
-    const int64_t koff = prep(g);
-#pragma unroll
-    for (int d = 0; d < NDMA; ++d) dma(d, koff, smem + (g % NS) * SLOT);
-  }
-  wait_vm<NDMA*(NS - 2)>();
-  __builtin_amdgcn_s_barrier();
-  i32x4 A0[MH], A1[MH], Bc[NR], Bn[NR];
-#pragma unroll
-  for (int j = 0; j < NR; ++j) Bc[j] = *(const i32x4*)(smem + boff + j * 16 * ROWB);
-#pragma unroll
-  for (int i = 0; i < MH; ++i) A0[i] = *(const i32x4*)(smem + aoff + i * 16 * ROWB);
-
-  constexpr int OSZ = out_size<OUT>();
-  int stores_window = 0;  // bit j: step g-1-j issued C stores
-  for (int g = 0; g < total; ++g) {
-    const char* cur = smem + (g % NS) * SLOT;
-    const char* nxt = smem + ((g + 1) % NS) * SLOT;
-    const int64_t koff = prep(g + NS - 1);
-    char* nbase = smem + ((g + NS - 1) % NS) * SLOT;
-    // ---- part A
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int q = 0; q < MH * NR; ++q) {
-      const int i = q / NR, j = q % NR;
-      Mma::step(acc[i][j], Bc[j], A0[i]);
-      if (q % 8 == 1) dma(q / 8, koff, nbase);
-      if (q % 4 == 3) A1[q / 4] = *(const i32x4*)(cur + aoff + (MH + q / 4) * 16 * ROWB);
-    }
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 2 * KM, 0);
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 2 * KM, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 4 * KM, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    }
-    __builtin_amdgcn_s_setprio(0);
-    // ---- wait for step g+1's DMA: issued after it are the DMAs of steps g+2..g+2 (both halves),
-    //      the part-A half of step g+3 and the C stores of tiles that ended in steps g-2..g-1
-    constexpr int VMB = NDMA * (NS - 2) - (NDMA - DA);
-    const int nst = __builtin_popcount(stores_window);
-    if (nst == 0) wait_vm<VMB>();
-    else if (nst == 1) wait_vm<(VMB + NSTORE < 63 ? VMB + NSTORE : 63)>();
-    else wait_vm<(VMB + 2 * NSTORE < 63 ? VMB + 2 * NSTORE : 63)>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    // ---- part C
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int q = 0; q < MH * NR; ++q) {
-      const int j = q / MH, i = MH + q % MH;  // j-major: Bc[j] is free after its 4 MFMAs
-      Mma::step(acc[i][j], Bc[j], A1[i - MH]);
-      if (q % 2 == 1) {
-        const int r = q / 2;  // Bn[0..3], then A0[0..3] of step g+1
-        if (r < NR) Bn[r] = *(const i32x4*)(nxt + boff + r * 16 * ROWB);
-        else A0[r - NR] = *(const i32x4*)(nxt + aoff + (r - NR) * 16 * ROWB);
-      }
-      if (q % 8 == 0) dma(DA + q / 8, koff, nbase);
-    }
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 2 * KM, 0);
-      if (r % 4 == 0) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    }
-    __builtin_amdgcn_s_setprio(0);
-#pragma unroll
-    for (int j = 0; j < NR; ++j) Bc[j] = Bn[j];
-
-    const int ti = g / nk;
-    const bool last_k = (g - ti * nk) == nk - 1;
-    stores_window = (stores_window << 1) & ((1 << (NS - 2)) - 1);
-    if (last_k) {
-      const int wg = tile_index_virtual(p, (int)blockIdx.x + ti * (int)gridDim.x, ntiles);
-      const int64_t m0 = (int64_t)(wg / tiles_n) * BM, n0 = (int64_t)(wg % tiles_n) * BN;
-      __builtin_amdgcn_sched_barrier(0);
-      if (p.act == ACT_NONE) {
-#pragma unroll
-        for (int i = 0; i < MR; ++i) {
-          char* crow = c_row<OSZ>(p, m0 + wm * TM + i * 16 + frow);
-#pragma unroll
-          for (int jp = 0; jp < NR / 2; ++jp)
-            Store8<OUT>::st(crow + (n0 + wn * TN + jp * 32 + fq * 8) * OSZ, acc[i][2 * jp],
-                            acc[i][2 * jp + 1]);
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < MR; ++i) {
-          char* crow = c_row<OSZ>(p, m0 + wm * TM + i * 16 + frow);
-#pragma unroll
-          for (int jp = 0; jp < NR / 2; ++jp)
-            Store8<OUT>::st(crow + (n0 + wn * TN + jp * 32 + fq * 8) * OSZ,
-                            act4(acc[i][2 * jp], p.act), act4(acc[i][2 * jp + 1], p.act));
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < MR; ++i)
-#pragma unroll
-        for (int j = 0; j < NR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      __builtin_amdgcn_sched_barrier(0);
-      stores_window |= 1;
-    }
-  }
-  // never leave an LDS-DMA in flight past the end of the workgroup
-  wait_vm<0>();
-}
-
-// ---------------------------------------------------------------- 256x256 ping-pong kernel
-// 8 waves = 2 groups (wr = 0: waves 0-3, wr = 1: waves 4-7; every SIMD hosts one wave of each)
-// x 4 column waves. Each wave owns a 128x64 output tile = 2x2 quadrants of 64x32 and runs, per
-// 64-deep K-tile, 4 phases of {LOAD section: ds_read the quadrant's fragments (+ LDS-DMA of the
-// next K-tile) | barrier | COMP section: 16 MFMAs | barrier}. Group 1 starts one barrier later,
-// so in every interval between two barriers one group computes while the other loads
-// (cdna guide §5 "256^2 8-phase template", T3/T4/T5).
-//
-// Sections of group 0 are numbered s = 8t + {0 L1, 1 C1, 2 L2, 3 C2, 4 L3, 5 C3, 6 L4, 7 C4} and
-// run between barriers B[s+1] and B[s+2]; group 1's section s runs between B[s+2] and B[s+3].
-//  * tile t+1 -> buffer (t+1)&1: group 1 issues its DMA in L1, L2 of tile t, group 0 in L2, L3.
-//    WAR: the last reads of tile t-1 (both groups' L4) retire in their C4, i.e. by B[8t+2],
-//    and group 1's L1 of tile t starts at B[8t+2].
-//  * RAW: group 0 waits vmcnt(0) at the end of C4 (before B[8t+9]), group 1 at the end of its
-//    L4 (before B[8t+9]); the first read of tile t+1 (group 0's L1) starts after B[8t+9].
-//  * Barrier balance: group 1 executes one extra barrier before the loop, group 0 one after it.
-template <class Mma, int OUT>
-__global__ __launch_bounds__(512) void gemm_tn_pp256_kernel(const GemmArgs p) {
-  constexpr int BM = 256, BN = 256, ROWB = 128;
-  constexpr int A_BYTES = BM * ROWB, STAGE = A_BYTES + BN * ROWB;
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 2, wc = wave & 3;
-  const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
-  const int wg = tile_index(p, tiles_m * tiles_n);
-  const int tm = wg / tiles_n, tn = wg % tiles_n;
-  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
-  const int esz = Mma::kElem;
-
-  // LDS-DMA sources: this wave stages rows [32*wave, 32*wave+32) of A and of B (4 x 8 rows each)
-  const char* aptr[4];
-  const char* bptr[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = (wave * 4 + i) * 8 + (lane >> 3);
-    int64_t gr = m0 + row;
-    gr = gr < p.M ? gr : p.M - 1;
-    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
-    aptr[i] = (const char*)p.a + map_row(gr, p.a_grp, p.a_gstride) * p.lda * esz + chunk * 16;
-    int64_t gc = n0 + row;
-    gc = gc < p.N ? gc : p.N - 1;
-    bptr[i] = (const char*)p.b + gc * p.ldb * esz + chunk * 16;
-  }
-  wait_tile(p, m0, BM);
-
-  // part 0: A rows 0-15 + B rows 0-15 of this wave's 32; part 1: the other 16 of each
-  auto stage_part = [&](int buf, int kt, int part) __attribute__((always_inline)) {
-    char* base = smem + buf * STAGE;
-    const int64_t koff = (int64_t)kt * ROWB;
-#pragma unroll
-    for (int i = 2 * part; i < 2 * part + 2; ++i) {
-      glds16(aptr[i] + koff, base + (wave * 4 + i) * 1024);
-      glds16(bptr[i] + koff, base + A_BYTES + (wave * 4 + i) * 1024);
-    }
-  };
-
-  const int swz = (lane & 15) >> 1, frow = lane & 15, fq = lane >> 4;
-  const int c0 = ((0 + fq) ^ swz) * 16, c1 = ((4 + fq) ^ swz) * 16;
-  const int arow0 = (wr * 128 + frow) * ROWB, brow0 = (wc * 64 + frow) * ROWB;
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  i32x4 aR[4][2], bR[2][2];
-
-  auto loadA = [&](const char* As, int mq) __attribute__((always_inline)) {
-#pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      const char* r = As + arow0 + (mq * 64 + f * 16) * ROWB;
-      aR[f][0] = *(const i32x4*)(r + c0);
-      aR[f][1] = *(const i32x4*)(r + c1);
-    }
-  };
-  auto loadB = [&](const char* Bs, int nq) __attribute__((always_inline)) {
-#pragma unroll
-    for (int f = 0; f < 2; ++f) {
-      const char* r = Bs + brow0 + (nq * 32 + f * 16) * ROWB;
-      bR[f][0] = *(const i32x4*)(r + c0);
-      bR[f][1] = *(const i32x4*)(r + c1);
-    }
-  };
-  auto comp = [&](int mq, int nq) __attribute__((always_inline)) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int f = 0; f < 4; ++f)
-#pragma unroll
-        for (int g = 0; g < 2; ++g) Mma::step(acc[mq * 4 + f][nq * 2 + g], bR[g][kk], aR[f][kk]);
-    __builtin_amdgcn_s_setprio(0);
-  };
-#define PP_BAR()                            \
-  do {                                      \
-    __builtin_amdgcn_sched_barrier(0);      \
-    __builtin_amdgcn_s_barrier();           \
-    __builtin_amdgcn_sched_barrier(0);      \
-  } while (0)
-#define PP_VM0() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
-
-  const int nk = p.K * esz / ROWB;
-  stage_part(0, 0, 0);
-  stage_part(0, 0, 1);
-  PP_VM0();
-  PP_BAR();
-  const bool g1 = wr == 1;  // wave-uniform (wave came through readfirstlane)
-  if (g1) PP_BAR();
-  for (int t = 0; t < nk; ++t) {
-    const char* As = smem + (t & 1) * STAGE;
-    const char* Bs = As + A_BYTES;
-    const int nb = (t + 1) & 1;
-    const bool nxt = t + 1 < nk;
-    // L1
-    loadA(As, 0);
-    loadB(Bs, 0);
-    if (g1 && nxt) stage_part(nb, t + 1, 0);
-    PP_BAR();
-    comp(0, 0);
-    PP_BAR();
-    // L2
-    loadB(Bs, 1);
-    if (nxt) stage_part(nb, t + 1, g1 ? 1 : 0);
-    PP_BAR();
-    comp(0, 1);
-    PP_BAR();
-    // L3
-    loadA(As, 1);
-    if (!g1 && nxt) stage_part(nb, t + 1, 1);
-    PP_BAR();
-    comp(1, 1);
-    PP_BAR();
-    // L4
-    loadB(Bs, 0);
-    if (g1) PP_VM0();
-    PP_BAR();
-    comp(1, 0);
-    if (!g1) PP_VM0();
-    PP_BAR();
-  }
-  if (!g1) PP_BAR();
-#undef PP_BAR
-#undef PP_VM0
-
-  constexpr int OSZ = out_size<OUT>();
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int64_t row = m0 + wr * 128 + (i >> 2) * 64 + (i & 3) * 16 + frow;
-    if (row >= p.M) continue;
-    char* crow = c_row<OSZ>(p, row);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t col = n0 + wc * 64 + (j >> 1) * 32 + (j & 1) * 16 + fq * 4;
-      if (col + 3 < p.N) {
-        Store4<OUT>::st(crow + col * OSZ, act4(acc[i][j], p.act));
-      } else {
-        const f32x4 a4 = act4(acc[i][j], p.act);
-        const float v[4] = {a4.x, a4.y, a4.z, a4.w};
-        for (int r = 0; r < 4; ++r)
-          if (col + r < p.N) Store4<OUT>::st1(crow + (col + r) * OSZ, v[r]);
-      }
-    }
-  }
-}
-
 
 // ---------------------------------------------------------------- t8: 8-phase ping-pong kernel
 // 256x256 tile, BK = one 128-byte row (64 bf16 / 128 fp8 / 32 f32), 8 waves = 2 groups (wr) x 4
@@ -2328,12 +1779,6 @@ hipError_t launch_mx(const GemmArgs& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-// The ring kernel streams whole tiles only (its vmcnt arithmetic counts every C store) and does
-// not take arrival flags.
-bool ring_ok(const GemmArgs& p) {
-  return p.M % 256 == 0 && p.N % 256 == 0 && p.flags == nullptr;
-}
-
 int num_cus() {
   static int n = 0;
   if (n == 0) {
@@ -2343,29 +1788,6 @@ int num_cus() {
       n = 256;
   }
   return n;
-}
-
-template <class Mma, int OUT, int BM, int BN, int WM, int WN, bool ILV = false>
-hipError_t launch_persist(const GemmArgs& p, int blocks_per_cu, hipStream_t s) {
-  const int tiles = (p.M / BM) * (p.N / BN);
-  int grid = num_cus() * blocks_per_cu;
-  grid = (grid / 8) * 8;  // keep blockIdx % 8 == XCD group for every virtual tile id
-  if (grid > tiles) grid = tiles;
-  if (grid < 1) grid = 1;
-  hipLaunchKernelGGL((gemm_tn_persist_kernel<Mma, OUT, BM, BN, WM, WN, ILV>), dim3(grid),
-                     dim3(WM * WN * 64), 0, s, p);
-  return hipGetLastError();
-}
-
-template <class Mma, int OUT>
-hipError_t launch_ring(const GemmArgs& p, hipStream_t s) {
-  const int tiles = (p.M / 256) * (p.N / 256);
-  int grid = num_cus();
-  grid = (grid / 8) * 8;  // blockIdx % 8 == XCD group for every virtual tile id
-  if (grid > tiles) grid = tiles;
-  if (grid < 1) grid = 1;
-  hipLaunchKernelGGL((gemm_tn_ring_kernel<Mma, OUT>), dim3(grid), dim3(512), 0, s, p);
-  return hipGetLastError();
 }
 
 // t8 takes whole 256x256 tiles (flags, grouped rows, shard tables and activations allowed)
@@ -2468,17 +1890,12 @@ template <class Mma, int OUT>
 hipError_t launch_pt8(const GemmArgs& p, hipStream_t s) {
   const int tiles = (p.M / 256) * (p.N / 256);
   int grid = num_cus();
+  // a CU split's masked compute stream: one workgroup per CU it may use (see launch_pt4)
+  if (p.reserve_cus > 0 && p.reserve_cus < grid) grid -= p.reserve_cus;
   grid = (grid / 8) * 8;  // blockIdx % 8 == XCD group for every virtual tile id
   if (grid > tiles) grid = tiles;
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL((gemm_tn_pt8_kernel<Mma, OUT>), dim3(grid), dim3(512), 0, s, p);
-  return hipGetLastError();
-}
-
-template <class Mma, int OUT>
-hipError_t launch_pp256(const GemmArgs& p, hipStream_t s) {
-  const int tiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
-  hipLaunchKernelGGL((gemm_tn_pp256_kernel<Mma, OUT>), dim3(tiles), dim3(512), 0, s, p);
   return hipGetLastError();
 }
 
@@ -2500,10 +1917,6 @@ hipError_t launch_cfg(const GemmArgs& p, int tile, hipStream_t s) {
     case TILE_T8:
       if (t8_ok(p)) return launch_t8<Mma, OUT>(p, s);
       return launch_tiled<Mma, OUT, 256, 256, 2, 4, true>(p, s);
-    case TILE_R256:
-      if (ring_ok(p)) return launch_ring<Mma, OUT>(p, s);
-      return launch_tiled<Mma, OUT, 256, 256, 2, 4, true>(p, s);
-    case TILE_PP256: return launch_pp256<Mma, OUT>(p, s);
     case TILE_256x256: return launch_tiled<Mma, OUT, 256, 256, 2, 4>(p, s);
     case TILE_256x128: return launch_tiled<Mma, OUT, 256, 128, 4, 2>(p, s);
     case TILE_128x256: return launch_tiled<Mma, OUT, 128, 256, 2, 4>(p, s);
@@ -2513,54 +1926,34 @@ hipError_t launch_cfg(const GemmArgs& p, int tile, hipStream_t s) {
     case TILE_I256: return launch_tiled<Mma, OUT, 256, 256, 2, 4, true>(p, s);
     case TILE_I128: return launch_tiled<Mma, OUT, 128, 128, 2, 2, true>(p, s);
     case TILE_I256W4: return launch_tiled<Mma, OUT, 256, 256, 2, 2, true>(p, s);
-    case TILE_PI256:
-      if (p.M % 256 == 0 && p.N % 256 == 0 && p.flags == nullptr)
-        return launch_persist<Mma, OUT, 256, 256, 2, 4, true>(p, 1, s);
-      return launch_tiled<Mma, OUT, 256, 256, 2, 4, true>(p, s);
-    case TILE_PI256W4:
-      if (p.M % 256 == 0 && p.N % 256 == 0 && p.flags == nullptr)
-        return launch_persist<Mma, OUT, 256, 256, 2, 2, true>(p, 1, s);
-      return launch_tiled<Mma, OUT, 256, 256, 2, 2, true>(p, s);
-    case TILE_P256:
-      if (p.M % 256 == 0 && p.N % 256 == 0 && p.flags == nullptr)
-        return launch_persist<Mma, OUT, 256, 256, 2, 4>(p, 1, s);
-      return launch_tiled<Mma, OUT, 256, 256, 2, 4>(p, s);
-    case TILE_P128:
-      if (p.M % 128 == 0 && p.N % 128 == 0 && p.flags == nullptr)
-        return launch_persist<Mma, OUT, 128, 128, 2, 2>(p, 2, s);
-      return launch_tiled<Mma, OUT, 128, 128, 2, 2>(p, s);
-    default: return hipErrorInvalidValue;
+    default: return hipErrorInvalidValue;  // (5, 8, 9, 13-15: retired kernel families)
   }
 }
 template <int OUT>
 hipError_t launch_mx_cfg(const GemmArgs& p, int tile, hipStream_t s) {
-  // whole 256x256 tiles: the 8-phase ping-pong schedule (persistent with >= 2 tiles per CU)
+  // whole 256x256 tiles: the ping-pong schedules (persistent with >= 2 tiles per CU)
   if (tile == TILE_PT4 && pt4_ok(p, 1) && !(p.c_table && (p.a_table || p.a_grp != p.M)))
     return launch_pt4<MmaMX, OUT>(p, s);
   if ((tile == TILE_T4 || tile == TILE_PT4) && t8_ok(p)) return launch_t4<MmaMX, OUT>(p, s);
-  if ((tile == TILE_T8 || tile == TILE_PT8 || tile == TILE_R256 || tile == TILE_AUTO) && t8_ok(p)) {
+  if ((tile == TILE_T8 || tile == TILE_PT8 || tile == TILE_AUTO) && t8_ok(p)) {
     const int tiles = (p.M / 256) * (p.N / 256);
     if (tile != TILE_T8 && p.flags == nullptr && tiles >= 2 * num_cus())
       return launch_pt8<MmaMX, OUT>(p, s);
     return launch_t8<MmaMX, OUT>(p, s);
   }
   switch (tile) {
-    case TILE_PP256:
     case TILE_256x256: return launch_mx<OUT, 256, 256, 2, 4>(p, s);
     case TILE_256x128: return launch_mx<OUT, 256, 128, 4, 2>(p, s);
     case TILE_128x256: return launch_mx<OUT, 128, 256, 2, 4>(p, s);
     case TILE_128x128: return launch_mx<OUT, 128, 128, 2, 2>(p, s);
     case TILE_256x256_W4: return launch_mx<OUT, 256, 256, 2, 2>(p, s);
-    case TILE_P256: case TILE_I256: return launch_mx<OUT, 256, 256, 2, 4>(p, s);
+    case TILE_I256: return launch_mx<OUT, 256, 256, 2, 4>(p, s);
     case TILE_I128: return launch_mx<OUT, 128, 128, 2, 2>(p, s);
     case TILE_I256W4: return launch_mx<OUT, 256, 256, 2, 2>(p, s);
-    case TILE_PI256: return launch_mx<OUT, 256, 256, 2, 4>(p, s);
-    case TILE_PI256W4: return launch_mx<OUT, 256, 256, 2, 2>(p, s);
-    case TILE_R256: case TILE_T8: case TILE_PT8: case TILE_T4: case TILE_PT4:
+    case TILE_T8: case TILE_PT8: case TILE_T4: case TILE_PT4:
       return launch_mx<OUT, 256, 256, 2, 4>(p, s);
-    case TILE_P128: return launch_mx<OUT, 128, 128, 2, 2>(p, s);
     case TILE_256x128_W4: return launch_mx<OUT, 256, 128, 2, 2>(p, s);
-    default: return hipErrorInvalidValue;
+    default: return hipErrorInvalidValue;  // (5, 8, 9, 13-15: retired kernel families)
   }
 }
 

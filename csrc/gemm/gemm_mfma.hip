@@ -38,12 +38,11 @@
 namespace ddlb {
 
 int tile_rows(int tile) {
-  return (tile == TILE_128x128 || tile == TILE_128x256 || tile == TILE_P128 || tile == TILE_I128)
-             ? 128 : 256;
+  return (tile == TILE_128x128 || tile == TILE_128x256 || tile == TILE_I128) ? 128 : 256;
 }
 int tile_cols(int tile) {
   return (tile == TILE_256x128 || tile == TILE_128x128 || tile == TILE_256x128_W4 ||
-          tile == TILE_P128 || tile == TILE_I128) ? 128 : 256;
+          tile == TILE_I128) ? 128 : 256;
 }
 
 bool gemm_fast_path_ok(const GemmArgs& p, int din, int dout) {
@@ -59,22 +58,20 @@ bool gemm_fast_path_ok(const GemmArgs& p, int din, int dout) {
 }
 
 int choose_tile(int64_t M, int64_t N, int64_t K, int din) {
-  // Measured on MI355X (profiles/r01/gemm_*): the LDS-ring kernel wins whenever it gets at least
-  // one 256x256 tile per CU and the K extent is short (<= 2 KiB per row, e.g. K <= 1024 bf16:
-  // the flagship 65536x1024x1024 and the row-parallel 16384x8192x1024 partial); long K prefers
-  // the 128-byte-row interleaved kernel; fewer tiles than CUs want 128x128 blocks.
-  // The 8-phase ping-pong kernel (t8) beats both on whole 256x256 tiles at every K measured
-  // (profiles/r01/s2/lab/t8_vs_ring2.txt) once the grid covers most of the CUs.
+  // Measured on MI355X: among the ping-pong kernels, pt4 (t4 made persistent) leads t4 / t8 / pt8
+  // on every shape and dtype measured once the C stores are non-temporal
+  // (profiles/r01/s2/s2_41_tune_nt.txt: bf16 flagship 108.9 vs t4 121.1 us, 16384x8192x1024
+  // 231.7 vs 251.9, 8192^3 695.7 vs 703.4; s2_44_fp8_tiles.txt: MX-fp8 flagship 63.6 vs pt8
+  // 67.4 us, 8192^3 363 vs t8 380) whenever the grid covers most of the CUs; it falls back to t4
+  // where it does not apply (a single K-tile, an odd K-tile count, activations). Long K with
+  // fewer whole tiles prefers the 128-byte-row interleaved kernel; fewer tiles than CUs want
+  // 128x128 blocks. (The LDS-ring, 256x256 ping-pong and persistent streaming families this
+  // table once chose between were retired in round 4: pt4 had superseded them on every shape.)
   auto tiles = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
-  const int64_t kbytes = K * dtype_size(din);
-  // Among the ping-pong kernels, pt4 (t4 made persistent) leads t4 / t8 / pt8 on every shape and
-  // dtype measured once the C stores are non-temporal (profiles/r01/s2/s2_41_tune_nt.txt: bf16
-  // flagship 108.9 vs t4 121.1 us, 16384x8192x1024 231.7 vs 251.9, 8192^3 695.7 vs 703.4;
-  // s2_44_fp8_tiles.txt: MX-fp8 flagship 63.6 vs pt8 67.4 us, 8192^3 363 vs t8 380). It falls back
-  // to t4 where it does not apply (shard tables, grouped A rows, flags, a single K-tile).
+  (void)K;
+  (void)din;
   const bool whole = M % 256 == 0 && N % 256 == 0 && tiles(256, 256) >= 192;
   if (whole) return TILE_PT4;
-  if (M % 256 == 0 && N % 256 == 0 && tiles(256, 256) >= 256 && kbytes <= 2048) return TILE_R256;
   if (tiles(256, 256) >= 384) return TILE_I256;
   if (tiles(256, 128) >= 384) return TILE_256x128;
   if (tiles(128, 256) >= 384) return TILE_128x256;
@@ -88,24 +85,25 @@ hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mo
   if (raster_env > 0) p.raster_g = raster_env;  // A/B knob of the tile raster (tile_map.h)
   if (p.a_grp <= 0) { p.a_grp = p.M > 0 ? p.M : 1; p.a_gstride = p.a_grp; }
   if (p.c_grp <= 0) { p.c_grp = p.M > 0 ? p.M : 1; p.c_gstride = p.c_grp; }
+  switch (tile) {  // known codes only (the retired families' codes are refused, not rerouted)
+    case TILE_AUTO: case TILE_256x256: case TILE_256x128: case TILE_128x256: case TILE_128x128:
+    case TILE_256x256_W4: case TILE_256x128_W4: case TILE_I256: case TILE_I128: case TILE_I256W4:
+    case TILE_T8: case TILE_PT8: case TILE_T4: case TILE_PT4: break;
+    default: return hipErrorInvalidValue;
+  }
   if (p.M == 0 || p.N == 0) return hipSuccess;
   if (p.a_table != nullptr) {
     // A through a row-block address table (direct access to the peers' shards, or the blocks of
     // a stage-major gather buffer): the ping-pong kernels (pt4 / t4 / t8 / pt8, whole 256-row
-    // blocks; pt4 takes one panel base per tile) and the tiled kernels read A through it; the
-    // persistent streaming family does not. Arrival flags then index LOGICAL rows.
+    // blocks; pt4 takes one panel base per tile) and the tiled kernels read A through it.
+    // Arrival flags then index LOGICAL rows.
     if (p.shard_rows <= 0) return hipErrorInvalidValue;
-    if (tile == TILE_PP256 || tile == TILE_P256 || tile == TILE_PI256 || tile == TILE_PI256W4)
-      tile = TILE_I256;
-    if (tile == TILE_P128) tile = TILE_I128;
     const bool whole = p.M % 256 == 0 && p.N % 256 == 0 && p.shard_rows % 256 == 0;
     if (tile == TILE_AUTO) {
       tile = choose_tile(p.M, p.N, p.K, din);
-      if (tile != TILE_PT4 && tile != TILE_PT8 && tile != TILE_R256 && tile != TILE_T4)
-        tile = TILE_T8;
+      if (tile != TILE_PT4 && tile != TILE_PT8 && tile != TILE_T4) tile = TILE_T8;
     }
-    const bool ping = tile == TILE_R256 || tile == TILE_T8 || tile == TILE_PT8 ||
-                      tile == TILE_T4 || tile == TILE_PT4;
+    const bool ping = tile == TILE_T8 || tile == TILE_PT8 || tile == TILE_T4 || tile == TILE_PT4;
     if (ping && !whole) tile = TILE_128x128;
     // the tiled MX kernel addresses plain rows: block-scaled MFMAs on whole blocks only
     if (mode == GEMM_MODE_MX && !(ping && whole)) mode = GEMM_MODE_AUTO;

@@ -77,15 +77,33 @@ void crash_handler(int sig) {
 
 bool copy_batch_api_available() { return batch_fn() != nullptr; }
 
+namespace {
+// what copy_batch actually did: a batch_memcpy timing is a batched-submission result
+// only if the API call succeeded; otherwise it timed one hipMemcpyAsync per segment
+int g_batch_state = 0;            // 0 not called, 1 batch API used, 2 fell back
+std::string g_batch_error;
+}  // namespace
+
+std::string copy_batch_status() {
+  if (batch_fn() == nullptr) return "unavailable (per-segment hipMemcpyAsync)";
+  if (g_batch_state == 0) return "not called";
+  if (g_batch_state == 1) return "hipMemcpyBatchAsync";
+  return "fallback to per-segment hipMemcpyAsync: " + g_batch_error;
+}
+
 hipError_t copy_batch(void** dst, void** src, size_t* bytes, size_t n, hipStream_t s) {
-  static bool api_ok = true;  // off after the first refusal (the header marks attrs unsupported)
-  if (BatchFn fn = batch_fn(); fn && api_ok) {
+  if (BatchFn fn = batch_fn(); fn && g_batch_state != 2) {
     size_t fail = 0;
     const hipError_t e = fn(dst, src, bytes, n, nullptr, nullptr, 0, &fail, s);
-    if (e == hipSuccess) return e;
+    if (e == hipSuccess) {
+      g_batch_state = 1;
+      return e;
+    }
     (void)hipGetLastError();
-    api_ok = false;
+    g_batch_state = 2;  // off after the first refusal (the header marks attrs unsupported)
+    g_batch_error = hipGetErrorString(e);
   }
+  if (batch_fn() == nullptr) g_batch_state = 2;
   for (size_t i = 0; i < n; ++i) {
     const hipError_t e = hipMemcpyAsync(dst[i], src[i], bytes[i], hipMemcpyDeviceToDevice, s);
     if (e != hipSuccess) return e;
@@ -281,6 +299,21 @@ void PlanExecutor::set_cu_split(int comm_cus) {
   DDLB_HIP(hipEventCreateWithFlags(&compute_fork_, hipEventDisableTiming));
   DDLB_HIP(hipEventCreateWithFlags(&compute_join_, hipEventDisableTiming));
   comm_cus_ = comm_cus;
+}
+
+std::vector<std::vector<int>> PlanExecutor::stream_info() const {
+  std::vector<std::vector<int>> out;
+  auto one = [&](int idx, hipStream_t st) {
+    unsigned flags = 0;
+    int prio = 0;
+    DDLB_HIP(hipStreamGetFlags(st, &flags));
+    DDLB_HIP(hipStreamGetPriority(st, &prio));
+    out.push_back({idx, (int)flags, prio});
+  };
+  for (size_t i = 1; i < streams_.size(); ++i)
+    if (streams_[i]) one((int)i, streams_[i]);
+  if (compute_) one(-1, compute_);
+  return out;
 }
 
 void PlanExecutor::set_trace(bool on, const std::vector<std::string>& labels) {

@@ -53,6 +53,7 @@ enum OpKind : int64_t {
 // hipMemcpyBatchAsync, resolved at run time (dlsym): the HIP runtime torch ships (7.0) predates
 // it, so a batch falls back to one hipMemcpyAsync per segment on the same stream there.
 bool copy_batch_api_available();
+std::string copy_batch_status();  // what copy_batch did so far (see plan.cpp)
 hipError_t copy_batch(void** dst, void** src, size_t* bytes, size_t n, hipStream_t s);
 // Host stack trace on SIGSEGV / SIGABRT / SIGBUS (glibc backtrace to stderr, then the default
 // action): a native frame list for crashes inside the HIP runtime without attaching a debugger.
@@ -70,6 +71,10 @@ class PlanExecutor {
   // and joined back into the caller's stream). 0 = unmasked. Call before the first run().
   void set_cu_split(int comm_cus);
   int cu_split() const { return comm_cus_; }
+  // (index, hipStreamGetFlags, hipStreamGetPriority) of every side stream and, with a CU split,
+  // of the masked compute stream (index -1): what HIP actually gave the streams (a CU-masked
+  // stream is created without flags / priority arguments)
+  std::vector<std::vector<int>> stream_info() const;
   // Stage-level tracing: while on, every op's enqueue is wrapped in a roctx range named by
   // `labels` (e.g. "gemm s3", "copy p2 b1"), so `rocprofv3 --marker-trace --kernel-rename`
   // splits a pipeline run into its stages. roctx is loaded lazily (no link dependency).

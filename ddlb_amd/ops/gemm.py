@@ -18,9 +18,10 @@ from typing import Optional
 from ddlb_amd.ops import load
 
 DT_F32, DT_F16, DT_BF16, DT_FP8, DT_F64, DT_U8 = 0, 1, 2, 3, 4, 5
-TILES = {"auto": 0, "256x256": 1, "256x128": 2, "128x256": 3, "128x128": 4, "pp256": 5, "256x256w4": 6,
-         "256x128w4": 7, "p256": 8, "p128": 9,
-         "i256": 10, "i128": 11, "i256w4": 12, "pi256": 13, "pi256w4": 14, "r256": 15,
+# (codes 5, 8, 9, 13-15 belonged to the pp256 / p256 / p128 / pi256 / pi256w4 / r256 families,
+# retired in round 4: no auto path reached them and pt4 superseded them on every shape measured)
+TILES = {"auto": 0, "256x256": 1, "256x128": 2, "128x256": 3, "128x128": 4, "256x256w4": 6,
+         "256x128w4": 7, "i256": 10, "i128": 11, "i256w4": 12,
          "t8": 16, "pt8": 17, "t4": 18, "pt4": 19}
 MODES = {"auto": 0, "generic": 1, "mx": 2}
 ACTS = {"none": 0, "gelu": 1, "relu": 2, "silu": 3}

@@ -148,8 +148,11 @@ def _finish(plan: Plan, cfg: AlgoConfig) -> None:
     workgroup per CU, so on a masked stream it must not count the communication's CUs."""
     plan.meta.update(comm_cus=cfg.comm_cus, register=cfg.register)
     if cfg.comm_cus > 0:
+        # every persistent launcher (pt4 plain / gated / in-kernel all-gather, pt8) sizes its
+        # grid to num_cus - reserve_cus: on the masked compute stream no workgroup may wait for a
+        # CU the communication holds (ADVICE r3)
         for op in plan.ops:
-            if op.kind == OP_GEMM and op.stream == S_MAIN and op.args.get("flags") is None:
+            if op.kind == OP_GEMM and op.stream == S_MAIN:
                 op.args["reserve_cus"] = max(op.args.get("reserve_cus", 0), cfg.comm_cus)
 
 

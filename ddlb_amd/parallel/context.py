@@ -187,6 +187,7 @@ class BoundPlan:
         self.local: Dict[str, torch.Tensor] = {}
         self.sym: Dict[str, SymmetricBuffer] = {}
         self.rmem: Dict[str, object] = {}
+        self._uncached: List = []
         dev = torch.device("cuda", ctx.device_index)
         externals = dict(externals or {})
         registered = set(rccl_buffers(plan)) if plan.meta.get("register") else set()
@@ -211,6 +212,14 @@ class BoundPlan:
                 # zero-initialised symmetric buffers are the cross-process flag words: peers
                 # write them over xGMI while this GPU polls, so they live in uncached memory
                 self.sym[name] = ctx.symmetric(spec.nbytes, uncached=spec.zero)
+            elif spec.zero:
+                # local flag words (e.g. the ARRIVE flags an RCCL-fed gated GEMM polls, set by
+                # signal kernels on another stream): uncached too, so a tile polling from one
+                # XCD never spins on a stale line of its L2 while the store sits in another's
+                # (r4 budget: erratic 0.18-0.69 ms plan times with cached flags)
+                h = ctx.C.SymmetricBuffer(max(spec.nbytes, 16), ctx.device_index, True)
+                self._uncached.append(h)
+                self.local[name] = torch.from_dlpack(ctx.C.buffer_dlpack(h, ctx.device_index))
             else:
                 self.local[name] = torch.zeros(max(spec.nbytes, 16), dtype=torch.uint8,
                                                device=dev)
@@ -305,7 +314,12 @@ class BoundPlan:
         torch.cuda.synchronize()
         self.ex = None
         self.ctx.release_symmetric(list(self.sym.values()))
-        for name in list(self.rmem):  # deregister + ncclMemFree while the communicator lives
+        for name in list(self.rmem):
+            # deregister while the communicator lives; ncclMemFree happens when the last view
+            # goes (a rowwise OUT returned by run() stays readable after close)
             self.local.pop(name, None)
             self.rmem.pop(name).release()
         self.sym, self.local = {}, {}
+        for h in self._uncached:  # local uncached flag words: no peer maps them
+            h.release()
+        self._uncached = []

@@ -76,9 +76,8 @@ COMMON_ALLOWED = {
     "multicast_protocol": ["memcpy", "batch_memcpy", "kernel"],
     "inter_stream_synchronization": [True, False],
     "signal": ["stream", "kernel"],
-    "tile": ["auto", "pp256", "256x256", "256x128", "128x256", "128x128", "256x256w4",
-             "256x128w4", "p256", "p128", "i256", "i128", "i256w4", "pi256", "pi256w4", "r256",
-             "t8", "pt8", "t4", "pt4"],
+    "tile": ["auto", "256x256", "256x128", "128x256", "128x128", "256x256w4", "256x128w4",
+             "i256", "i128", "i256w4", "t8", "pt8", "t4", "pt4"],
     "gemm_mode": ["auto", "mx", "generic"],
     "copy_blocks": (1, 4096),
     "copy_streams": (1, 4),
@@ -96,10 +95,7 @@ COMMON_ALIASES = {
     "multicast_protocol": {"default": "memcpy", "multimem": "kernel"},
 }
 
-TILE_CODE = {"auto": 0, "256x256": 1, "256x128": 2, "128x256": 3, "128x128": 4, "pp256": 5,
-             "256x256w4": 6, "256x128w4": 7, "p256": 8, "p128": 9, "i256": 10,
-             "i128": 11, "i256w4": 12, "pi256": 13, "pi256w4": 14, "r256": 15, "t8": 16, "pt8": 17,
-             "t4": 18, "pt4": 19}
+from ddlb_amd.ops.gemm import TILES as TILE_CODE  # noqa: E402  (one table: csrc/gemm/gemm.h)
 MODE_CODE = {"auto": 0, "generic": 1, "mx": 2}
 
 

@@ -52,7 +52,7 @@ def main():
     p.add_argument("--dtype", default="bfloat16")
     p.add_argument("--rounds", type=int, default=5)
     p.add_argument("--iters", type=int, default=20)
-    p.add_argument("--tiles", default="auto,pp256,256x256,128x128")
+    p.add_argument("--tiles", default="auto,pt4,t4,256x256,128x128")
     p.add_argument("--modes", default="auto")
     p.add_argument("--shapes", default="all")
     p.add_argument("--json", default=None)

@@ -36,9 +36,9 @@ def main():
     variants = {
         "impl.run": lambda: impl.run(),
         "gemm(impl bufs) auto": lambda: gemm(A, W, C),
-        "gemm(impl bufs) pi256": lambda: gemm(A, W, C, tile="pi256"),
+        "gemm(impl bufs) pt4": lambda: gemm(A, W, C, tile="pt4"),
         "gemm(fresh bufs) auto": lambda: gemm(A2, W2, C2),
-        "gemm(fresh bufs) pi256": lambda: gemm(A2, W2, C2, tile="pi256"),
+        "gemm(fresh bufs) pt4": lambda: gemm(A2, W2, C2, tile="pt4"),
         "torch.matmul": lambda: torch.matmul(A2, W2.t(), out=C2),
     }
     res = {kname: ([], []) for kname in variants}

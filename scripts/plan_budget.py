@@ -72,7 +72,7 @@ def _time(bound, iters: int, warm: int = 5):
     return gpu_ms, sorted(host)[len(host) // 2]
 
 
-def measure(ctx, plan, io, cfg_graph, iters: int, rccl_blocks: int):
+def measure(ctx, plan, io, cfg_graph, iters: int, rccl_blocks: int, timeline: bool = False):
     import torch
 
     from ddlb_amd.parallel.budget import PRESET, emulate, flag_buffers, gemm_only
@@ -90,6 +90,15 @@ def measure(ctx, plan, io, cfg_graph, iters: int, rccl_blocks: int):
                 v.copy_((torch.rand(v.shape, device=v.device) * 2 - 1).to(v.dtype))
             torch.cuda.synchronize()
             res[f"{kind}_ms"], res[f"{kind}_host_us"] = _time(bound, iters)
+            if kind == "plan" and timeline:
+                from ddlb_amd.parallel.explain import format_timeline
+
+                bound.set_timeline(True)
+                for _ in range(3):
+                    bound.run()
+                torch.cuda.synchronize()
+                res["timeline"] = format_timeline(bound.timeline())
+                bound.set_timeline(False)
             if kind == "plan" and cfg_graph in (True, "auto"):
                 try:
                     if maybe_enable_graph(bound, cfg_graph):
@@ -114,6 +123,9 @@ def main(argv=None) -> int:
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rccl-blocks", type=int, default=32)
     ap.add_argument("--out", default="")
+    ap.add_argument("--timeline", default="",
+                    help="comma list of candidates whose last eager run is printed as a per-op "
+                         "timeline (ddlb_amd.parallel.explain.format_timeline)")
     a = ap.parse_args(argv)
 
     import torch
@@ -146,7 +158,9 @@ def main(argv=None) -> int:
                        counts=op_counts(plan))
             from ddlb_amd.parallel.budget import emulate
             row["copy_mb"] = round(copy_bytes(emulate(plan, a.rccl_blocks)) / 2 ** 20, 1)
-            row.update(measure(ctx, plan, io, opts.get("graph", "auto"), a.iters, a.rccl_blocks))
+            tl = [c.strip() for c in a.timeline.split(",") if c.strip()]
+            row.update(measure(ctx, plan, io, opts.get("graph", "auto"), a.iters, a.rccl_blocks,
+                               timeline=label in tl))
         except Exception as e:  # recorded, the sweep goes on
             row["error"] = f"{type(e).__name__}: {str(e)[:200]}"
         rows.append(row)
@@ -159,6 +173,8 @@ def main(argv=None) -> int:
               f"{row.get('plan_host_us', 0.0):8.1f} {row.get('ops', 0):5d} "
               f"{row.get('signal_ops', 0):4d} {row.get('copy_mb', 0.0):7.1f}"
               + (f"  {row['error']}" if "error" in row else ""), flush=True)
+        if "timeline" in row:
+            print(row["timeline"], flush=True)
         torch.cuda.synchronize()
     if a.out:
         os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)

@@ -15,7 +15,7 @@ def main():
     p.add_argument("-m", type=int, default=65536)
     p.add_argument("-n", type=int, default=1024)
     p.add_argument("-k", type=int, default=1024)
-    p.add_argument("--tiles", default="256x256,pp256,128x128")
+    p.add_argument("--tiles", default="256x256,pt4,128x128")
     p.add_argument("--hipblaslt", action="store_true",
                    help="also the vendor GEMM (F.linear: hipBLASLt, K-contiguous weight)")
     p.add_argument("--iters", type=int, default=20)

@@ -35,9 +35,8 @@ def gen():
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
-@pytest.mark.parametrize("tile", ["256x256", "256x128", "128x256", "128x128", "pp256", "256x256w4",
-                                  "256x128w4", "p256", "p128", "i256", "i128", "i256w4", "pi256",
-                                  "pi256w4", "r256", "t8"])
+@pytest.mark.parametrize("tile", ["256x256", "256x128", "128x256", "128x128", "256x256w4",
+                                  "256x128w4", "i256", "i128", "i256w4", "t8", "pt8", "t4", "pt4"])
 def test_gemm_tiles(dtype, tile, gen):
     from ddlb_amd.ops.gemm import gemm
 
@@ -98,8 +97,8 @@ def test_gemm_fp8(mode, odt, gen):
     torch.testing.assert_close(out.float(), _ref(a, w), rtol=0, atol=_tol(torch.float8_e4m3fn, K))
 
 
-@pytest.mark.parametrize("tile", ["auto", "pp256", "128x128", "256x256w4", "256x128w4", "p256", "p128",
-                                  "i256", "i128", "i256w4", "pi256", "r256", "t8", "pt8", "t4", "pt4"])
+@pytest.mark.parametrize("tile", ["auto", "128x128", "256x256w4", "256x128w4", "i256", "i128",
+                                  "i256w4", "t8", "pt8", "t4", "pt4"])
 def test_fp8_integer_exact(gen, tile):
     """Small integers are exact in e4m3: both fp8 paths must match bit for bit."""
     from ddlb_amd.ops.gemm import gemm
@@ -136,8 +135,8 @@ def test_grouped_rows(gen):
     assert torch.count_nonzero(C[untouched].float()) == 0
 
 
-@pytest.mark.parametrize("tile", ["auto", "pp256", "128x128", "256x256w4", "256x128w4", "p256", "p128",
-                                  "i256", "i128", "i256w4", "pi256", "r256", "t8"])
+@pytest.mark.parametrize("tile", ["auto", "128x128", "256x256w4", "256x128w4", "i256", "i128",
+                                  "i256w4", "t8", "pt8", "t4", "pt4"])
 @pytest.mark.parametrize("shape", [(2048, 1024, 1024), (4096, 2048, 2048), (768, 512, 192)])
 def test_repeat_race_screen(gen, tile, shape):
     """Same inputs, 20 launches: identical bits every time (LDS-DMA/barrier race screen)."""
@@ -165,7 +164,7 @@ def test_host_checks_reject_bad_shapes(gen):
         gemm(a, _rand((64, 128), torch.bfloat16, gen), M=128)
 
 
-@pytest.mark.parametrize("tile", ["p256", "p128", "pi256", "r256", "pt8", "pt4"])
+@pytest.mark.parametrize("tile", ["pt8", "pt4"])
 def test_persistent_many_tiles_grouped(gen, tile):
     """Persistent streaming kernel: more tiles than blocks, grouped C rows, repeat-identical."""
     from ddlb_amd.ops.gemm import gemm
@@ -188,7 +187,7 @@ def test_persistent_many_tiles_grouped(gen, tile):
 
 
 @pytest.mark.parametrize("act", ["gelu", "relu", "silu"])
-@pytest.mark.parametrize("tile", ["auto", "128x128", "pi256", "r256", "t8", "pt8", "t4", "pt4"])
+@pytest.mark.parametrize("tile", ["auto", "128x128", "i256", "t8", "pt8", "t4", "pt4"])
 def test_fused_activation_epilogue(gen, act, tile):
     from ddlb_amd.ops.gemm import gemm
     from ddlb_amd.parallel.sim import apply_act
@@ -201,51 +200,44 @@ def test_fused_activation_epilogue(gen, act, tile):
     torch.testing.assert_close(out.float(), apply_act(_ref(a, w), code), rtol=0.02, atol=0.05)
 
 
-_RING_DT = [(torch.bfloat16, torch.bfloat16), (torch.bfloat16, torch.float32),
+_ALL_DT = [(torch.bfloat16, torch.bfloat16), (torch.bfloat16, torch.float32),
             (torch.float16, torch.float16), (torch.float16, torch.float32),
             (torch.float32, torch.float32), (torch.float8_e4m3fn, torch.bfloat16),
             (torch.float8_e4m3fn, torch.float32)]
 
 
-@pytest.mark.parametrize("dt", _RING_DT, ids=lambda d: f"{str(d[0])[6:]}-{str(d[1])[6:]}")
+def test_retired_tiles_refused(gen):
+    """The retired kernel families' codes (pp256 5, p256 8, p128 9, pi256 13, pi256w4 14, r256 15)
+    are refused by the launcher: never silently rerouted to another kernel."""
+    from ddlb_amd.ops import load
+
+    a, w = _rand((512, 256), torch.bfloat16, gen), _rand((256, 256), torch.bfloat16, gen)
+    out = torch.empty((512, 256), dtype=torch.bfloat16, device=DEV)
+    for code in (5, 8, 9, 13, 14, 15, 20):
+        with pytest.raises(RuntimeError):
+            load().gemm(a.data_ptr(), w.data_ptr(), out.data_ptr(), 256, 256, 256, 512, 256, 256,
+                        2, 2, code, 0, 0, 0, 0, 0, torch.cuda.current_stream().cuda_stream, 0)
+
+
 @pytest.mark.parametrize("shape", [(256, 256, 128), (8192, 1024, 512), (32768, 1024, 256),
                                    (4096, 768, 1024)])
-def test_ring_kernel(dt, shape, gen):
-    """LDS-ring kernel: one tile, fewer tiles than CUs, several tiles per block (C stores of one
-    tile draining under the next), N not a power of two; every input/output dtype."""
+@pytest.mark.parametrize("dt", _ALL_DT, ids=lambda d: f"{str(d[0])[6:]}-{str(d[1])[6:]}")
+def test_auto_every_dtype(dt, shape, gen):
+    """auto tile (pt4 on whole grids, tiled kernels otherwise) for every input / output dtype:
+    one tile, fewer tiles than CUs, several tiles per persistent block, N not a power of two;
+    repeat-identical."""
     from ddlb_amd.ops.gemm import gemm
 
     din, dout = dt
     M, N, K = shape
     a, w = _rand((M, K), din, gen), _rand((N, K), din, gen)
-    out = gemm(a, w, tile="r256", out_dtype=dout)
+    out = gemm(a, w, out_dtype=dout)
     torch.cuda.synchronize()
     assert out.dtype == dout
     torch.testing.assert_close(out.float(), _ref(a, w), rtol=0, atol=_tol(din, K))
-    again = gemm(a, w, tile="r256", out_dtype=dout)
+    again = gemm(a, w, out_dtype=dout)
     torch.cuda.synchronize()
     assert torch.equal(out, again)
-
-
-def test_ring_grouped_rows(gen):
-    """Ring kernel with the pipelines' strided A and C row blocks."""
-    from ddlb_amd.ops.gemm import gemm
-
-    d, blk, K, N = 4, 512, 256, 1024
-    A = _rand((d * 2048, K), torch.bfloat16, gen)
-    w = _rand((N, K), torch.bfloat16, gen)
-    C = torch.zeros((d * 2048, N), dtype=torch.bfloat16, device=DEV)
-    j = 1
-    gemm(A[j * blk:], w, C[j * blk:], M=d * blk, a_grp=blk, a_gstride=2048, c_grp=blk,
-         c_gstride=2048, tile="r256")
-    torch.cuda.synchronize()
-    ref = _ref(A, w)
-    mask = torch.zeros(d * 2048, dtype=torch.bool, device=DEV)
-    for r in range(d):
-        rows = slice(r * 2048 + j * blk, r * 2048 + (j + 1) * blk)
-        mask[rows] = True
-        torch.testing.assert_close(C[rows].float(), ref[rows], rtol=0, atol=_tol(torch.bfloat16, K))
-    assert torch.count_nonzero(C[~mask].float()) == 0
 
 
 def test_no_vendor_mode(gen):
@@ -261,7 +253,7 @@ def test_no_vendor_mode(gen):
 
 
 @pytest.mark.parametrize("tile", ["t8", "pt8", "t4", "pt4"])
-@pytest.mark.parametrize("dt", _RING_DT, ids=lambda d: f"{str(d[0])[6:]}-{str(d[1])[6:]}")
+@pytest.mark.parametrize("dt", _ALL_DT, ids=lambda d: f"{str(d[0])[6:]}-{str(d[1])[6:]}")
 @pytest.mark.parametrize("shape", [(256, 256, 64), (256, 256, 128), (8192, 1024, 512),
                                    (4096, 768, 1024), (2048, 2048, 3072), (65536, 1024, 128),
                                    (3328, 1536, 256)])  # grouped raster: 13 m-blocks, 6 n
@@ -341,8 +333,8 @@ def _tight_bound(ref, k):
     return 2.0 ** -7 * float(ref.abs().max()) + k * 2.0 ** -12
 
 
-@pytest.mark.parametrize("tile", ["auto", "pt4", "t4", "t8", "pt8", "r256", "i256", "pi256",
-                                  "256x256", "128x128"])
+@pytest.mark.parametrize("tile", ["auto", "pt4", "t4", "t8", "pt8", "i256", "256x256",
+                                  "128x128"])
 @pytest.mark.parametrize("dt", [(torch.bfloat16, "auto"), (torch.float16, "auto"),
                                 (torch.float8_e4m3fn, "mx"), (torch.float8_e4m3fn, "auto")],
                          ids=lambda d: f"{str(d[0])[6:]}-{d[1]}")

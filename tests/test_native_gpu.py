@@ -385,6 +385,11 @@ def test_rccl_data_plane_world1(comm, mode):
         assert all(m.registered for m in bound.rmem.values())
     if "cumask" in mode:
         assert bound.ex.cu_split() == 32 and not bound.ex.graph_capturable()
+        # what HIP gives a CU-masked stream (no flags / priority arguments): recorded, and the
+        # enqueue logic (fork / join by events) stays correct for blocking or non-blocking ones
+        info = {i: (fl, pr) for i, fl, pr in bound.ex.stream_info()}
+        assert set(info) == {1, -1}, info
+        print("cu-masked stream flags / priority:", info)
     if graph:  # RCCL plans are not captured (replaying captured RCCL calls crashed here)
         assert not bound.ex.graph_capturable()
         with pytest.raises(RuntimeError):
@@ -403,6 +408,61 @@ def test_rccl_data_plane_world1(comm, mode):
     out = bound.buffer("c").view(torch.float32).view(256, 128)
     torch.testing.assert_close(out, A.float() @ W.float().T, rtol=0, atol=1e-3 * 128)
     assert ctx.rccl().async_error() == ""
+    kept = bound.buffer("ag").view(torch.float32)  # an output view a caller may still hold
+    bound.close()
+    ctx.close()
+    # registered buffers are deregistered at close; the memory lives while a view does
+    assert torch.equal(kept, x)
+
+
+@pytest.mark.parametrize("kind", ["pt8-mx", "pt4-gated"])
+def test_cu_split_persistent_launchers_world1(comm, kind):
+    """with a CU split every persistent launcher sizes its grid to the masked compute
+    stream (num_cus - reserve_cus): the MX-fp8 pt8 kernel and a flag-gated pt4 fed by the
+    (masked) comm stream, both validated against fp32; no workgroup waits for a comm CU."""
+    from ddlb_amd.parallel.context import NativeContext
+    from ddlb_amd.parallel.plan import DT_BF16, DT_FP8, Plan, SIG_KERNEL
+
+    M, N, K = 32768, 1024, 1024
+    din = DT_FP8 if kind == "pt8-mx" else DT_BF16
+    tdt = torch.float8_e4m3fn if kind == "pt8-mx" else torch.bfloat16
+    es = 1 if kind == "pt8-mx" else 2
+    plan = Plan(0, 1, nstreams=2, stream_priority=[0, 1])
+    a = plan.buffer("a", M * K * es)
+    src = plan.buffer("src", M * K * es)
+    bt = plan.buffer("bt", N * K * es)
+    c = plan.buffer("c", M * N * 2)
+    fl = plan.buffer("flags", 256, zero=True)
+    if kind == "pt8-mx":
+        plan.gemm(0, a, bt, c, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, din=din, dout=DT_BF16,
+                  tile=17, mode=2, reserve_cus=32)
+    else:
+        rows = M // 4
+        for j in range(4):
+            plan.copy(1, a + j * rows * K * es, src + j * rows * K * es, rows * K * es,
+                      method=1, max_blocks=32)
+            plan.signal(1, [fl + 4 * j], method=SIG_KERNEL)
+        plan.gemm(0, a, bt, c, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, din=din, dout=DT_BF16,
+                  tile=19, flags=fl, flag_rows=rows, nshards=4, tile_order=1, reserve_cus=32)
+    plan.meta.update(comm_cus=32)
+    ctx = NativeContext(comm)
+    bound = ctx.bind(plan)
+    assert bound.ex.cu_split() == 32
+    A = (torch.rand(M, K, device="cuda") * 2 - 1).to(tdt)
+    W = (torch.rand(N, K, device="cuda") * 2 - 1).to(tdt)
+    bound.buffer("a" if kind == "pt8-mx" else "src").view(tdt).view(M, K).copy_(A)
+    bound.buffer("bt").view(tdt).view(N, K).copy_(W)
+    ref = A.float() @ W.float().T
+    out = bound.buffer("c").view(torch.bfloat16).view(M, N)
+    for _ in range(3):
+        if kind != "pt8-mx":
+            bound.buffer("a").view(torch.uint8).fill_(0xFF)
+        out.zero_()
+        bound.run()
+        torch.cuda.synchronize()
+        bound.check_health()
+        err = float((out.float() - ref).abs().max())
+        assert err <= _tight(ref, K), err
     bound.close()
     ctx.close()
 

@@ -353,3 +353,20 @@ def test_in_kernel_allgather_shape_rules():
                      copy_blocks=8, act=1)
     with pytest.raises(ValueError, match="activation"):
         build_tp_columnwise(0, 2, 512, 256, 64, DT_F32, DT_F32, act)
+
+
+@pytest.mark.parametrize("alg,fused,proto", [("coll_pipeline", False, "memcpy"),
+                                             ("coll_pipeline", True, "memcpy"),
+                                             ("coll_pipeline", True, "kernel"),
+                                             ("p2p_pipeline", True, "memcpy")])
+@pytest.mark.parametrize("backend", ["rccl", "ipc"])
+def test_cu_split_reserves_every_gemm(alg, fused, proto, backend):
+    """with comm_cus > 0 EVERY compute-stream GEMM (gated, in-kernel all-gather and
+    plain) leaves at least comm_cus CUs: its persistent grid fits the masked compute stream."""
+    if backend == "rccl" and proto == "kernel":
+        pytest.skip("kernel copies are an ipc protocol")
+    cfg = AlgoConfig(algorithm=alg, backend=backend, fused=fused, protocol=proto, s=2,
+                     comm_cus=48, copy_blocks=8)
+    plan, _ = build_tp_columnwise(0, 2, 1024, 256, 64, DT_F32, DT_F32, cfg)
+    g = [op for op in plan.ops if op.kind == OP_GEMM and op.stream == 0]
+    assert g and all(op.args["reserve_cus"] >= 48 for op in g)
