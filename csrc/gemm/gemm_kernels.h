@@ -1852,6 +1852,14 @@ hipError_t launch_pt4(const GemmArgs& p, hipStream_t s) {
   if (q.ag_ctas > 0 && (p.ag_mode & AG_FILL_ROUNDS)) q.ag_ctas = ag_fill_ctas(grid, q.ag_ctas, tiles);
   grid -= q.ag_ctas;
   grid = (grid / 8) * 8;  // blockIdx % 8 == XCD group for every virtual tile id
+  if (p.flags != nullptr && q.ag_ctas == 0 && grid >= 8) {
+    // a gated GEMM fed by other kernels (RCCL, copy kernels, signal kernels): shrink the grid to
+    // the fewest workgroups that keep its number of tile rounds, so every CU it does not need is
+    // free for the producers (flagship with 32 reserved: 1024 tiles in 5 rounds on 208, not 224)
+    const int rounds = (tiles + grid - 1) / grid;
+    const int need = ((tiles + rounds - 1) / rounds + 7) / 8 * 8;
+    if (need < grid) grid = need;
+  }
   if (grid > tiles) grid = tiles;
   if (grid < 1) grid = 1;
   // write-through stores address C from a per-tile scalar row (the tile's rows contiguous)
