@@ -8,6 +8,9 @@
 
 #include <chrono>
 #include <functional>
+#include <map>
+#include <mutex>
+#include <tuple>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
@@ -119,6 +122,35 @@ void install_crash_handler() {
   for (int sig : {SIGSEGV, SIGBUS, SIGABRT, SIGFPE}) sigaction(sig, &sa, nullptr);
 }
 
+namespace {
+// Process-wide stream pool: slot s of priority class p on a device is created once (non-blocking)
+// and reused by every executor (see PlanExecutor::home_). Slots are created in index order the
+// first time an executor asks for them, so the home stream (slot 0) and the side streams of the
+// first plan of a process land on consecutive hardware queues, and later plans get the same.
+// cu_mask (optional, `words` 32-bit words): a CU-masked stream (hipExtStreamCreateWithCUMask);
+// the mask is part of the key (a CU split's streams are pooled the same way).
+hipStream_t pool_stream(int device, int slot, int prio_class, const uint32_t* cu_mask = nullptr,
+                        int words = 0) {
+  static std::mutex mu;
+  static std::map<std::tuple<int, int, int, std::vector<uint32_t>>, hipStream_t> pool;
+  std::lock_guard<std::mutex> lock(mu);
+  std::vector<uint32_t> mask(cu_mask, cu_mask + (cu_mask ? words : 0));
+  auto key = std::make_tuple(device, slot, prio_class, mask);
+  auto it = pool.find(key);
+  if (it != pool.end()) return it->second;
+  hipStream_t st = nullptr;
+  if (cu_mask != nullptr) {
+    DDLB_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)words, cu_mask));
+  } else {
+    int lo = 0, hi = 0;
+    DDLB_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    DDLB_HIP(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, prio_class > 0 ? hi : lo));
+  }
+  pool[key] = st;
+  return st;
+}
+}  // namespace
+
 PlanExecutor::PlanExecutor(int device, int nstreams, int nevents,
                            const std::vector<int>& priorities)
     : device_(device) {
@@ -127,13 +159,12 @@ PlanExecutor::PlanExecutor(int device, int nstreams, int nevents,
   streams_.assign((size_t)nstreams, nullptr);
   fork_join_.assign((size_t)nstreams * 2, nullptr);
   used_.assign((size_t)nstreams, false);
-  int lo = 0, hi = 0;
-  DDLB_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  home_ = pool_stream(device, 0, 0);
+  DDLB_HIP(hipEventCreateWithFlags(&compute_join_, hipEventDisableTiming));
   for (int i = 1; i < nstreams; ++i) {
-    int prio = (size_t)i < priorities.size() ? priorities[(size_t)i] : 0;
     // priority: 0 = normal, 1 = high (comm streams)
-    const int p = prio > 0 ? hi : lo;
-    DDLB_HIP(hipStreamCreateWithPriority(&streams_[(size_t)i], hipStreamNonBlocking, p));
+    const int prio = (size_t)i < priorities.size() ? priorities[(size_t)i] : 0;
+    streams_[(size_t)i] = pool_stream(device, i, prio > 0 ? 1 : 0);
   }
   for (auto& e : fork_join_) DDLB_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   sync_ev_.assign((size_t)nstreams, nullptr);
@@ -153,17 +184,12 @@ PlanExecutor::~PlanExecutor() {
   if (graph_exec_) hipGraphExecDestroy(graph_exec_);
   if (graph_) hipGraphDestroy(graph_);
   if (cap_stream_) hipStreamDestroy(cap_stream_);
-  if (compute_) {
-    hipStreamSynchronize(compute_);
-    hipStreamDestroy(compute_);
-  }
+  if (compute_) hipStreamSynchronize(compute_);  // a pool stream
   if (compute_fork_) hipEventDestroy(compute_fork_);
   if (compute_join_) hipEventDestroy(compute_join_);
+  if (home_) hipStreamSynchronize(home_);
   for (size_t i = 1; i < streams_.size(); ++i)
-    if (streams_[i]) {
-      hipStreamSynchronize(streams_[i]);
-      hipStreamDestroy(streams_[i]);
-    }
+    if (streams_[i]) hipStreamSynchronize(streams_[i]);  // pool streams live on
   for (auto e : fork_join_) if (e) hipEventDestroy(e);
   for (auto e : sync_ev_) if (e) hipEventDestroy(e);
   for (auto e : events_) if (e) hipEventDestroy(e);
@@ -290,14 +316,11 @@ void PlanExecutor::set_cu_split(int comm_cus) {
   const int words = (ncu + 31) / 32;
   std::vector<uint32_t> comm((size_t)words, 0u), comp((size_t)words, 0u);
   for (int i = 0; i < ncu; ++i) (i < comm_cus ? comm : comp)[(size_t)(i / 32)] |= 1u << (i % 32);
-  for (size_t i = 1; i < streams_.size(); ++i) {
-    if (streams_[i]) DDLB_HIP(hipStreamDestroy(streams_[i]));
-    streams_[i] = nullptr;
-    DDLB_HIP(hipExtStreamCreateWithCUMask(&streams_[i], (uint32_t)words, comm.data()));
-  }
-  DDLB_HIP(hipExtStreamCreateWithCUMask(&compute_, (uint32_t)words, comp.data()));
+  // masked streams come from the pool too (keyed by their mask): see home_ in plan.h
+  compute_ = pool_stream(device_, 0, 0, comp.data(), words);
+  for (size_t i = 1; i < streams_.size(); ++i)
+    streams_[i] = pool_stream(device_, (int)i, 0, comm.data(), words);
   DDLB_HIP(hipEventCreateWithFlags(&compute_fork_, hipEventDisableTiming));
-  DDLB_HIP(hipEventCreateWithFlags(&compute_join_, hipEventDisableTiming));
   comm_cus_ = comm_cus;
 }
 
@@ -404,12 +427,12 @@ void PlanExecutor::enqueue(hipStream_t main) {
     DDLB_HIP(bump_signal_launch(b, main));
   }
   if (any_side_ || compute_) {
-    // fork: every used side stream (and the CU-split compute stream) waits for everything
-    // already queued on `main`
+    // fork: every used side stream and the stream-0 stream (home, or the CU-split compute
+    // stream) wait for everything already queued on `main`
     DDLB_HIP(hipEventRecord(fork_join_[0], main));
     for (size_t i = 1; i < streams_.size(); ++i)
       if (used_[i]) DDLB_HIP(hipStreamWaitEvent(streams_[i], fork_join_[0], 0));
-    if (compute_) DDLB_HIP(hipStreamWaitEvent(compute_, fork_join_[0], 0));
+    if (S(0, main) != main) DDLB_HIP(hipStreamWaitEvent(S(0, main), fork_join_[0], 0));
   }
   if (timeline_on_) host_us_.assign(ops_.size() / kOpWords, 0.f);
   for (size_t i = first; i < ops_.size(); i += kOpWords) {
@@ -449,8 +472,8 @@ void PlanExecutor::enqueue(hipStream_t main) {
       }
   }
   if (graph_on_) GDBG("  enqueue done");
-  if (compute_) {
-    DDLB_HIP(hipEventRecord(compute_join_, compute_));
+  if (S(0, main) != main) {
+    DDLB_HIP(hipEventRecord(compute_join_, S(0, main)));
     DDLB_HIP(hipStreamWaitEvent(main, compute_join_, 0));
   }
 }

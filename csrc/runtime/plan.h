@@ -111,9 +111,19 @@ class PlanExecutor {
   hipGraph_t graph_ = nullptr;
   hipGraphExec_t graph_exec_ = nullptr;
   hipStream_t S(int64_t idx, hipStream_t main) const {
-    return idx == 0 ? (compute_ ? compute_ : main) : streams_.at((size_t)idx);
+    // (graph capture keeps stream 0 on the capture's origin stream: a cycle of dependencies
+    // among NON-origin streams crashes this runtime's hipStreamEndCapture, see side_stream_cycle)
+    return idx == 0 ? (compute_ ? compute_ : (any_side_ && !graph_on_ ? home_ : main))
+                    : streams_.at((size_t)idx);
   }
   int comm_cus_ = 0;
+  // Stream-0 ops of a multi-stream plan run on `home_`, forked from and joined back into the
+  // caller's stream; home_ and the side streams come from a process-wide pool (created once, in
+  // a fixed order, never destroyed): the HIP stream -> hardware-queue mapping is fixed at
+  // creation, and the one-GPU budget measured the SAME plan at 0.18 ms in one bind and 0.6-0.7
+  // ms in the next when every bind created fresh streams beside the caller's null stream
+  // (profiles/r04/r4_5_*). A single-stream plan stays on the caller's stream (no fork).
+  hipStream_t home_ = nullptr;
   hipStream_t compute_ = nullptr;        // stream-0 ops under a CU split
   hipEvent_t compute_fork_ = nullptr, compute_join_ = nullptr;
   bool trace_on_ = false;
