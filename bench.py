@@ -554,9 +554,10 @@ def autotune(job, pool, a, world: int, tune: dict, pre: dict = None):
             best_ms[label] = min(r["ms"], best_ms.get(label, float("inf")))
             tune[label] = round(best_ms[label], 4)
         else:
-            if r["error"].startswith("timeout"):
-                for ch in req:
-                    timeouts[ch] = timeouts.get(ch, 0) + 1
+            if r["error"].startswith("timeout") and req:
+                # charged to the candidate's most specific mechanism (e.g. rccl_fused, ipc_agk):
+                # two hangs of the RCCL-fed fused GEMM must not drop the plain RCCL pipelines
+                timeouts[req[-1]] = timeouts.get(req[-1], 0) + 1
             if label not in best_ms:
                 tune[label] = r["error"][:160]
         job.log(f"tune {label}: {round(r['ms'], 4) if r['ok'] else r['error'][:160]} "

@@ -1011,6 +1011,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   // (profiles/r03/r3_27, r3_33), and their arrival gate sits at that schedule's A staging.
   constexpr bool DEFER = !GATED && CMODE == 2;
   constexpr int NH = DEFER ? 2 : 1;  // fragment register sets
+  const bool slack = (p.knob & 1) == 0;  // A/B: C stores left in flight into the next tile
   __shared__ __attribute__((aligned(1024))) char smem[8 * UNIT];
   // CMODE 2: C through one wave-uniform descriptor (launch_pt4 checks the extent fits)
   const __amdgpu_buffer_rsrc_t crc =
@@ -1258,21 +1259,34 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
       stage(0, 1, BUF ^ 1, qa);
       stage(1, 1, BUF ^ 1, qa);
       T4_LGKM0();
-      if (g1) wait_vm<KIND == 2 ? 8 + 3 * NS : 8>();
+      // KIND 2 (first K-tile after a tile's last): phase B reads K-tile 0 halves 1, staged in
+      // the last K-tile's phase A before ALL four quadrants' stores -> 8 + 4 NS may stay out
+      if (g1) {
+        if (slack) wait_vm<KIND == 2 ? 8 + 4 * NS : 8>();
+        else wait_vm<KIND == 2 ? 8 + 3 * NS : 8>();
+      }
       T4_BAR();
       __builtin_amdgcn_s_setprio(1);
       if constexpr (DEF) mm(1, 1, false);
       mm(0, 0, Z);
       __builtin_amdgcn_s_setprio(0);
       if constexpr (KIND == 1) store_q(0, 0);
-      if (!g1) wait_vm<KIND == 2 ? 8 + 3 * NS : (KIND == 1 ? 8 + NS : 8)>();
+      if (!g1) {
+        if (slack) wait_vm<KIND == 2 ? 8 + 4 * NS : (KIND == 1 ? 8 + NS : 8)>();
+        else wait_vm<KIND == 2 ? 8 + 3 * NS : (KIND == 1 ? 8 + NS : 8)>();
+      }
       T4_BAR();
       loadB(bufc, 1);  // phase B: halves 1
       loadA(bufc, 1);
       stage(0, 0, BUF, qb);
       stage(1, 0, BUF, qb);
       T4_LGKM0();
-      if (g1) wait_vm<KIND == 1 ? 8 + NS : 8>();
+      // KIND 2: the next phase (K-tile 1, phase A) reads K-tile 1 halves 0, staged in the last
+      // K-tile's phase B before its three quadrants' stores -> 8 + 3 NS may stay out
+      if (g1) {
+        if (slack) wait_vm<KIND == 1 ? 8 + NS : (KIND == 2 ? 8 + 3 * NS : 8)>();
+        else wait_vm<KIND == 1 ? 8 + NS : 8>();
+      }
       T4_BAR();
       __builtin_amdgcn_s_setprio(1);
       mm(0, 1, Z);
@@ -1289,7 +1303,10 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
           acc[4 + f][3] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
-      if (!g1) wait_vm<KIND == 1 ? 8 + 4 * NS : 8>();
+      if (!g1) {
+        if (slack) wait_vm<KIND == 1 ? 8 + 4 * NS : (KIND == 2 ? 8 + 3 * NS : 8)>();
+        else wait_vm<KIND == 1 ? 8 + 4 * NS : 8>();
+      }
       T4_BAR();
     } else {
       if (GATED && qa.kt == 0) {

@@ -326,3 +326,20 @@ def test_autotune_drops_candidates_of_failed_primitive_phases():
     pre = {"ipc": "ok", "ipc_ksig": "ok", "ipc_sdma": "ok", "ipc_dstore": "failed: timeout"}
     chosen, _ = bench.autotune(job, row_pool, _args(primitive="tp_rowwise"), 8, tune, pre)
     assert chosen[0] == "m" and tune["d"].startswith("skipped (ipc_dstore")
+
+
+def test_fused_rccl_hangs_do_not_drop_plain_rccl():
+    """Timeouts are charged to a candidate's most specific mechanism: two hangs of the RCCL-fed
+    fused GEMM skip the other fused candidates, never the plain RCCL pipelines."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    fused = {"backend": "rccl", "algorithm": "coll_pipeline", "fused": True}
+    pool = [("f1", "native", dict(fused, s=8)), ("f2", "native", dict(fused, s=4)),
+            ("f3", "native", dict(fused, s=2)), ("r", "native", {"backend": "rccl", "s": 4})]
+    to = {"ok": False, "error": "timeout after 45s"}
+    job = _FakeJob(pool, {"f1": [to], "f2": [to], "r": [_ok(1.0)]})
+    tune = {}
+    chosen, _ = bench.autotune(job, pool, _args(), 8, tune, {})
+    assert chosen[0] == "r"
+    assert "rccl_fused candidates timed out twice" in tune["f3"]
