@@ -107,8 +107,6 @@ PYBIND11_MODULE(_C, m) {
           return gemm_fast_path_ok(g, din, dout);
         });
   m.def("choose_tile", &choose_tile);
-  m.def("set_gemm_knob", &set_gemm_knob);
-  m.def("gemm_knob", &gemm_knob);
   m.def("tile_rows", &tile_rows);
   m.def("tile_cols", &tile_cols);
 

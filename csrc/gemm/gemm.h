@@ -66,7 +66,6 @@ struct GemmArgs {
   int ag_mode = 0;                  // AgMode bits below
   const uint64_t* ag_tab = nullptr;
   int act = 0;                      // fused epilogue activation: ACT_* below
-  int knob = 0;                     // kernel A/B switches (DDLB_GEMM_KNOB; 0 = product)
   // Direct-access A (optional): row block s of shard_rows rows starts at a_table[s] (device
   // array of addresses, e.g. the peers' IPC-mapped shards read straight over xGMI).
   const uint64_t* a_table = nullptr;
@@ -93,8 +92,6 @@ enum AgMode : int {
 hipError_t gemm_launch(const GemmArgs& p, int din, int dout, int tile, int mode, hipStream_t s);
 bool gemm_fast_path_ok(const GemmArgs& p, int din, int dout);
 int choose_tile(int64_t M, int64_t N, int64_t K, int din);
-int gemm_knob();
-void set_gemm_knob(int k);
 int tile_rows(int tile);
 int tile_cols(int tile);
 

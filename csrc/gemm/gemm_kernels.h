@@ -177,6 +177,7 @@ template <int OUT> constexpr int out_size() { return OUT == DT_F32 ? 4 : 2; }
 // first row's. The acquire is at system scope: the rows were written by a copy engine or by a
 // peer GPU over xGMI, not by this agent.
 // Thread 0 spins and acquires; the caller orders the other threads after it with a barrier.
+template <bool OWN_FIRST = true>  // false: tile_order 3 compiled out (see tile_map.h)
 __device__ __forceinline__ void wait_flag_t0(const GemmArgs& p, int64_t row_first,
                                              int64_t row_last) {
   if (threadIdx.x == 0) {
@@ -184,7 +185,7 @@ __device__ __forceinline__ void wait_flag_t0(const GemmArgs& p, int64_t row_firs
     const unsigned want = p.epoch_ptr ? *p.epoch_ptr : p.epoch;
     for (int sh = s0; sh <= s1; ++sh) {
       // tile_order 3: the first producer's blocks are the caller's own rows (never gated)
-      if (p.tile_order == 3 && sh / p.nsub == p.first_shard) continue;
+      if (OWN_FIRST && p.tile_order == 3 && sh / p.nsub == p.first_shard) continue;
       unsigned* f = const_cast<unsigned*>(p.flags) + sh;
       unsigned spins = 0;
       while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
@@ -205,9 +206,10 @@ __device__ __forceinline__ void wait_flag_t0(const GemmArgs& p, int64_t row_firs
   }
 }
 
+template <bool OWN_FIRST = true>
 __device__ __forceinline__ void wait_flag(const GemmArgs& p, int64_t row_first, int64_t row_last) {
   if (p.flags == nullptr) return;
-  wait_flag_t0(p, row_first, row_last);
+  wait_flag_t0<OWN_FIRST>(p, row_first, row_last);
   __syncthreads();
 }
 
@@ -976,7 +978,10 @@ __global__ __launch_bounds__(512) void gemm_tn_t4_kernel(const GemmArgs p) {
 //  * DEFER (12 / 12 reads): Q00 after phase A of the last K-tile, the other three after phase
 //    B; every wait is 8, plus the stores issued after the unit it waits for (iter below).
 // (stores count in issue order with the LDS-DMA; the counts keep exactly the ops issued after
-// the unit the next phase reads in flight).
+// the unit the next phase reads in flight). Round 4 measured leaving the previous tile's stores
+// in flight for one more phase of the next tile (KIND 2 waits 8 + 4 NS / 8 + 3 NS): neutral on
+// every shape (profiles/r04/r4_7_ab_store_slack.txt): the store cost is CU-side issue, not the
+// wait for the write acknowledgements.
 // Load phases carry no VALU (round 3, profiles/r03/r3_20..r3_22: the un-prioritized loading wave
 // pays ~90 cycles per VALU at the head of a segment, MI355X_MICROARCH.md "Two waves per SIMD"
 // item 6; lab flagship 0.1093 -> 0.1039 ms, 8192^3 0.7555 -> 0.7286):
@@ -1011,7 +1016,9 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   // (profiles/r03/r3_27, r3_33), and their arrival gate sits at that schedule's A staging.
   constexpr bool DEFER = !GATED && CMODE == 2;
   constexpr int NH = DEFER ? 2 : 1;  // fragment register sets
-  const bool slack = (p.knob & 1) == 0;  // A/B: C stores left in flight into the next tile
+  // tile_order 3 (own rows first, never gated) exists only for the RCCL-fed gated GEMM, whose A
+  // is a row table (APAN): every other pt4 kernel compiles it out (SGPR pressure)
+  constexpr bool OWN = GATED && APAN;
   __shared__ __attribute__((aligned(1024))) char smem[8 * UNIT];
   // CMODE 2: C through one wave-uniform descriptor (launch_pt4 checks the extent fits)
   const __amdgpu_buffer_rsrc_t crc =
@@ -1023,7 +1030,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   const int esz = Mma::kElem;
   const int nk = p.K * esz / ROWB;  // even (pt4_ok)
   int bid = (int)blockIdx.x, nblk = (int)gridDim.x;
-  if constexpr (GATED) {
+  if constexpr (GATED && !APAN) {  // (the in-kernel all-gather reads plain A rows: gemm_launch)
     if (p.ag_ctas > 0) {  // in-kernel all-gather: the first ag_ctas workgroups copy
       if (bid < p.ag_ctas) {
         ag_copy_role<Mma::kElem>(p);
@@ -1070,7 +1077,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   };
   const char* na = nullptr;  // APAN: the next tile's A panel
   auto origin = [&](int ti, int64_t& m0, int64_t& n0) __attribute__((always_inline)) {
-    const int wg = tile_index_virtual(p, bid + ti * nblk, ntiles);
+    const int wg = tile_index_virtual<OWN>(p, bid + ti * nblk, ntiles);
     int tm_, tn_;
     tile_mn(p, wg, p.M / 256, tiles_n, tm_, tn_);
     m0 = (int64_t)tm_ * 256;
@@ -1218,7 +1225,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   const bool g1 = wr == 1;  // wave-uniform (wave came through readfirstlane)
   if constexpr (GATED) {  // arrival gate of the first tile
     const int64_t f0 = flag_row(nm0);
-    wait_flag(p, f0, f0 + 255);
+    wait_flag<OWN>(p, f0, f0 + 255);
   }
   Cur q0{0, 0}, q1{0, 0};
   adv(q1);
@@ -1259,34 +1266,21 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
       stage(0, 1, BUF ^ 1, qa);
       stage(1, 1, BUF ^ 1, qa);
       T4_LGKM0();
-      // KIND 2 (first K-tile after a tile's last): phase B reads K-tile 0 halves 1, staged in
-      // the last K-tile's phase A before ALL four quadrants' stores -> 8 + 4 NS may stay out
-      if (g1) {
-        if (slack) wait_vm<KIND == 2 ? 8 + 4 * NS : 8>();
-        else wait_vm<KIND == 2 ? 8 + 3 * NS : 8>();
-      }
+      if (g1) wait_vm<KIND == 2 ? 8 + 3 * NS : 8>();
       T4_BAR();
       __builtin_amdgcn_s_setprio(1);
       if constexpr (DEF) mm(1, 1, false);
       mm(0, 0, Z);
       __builtin_amdgcn_s_setprio(0);
       if constexpr (KIND == 1) store_q(0, 0);
-      if (!g1) {
-        if (slack) wait_vm<KIND == 2 ? 8 + 4 * NS : (KIND == 1 ? 8 + NS : 8)>();
-        else wait_vm<KIND == 2 ? 8 + 3 * NS : (KIND == 1 ? 8 + NS : 8)>();
-      }
+      if (!g1) wait_vm<KIND == 2 ? 8 + 3 * NS : (KIND == 1 ? 8 + NS : 8)>();
       T4_BAR();
       loadB(bufc, 1);  // phase B: halves 1
       loadA(bufc, 1);
       stage(0, 0, BUF, qb);
       stage(1, 0, BUF, qb);
       T4_LGKM0();
-      // KIND 2: the next phase (K-tile 1, phase A) reads K-tile 1 halves 0, staged in the last
-      // K-tile's phase B before its three quadrants' stores -> 8 + 3 NS may stay out
-      if (g1) {
-        if (slack) wait_vm<KIND == 1 ? 8 + NS : (KIND == 2 ? 8 + 3 * NS : 8)>();
-        else wait_vm<KIND == 1 ? 8 + NS : 8>();
-      }
+      if (g1) wait_vm<KIND == 1 ? 8 + NS : 8>();
       T4_BAR();
       __builtin_amdgcn_s_setprio(1);
       mm(0, 1, Z);
@@ -1303,10 +1297,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
           acc[4 + f][3] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
-      if (!g1) {
-        if (slack) wait_vm<KIND == 1 ? 8 + 4 * NS : (KIND == 2 ? 8 + 3 * NS : 8)>();
-        else wait_vm<KIND == 1 ? 8 + 4 * NS : 8>();
-      }
+      if (!g1) wait_vm<KIND == 1 ? 8 + 4 * NS : 8>();
       T4_BAR();
     } else {
       if (GATED && qa.kt == 0) {
@@ -1316,7 +1307,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
         // groups insert it at the same place, so their one-barrier stagger is unchanged; an extra
         // barrier only adds ordering (LDS RAW / WAR distances grow).
         const int64_t f0 = flag_row(nm0);  // qa.ti is the next tile (or tile 0)
-        wait_flag_t0(p, f0, f0 + 255);
+        wait_flag_t0<OWN>(p, f0, f0 + 255);
         T4_BAR();
       }
       loadB(bufc, 0);  // phase A

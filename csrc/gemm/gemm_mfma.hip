@@ -78,20 +78,11 @@ int choose_tile(int64_t M, int64_t N, int64_t K, int din) {
   return TILE_128x128;
 }
 
-// Kernel A/B switches (GemmArgs::knob): DDLB_GEMM_KNOB at first use, set_gemm_knob() after.
-static int g_knob = -1;
-int gemm_knob() {
-  if (g_knob < 0) g_knob = getenv("DDLB_GEMM_KNOB") ? atoi(getenv("DDLB_GEMM_KNOB")) : 0;
-  return g_knob;
-}
-void set_gemm_knob(int k) { g_knob = k; }
-
 hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mode,
                        hipStream_t s) {
   GemmArgs p = p_in;
   static const int raster_env = getenv("DDLB_RASTER_G") ? atoi(getenv("DDLB_RASTER_G")) : 0;
   if (raster_env > 0) p.raster_g = raster_env;  // A/B knob of the tile raster (tile_map.h)
-  p.knob = gemm_knob();
   if (p.a_grp <= 0) { p.a_grp = p.M > 0 ? p.M : 1; p.a_gstride = p.a_grp; }
   if (p.c_grp <= 0) { p.c_grp = p.M > 0 ? p.M : 1; p.c_gstride = p.c_grp; }
   switch (tile) {  // known codes only (the retired families' codes are refused, not rerouted)

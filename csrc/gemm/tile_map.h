@@ -30,9 +30,12 @@ __host__ __device__ inline int xcd_remap(int bid, int nwg) {
 // tile_order 3 (own first): the first producer's nsub blocks (the caller's own rows: a gated
 // GEMM never waits for them, wait_flag_t0), then block-major over the other producers, rotating
 // from first_shard + 1 (the order the stage collectives of an RCCL-fed gated GEMM deliver them).
+// OWN_FIRST = false compiles tile_order 3 out (it then dispatches like 1): the ungated kernels
+// never get it, and the extra branch cost the flagship kernel 11 spilled SGPRs.
+template <bool OWN_FIRST = true>
 __host__ __device__ inline int ordered_shard(const GemmArgs& p, int j) {
   const int np = p.nshards / p.nsub;
-  if (p.tile_order == 3) {
+  if (OWN_FIRST && p.tile_order == 3) {
     if (j < p.nsub || np < 2) return p.first_shard * p.nsub + j;
     j -= p.nsub;
     return ((p.first_shard + 1 + j % (np - 1)) % np) * p.nsub + j / (np - 1);
@@ -40,6 +43,7 @@ __host__ __device__ inline int ordered_shard(const GemmArgs& p, int j) {
   return ((p.first_shard + j % np) % np) * p.nsub + j / np;
 }
 
+template <bool OWN_FIRST = true>
 __host__ __device__ inline int tile_index_virtual(const GemmArgs& p, int vid, int nwg) {
   if (!p.tile_order) return xcd_remap(vid, nwg);
   if (p.tile_order == 2) {
@@ -51,7 +55,7 @@ __host__ __device__ inline int tile_index_virtual(const GemmArgs& p, int vid, in
   }
   const int per = nwg / p.nshards;
   const int j = vid / per, local = vid % per;
-  return ordered_shard(p, j) * per + xcd_remap(local, per);
+  return ordered_shard<OWN_FIRST>(p, j) * per + xcd_remap(local, per);
 }
 
 // Tile id -> (tm, tn). Row-major, except that without a shard order and with more than 4 column
