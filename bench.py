@@ -73,59 +73,65 @@ def _graph(opts):
     return dict(opts, graph=True)
 
 
-# N > 1, RCCL candidates first: RCCL is the vendor-proven transport and our plans drive it on
-# our own communicator and streams (BASELINE config #4 = coll_pipeline over RCCL). The IPC / xGMI
-# candidates follow; the preflight drops whichever family this node cannot run.
+# N > 1 pool, ordered by the one-GPU per-rank budget (scripts/plan_budget.py --world 8,
+# profiles/r04/r4_6_budget_col8.txt: rank 0's d = 8 plan replayed on one GPU, transfers as local
+# copies -- an emulated lower bound): each family's best form first, the RCCL and IPC / xGMI
+# families interleaved, dominated variants last (the tuning deadline cuts the tail). The
+# preflight (RCCL, IPC, in-kernel all-gather, direct store, RCCL-fed gated GEMM, across the real
+# peers) drops whatever this node cannot run.
 # "/graph": the whole plan is captured once and replayed with one hipGraphLaunch per run (the IPC
 # pipelines issue ~200 HIP calls per run at d = 8 otherwise, profiles/r02/r2_13_*).
 CANDIDATES = [
     # RCCL stage all-gathers feeding ONE flag-gated persistent GEMM over all m rows (the
     # flagship's 1024-tile pt4 kernel at m = 65536; per stage a signal kernel raises the
     # arrival flags, the own rows run first, ungated): no under-filled stage GEMMs (at d = 8,
-    # s = 8 a stage GEMM has 128 tiles of 256^2 for 256 CUs)
-    ("coll_pipeline/rccl/s8/fused", "native", dict(_COLL4, s=8, fused=True)),
+    # s = 8 a stage GEMM has 128 tiles of 256^2 for 256 CUs). Budget 0.196 ms (s4), GEMM work
+    # 0.116-0.119 ms (5 tile rounds on the CUs RCCL leaves)
     ("coll_pipeline/rccl/s4/fused", "native", dict(_COLL4, fused=True)),
-    ("coll_pipeline/rccl/s8/fused/r48", "native", dict(_COLL4, s=8, fused=True, reserve_cus=48)),
+    # in-kernel all-gather: budget 0.128 ms (graph), GEMM work 0.085 ms
+    ("coll_pipeline/ipc/agk32/s4/graph", "native", _graph(dict(_AGK, s=4))),
+    # one GEMM reading every peer's shard in place over xGMI (pt4 through a shard table)
+    ("direct/ipc", "native", dict(algorithm="direct", backend="ipc")),
+    ("coll_pipeline/rccl/s8/fused", "native", dict(_COLL4, s=8, fused=True)),
     ("coll_pipeline/rccl/s4", "native", _COLL4),
-    ("coll_pipeline/rccl/s8", "native", dict(_COLL4, s=8)),
+    ("coll_pipeline/ipc/agk32/s8/graph", "native", _graph(_AGK)),
     ("default/rccl", "native", _DEF),
+    ("p2p_pipeline/rccl/fused", "native", dict(algorithm="p2p_pipeline", backend="rccl",
+                                               fused=True)),
+    ("coll_pipeline/ipc/agk64/s8/graph", "native", _graph(dict(_AGK, copy_blocks=64))),
+    ("default/ipc/kernel", "native", _DEF_K),
+    ("coll_pipeline/rccl/s8", "native", dict(_COLL4, s=8)),
+    ("p2p_pipeline/rccl", "native", dict(algorithm="p2p_pipeline", backend="rccl")),
+    ("coll_pipeline/ipc/kernel/s4", "native", dict(_COLL_IPC, multicast_protocol="kernel",
+                                                   copy_blocks=128, tile="128x128")),
+    ("p2p_pipeline/ipc/memcpy/graph", "native", _graph(_P2P)),
+    ("coll_pipeline/ipc/memcpy/s4/graph", "native", _graph(_COLL_IPC)),
+    ("default/ipc/push", "native", dict(_P2P, algorithm="default", direction="push")),
+    ("coll_pipeline/ipc/push/s4", "native", dict(_COLL_IPC, direction="push")),
     # the stage GEMMs next to RCCL's CU-resident kernels: 128x128 tiles (4x as many, dispatched
     # dynamically) let the CUs busy with RCCL simply take fewer of them
     ("coll_pipeline/rccl/s4/128", "native", dict(_COLL4, tile="128x128")),
-    # RCCL's kernels on a CU-masked comm stream (csrc/comm: hipExtStreamCreateWithCUMask), the
-    # stage GEMMs sized to the complement; buffers registered with ncclCommRegister
-    ("coll_pipeline/rccl/s4/cumask", "native", dict(_COLL4, comm_cus=32, register=True)),
-    ("coll_pipeline/rccl/s8/cumask", "native", dict(_COLL4, s=8, comm_cus=32, register=True)),
-    ("coll_pipeline/rccl/s4/cumask64", "native", dict(_COLL4, comm_cus=64)),
     ("coll_pipeline/rccl/s4/128/c16", "native", dict(_COLL4, tile="128x128",
                                                       _env={"NCCL_MAX_NCHANNELS": "16"})),
-    ("p2p_pipeline/rccl", "native", dict(algorithm="p2p_pipeline", backend="rccl")),
-    ("p2p_pipeline/rccl/fused", "native", dict(algorithm="p2p_pipeline", backend="rccl",
-                                               fused=True)),
-    ("coll_pipeline/ipc/agk32/s8/graph", "native", _graph(_AGK)),
-    ("coll_pipeline/ipc/agk64/s8/graph", "native", _graph(dict(_AGK, copy_blocks=64))),
-    ("coll_pipeline/ipc/memcpy/s8/graph", "native", _graph(dict(_COLL_IPC, s=8))),
     ("coll_pipeline/ipc/kernel/s8/graph", "native", _graph(dict(
         _COLL_IPC, s=8, multicast_protocol="kernel", copy_blocks=128, tile="128x128"))),
-    ("direct/ipc", "native", dict(algorithm="direct", backend="ipc")),
     ("coll_pipeline/ipc/batch/s8/graph", "native", _graph(dict(
         _COLL_IPC, s=8, multicast_protocol="batch_memcpy"))),
-    ("coll_pipeline/ipc/memcpy/s4/graph", "native", _graph(_COLL_IPC)),
-    ("p2p_pipeline/ipc/memcpy/graph", "native", _graph(_P2P)),
+    ("coll_pipeline/ipc/memcpy/s8/graph", "native", _graph(dict(_COLL_IPC, s=8))),
     # one flag-gated GEMM fed by copy-engine pulls: eager only (a graph would have to order the
     # gated GEMM after every copy stream, see PlanExecutor::graph_capturable)
     ("coll_pipeline/ipc/memcpy/s8/fused", "native", dict(_COLL_IPC, s=8, fused=True)),
+    # RCCL's kernels on a CU-masked comm stream (csrc/comm: hipExtStreamCreateWithCUMask), the
+    # stage GEMMs sized to the complement; buffers registered with ncclCommRegister (budget:
+    # 3.5x the unmasked plans: the masked GEMMs lose 32-64 CUs for the whole run)
+    ("coll_pipeline/rccl/s4/cumask", "native", dict(_COLL4, comm_cus=32, register=True)),
+    ("coll_pipeline/rccl/s8/cumask", "native", dict(_COLL4, s=8, comm_cus=32, register=True)),
+    ("coll_pipeline/rccl/s4/cumask64", "native", dict(_COLL4, comm_cus=64)),
+    ("p2p_pipeline/ipc/memcpy/cs2", "native", dict(_P2P, copy_streams=2)),
     # each peer's chunks split over 2 copy streams (2 copy engines per link)
     ("coll_pipeline/ipc/memcpy/s8/cs2/graph", "native",
      dict(_COLL_IPC, s=8, copy_streams=2, graph=True)),
-    ("coll_pipeline/ipc/kernel/s4", "native", dict(_COLL_IPC, multicast_protocol="kernel",
-                                                   copy_blocks=128, tile="128x128")),
     ("coll_pipeline/ipc/memcpy/s8", "native", dict(_COLL_IPC, s=8)),
-    ("coll_pipeline/ipc/agk32/s4/graph", "native", _graph(dict(_AGK, s=4))),
-    ("default/ipc/kernel", "native", _DEF_K),
-    ("p2p_pipeline/ipc/memcpy/cs2", "native", dict(_P2P, copy_streams=2)),
-    ("coll_pipeline/ipc/push/s4", "native", dict(_COLL_IPC, direction="push")),
-    ("default/ipc/push", "native", dict(_P2P, algorithm="default", direction="push")),
 ]
 VENDOR = [
     ("pytorch(rccl+hipblaslt)", "pytorch", dict(backend="nccl", empty_cache=False)),

@@ -127,11 +127,13 @@ def test_candidate_pools():
 
     col8 = bench.candidate_pool("tp_columnwise", "bfloat16", 8)
     assert any(c[0] == "direct/ipc" for c in col8) and all(c[0][:4] != "row/" for c in col8)
-    # RCCL candidates first, the vendor slot last; no vendor-library GEMM behind "native"
+    # the families interleaved by the per-rank budget: the RCCL-fed fused GEMM, the in-kernel
+    # all-gather and direct/ipc lead; the vendor slot last; no vendor-library GEMM behind native
     natives = [c for c in col8 if c[1] == "native"]
-    assert natives[0][2]["backend"] == "rccl" and col8[-1][1] == "pytorch"
-    first_ipc = next(i for i, c in enumerate(natives) if c[2]["backend"] == "ipc")
-    assert all(c[2]["backend"] == "rccl" for c in natives[:first_ipc])
+    assert [c[0] for c in natives[:3]] == ["coll_pipeline/rccl/s4/fused",
+                                           "coll_pipeline/ipc/agk32/s4/graph", "direct/ipc"]
+    assert col8[-1][1] == "pytorch"
+    assert {c[2]["backend"] for c in natives[:5]} == {"rccl", "ipc"}
     for pool in (col8, bench.candidate_pool("tp_rowwise", "bfloat16", 8),
                  bench.candidate_pool("tp_columnwise", "bfloat16", 1)):
         assert not any("blas" in str(c[2]) for c in pool)
