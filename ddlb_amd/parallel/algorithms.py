@@ -416,13 +416,17 @@ def _col_rccl_fused_coll(plan, rank, d, m, n, k, ein, cfg, A, Bt, C, comm_dt, gd
         for j in range(s):
             table.append(A + (rank * ml + j * rows) * k * ein if p == rank
                          else G + (j * d + p) * blk)
+    s_sig = 2  # the signal kernels run on their own stream, off the collectives' critical path
     for j in range(s):
         plan.allgather(S_COMM, A + (rank * ml + j * rows) * k * ein, G + j * d * blk, rows * k,
                        comm_dt)
+        e = plan.event()
+        plan.record(S_COMM, e)
+        plan.wait(s_sig, e)
         # a kernel (release at system scope after the collective's kernel): the gated tiles
         # acquire the rows RCCL wrote; a stream memop has no such fence
         for c in _chunks([flags.ref("ARRIVE", p * s + j) for p in range(d) if p != rank]):
-            plan.signal(S_COMM, c, method=SIG_KERNEL)
+            plan.signal(s_sig, c, method=SIG_KERNEL)
     plan.gemm(S_MAIN, A, Bt, C, M=m, N=n, K=k, lda=k, ldb=k, ldc=n, **gdt,
               a_shards=table, shard_rows=rows, flags=flags.ref("ARRIVE", 0), flag_rows=rows,
               nshards=d * s, nsub=s, first_shard=rank, tile_order=3,
@@ -437,13 +441,17 @@ def _col_rccl_fused_p2p(plan, rank, d, m, n, k, ein, cfg, A, Bt, C, comm_dt, gdt
     ml = m // d
     flags = _Flags(plan, d, 1, symmetric=False)
     _signal(plan, S_MAIN, [flags.ref("ARRIVE", rank)], cfg)
+    s_sig = 2  # signal kernels off the send / recv stream (see _col_rccl_fused_coll)
     for j in range(1, d):
         to, frm = (rank - j) % d, (rank + j) % d
         plan.group_start(S_COMM)
         plan.send(S_COMM, A + rank * ml * k * ein, ml * k, comm_dt, to)
         plan.recv(S_COMM, A + frm * ml * k * ein, ml * k, comm_dt, frm)
         plan.group_end(S_COMM)
-        plan.signal(S_COMM, [flags.ref("ARRIVE", frm)], method=SIG_KERNEL)
+        e = plan.event()
+        plan.record(S_COMM, e)
+        plan.wait(s_sig, e)
+        plan.signal(s_sig, [flags.ref("ARRIVE", frm)], method=SIG_KERNEL)
     plan.gemm(S_MAIN, A, Bt, C, M=m, N=n, K=k, lda=k, ldb=k, ldc=n, **gdt,
               flags=flags.ref("ARRIVE", 0), flag_rows=ml, nshards=d, first_shard=rank,
               tile_order=1, reserve_cus=cfg.reserve_cus)

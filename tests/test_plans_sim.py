@@ -185,7 +185,7 @@ def test_rccl_fused_coll_plan(d, s):
     assert [t.buf for t in tab[rank * s:(rank + 1) * s]] == ["A_full"] * s
     assert all(t.buf == "G" for i, t in enumerate(tab) if i // s != rank)
     assert not plan.buffers["flags"].symmetric
-    sigs = [op for op in plan.ops if op.kind == OP_SIGNAL and op.stream == 1]
+    sigs = [op for op in plan.ops if op.kind == OP_SIGNAL and op.stream == 2]
     assert all(op.args["method"] == SIG_KERNEL for op in sigs) and len(sigs) >= s
 
 
@@ -207,7 +207,7 @@ def test_rccl_fused_coll_negative_no_signal():
     built = [build_tp_columnwise(r, 2, 8, 8, 8, DT_F32, DT_F32, cfg) for r in range(2)]
     plans = [p for p, _ in built]
     for p in plans:
-        p.ops = [op for op in p.ops if not (op.kind == OP_SIGNAL and op.stream == 1)]
+        p.ops = [op for op in p.ops if not (op.kind == OP_SIGNAL and op.stream == 2)]
     sim = Simulator(plans, make_buffers(plans))
     with pytest.raises(Deadlock):
         sim.run_epoch()
