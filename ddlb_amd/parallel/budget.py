@@ -156,3 +156,63 @@ def copy_bytes(plan: Plan) -> int:
         elif op.kind == OP_REDUCE:
             total += op.args["count"] * DT_SIZE[op.args["dtype"]] * len(op.args["srcs"])
     return total
+
+
+def link_bytes(plan: Plan) -> Dict[int, int]:
+    """Bytes each peer's link carries in ONE direction in one run of rank ``plan.rank``'s ORIGINAL
+    (not emulated) plan (what it receives, or sends for pushes and direct stores): pulls / pushes
+    by copy engines or CU copies, RCCL
+    collectives and send / recv (full-mesh model: an all-gather or reduce-scatter of ``count``
+    elements per rank moves ``count`` to and from every peer), the in-kernel all-gather's row
+    blocks, a direct-access GEMM's peer shards (read once: the re-reads of an A panel by the
+    tiles of other N columns are assumed to hit the local L2) and a direct-store GEMM's peer row
+    blocks. A model for ranking candidates against a link budget, not a measurement."""
+    from ddlb_amd.parallel.plan import OP_ALLGATHER, OP_REDUCE_SCATTER, OP_RECV, OP_SEND
+
+    me = plan.rank
+    out: Dict[int, int] = {p: 0 for p in range(plan.world) if p != me}
+
+    def peer(ref: Optional[Ref]) -> Optional[int]:
+        return ref.owner if ref is not None and ref.owner not in (None, me) else None
+
+    for op in plan.ops:
+        a, k = op.args, op.kind
+        if k == OP_COPY:
+            p = peer(a["src"]) if peer(a["src"]) is not None else peer(a["dst"])
+            if p is not None:
+                out[p] += a["nbytes"]
+        elif k in (OP_COPY_MULTI, OP_COPY_BATCH):
+            for dst, src, n in a["segs"]:
+                p = peer(src) if peer(src) is not None else peer(dst)
+                if p is not None:
+                    out[p] += n
+        elif k in (OP_ALLGATHER, OP_REDUCE_SCATTER):
+            for p in out:
+                out[p] += a["count"] * DT_SIZE[a["dtype"]]
+        elif k in (OP_SEND, OP_RECV):
+            if a["peer"] in out:
+                out[a["peer"]] += a["count"] * DT_SIZE[a["dtype"]]
+        elif k == OP_REDUCE:
+            for src in a["srcs"]:
+                p = peer(src)
+                if p is not None:
+                    out[p] += a["count"] * DT_SIZE[a["dtype"]]
+        elif k == OP_GEMM:
+            es, eo = DT_SIZE[a["din"]], DT_SIZE[a["dout"]]
+            g = a.get("ag")
+            if g is not None:
+                npro, nsub = a["nshards"] // a["nsub"], a["nsub"]
+                for q in range(npro):
+                    if q != g["rank"] and q in out:
+                        out[q] += nsub * a["flag_rows"] * a["lda"] * es
+            for i, ref in enumerate(a.get("a_shards") or []):
+                p = peer(ref)
+                if p is not None:
+                    rows = min(a["shard_rows"], a["M"] - i * a["shard_rows"])
+                    out[p] += max(rows, 0) * a["K"] * es
+            for i, ref in enumerate(a.get("c_shards") or []):
+                p = peer(ref)
+                if p is not None:
+                    rows = min(a["c_shard_rows"], a["M"] - i * a["c_shard_rows"])
+                    out[p] += max(rows, 0) * a["N"] * eo
+    return out

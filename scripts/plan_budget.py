@@ -8,7 +8,10 @@ of the same bytes on the same streams / engines, flags pre-set) and timed:
 * ``plan_ms``      the whole emulated plan (GEMMs + concurrent copies + signal / wait ops), eager;
 * ``graph_ms``     the same with hipGraph replay, where the plan is capturable;
 * ``host_us``      host time of one ``run()`` call (enqueue only; the device is idle before it);
-* op counts and the bytes the copies move.
+* op counts and the bytes the copies move;
+* ``link_us``      a MODEL, not a measurement: the most loaded peer link's bytes
+                   (``budget.link_bytes``) at ``--link-gbps`` per direction, i.e. the transfer
+                   floor a real d-rank node adds beside the GEMM work.
 
 EMULATED: local HBM copies stand in for xGMI links and no peer is ever late, so this is a budget
 (a lower bound on rank 0's time), never a scaling value.
@@ -122,6 +125,8 @@ def main(argv=None) -> int:
     ap.add_argument("--candidates", default="")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rccl-blocks", type=int, default=32)
+    ap.add_argument("--link-gbps", type=float, default=64.0,
+                    help="per-direction xGMI link bandwidth of the link_us model (GB/s)")
     ap.add_argument("--out", default="")
     ap.add_argument("--timeline", default="",
                     help="comma list of candidates whose last eager run is printed as a per-op "
@@ -132,7 +137,7 @@ def main(argv=None) -> int:
 
     from ddlb_amd.communicator import Communicator
     from ddlb_amd.parallel.algorithms import build_tp_columnwise, build_tp_rowwise
-    from ddlb_amd.parallel.budget import copy_bytes, op_counts, signal_ops
+    from ddlb_amd.parallel.budget import copy_bytes, link_bytes, op_counts, signal_ops
     from ddlb_amd.primitives.native_common import dtype_codes
 
     os.environ.setdefault("DDLB_CHILD_INIT_METHOD", "tcp://127.0.0.1:29517")
@@ -147,7 +152,7 @@ def main(argv=None) -> int:
           f"m={a.m} n={a.n} k={a.k} {a.dtype} (local copies stand in for xGMI; not a scaling "
           f"value)", flush=True)
     print(f"{'candidate':44s} {'gemm_ms':>8s} {'plan_ms':>8s} {'graph_ms':>8s} {'host_us':>8s} "
-          f"{'ops':>5s} {'sig':>4s} {'copyMB':>7s}", flush=True)
+          f"{'ops':>5s} {'sig':>4s} {'copyMB':>7s} {'link_us':>8s}", flush=True)
     for label, opts, cfg in candidate_cfgs(a.primitive, a.dtype, a.world):
         if want and label not in want:
             continue
@@ -156,6 +161,8 @@ def main(argv=None) -> int:
             plan, io = build(a.rank, a.world, a.m, a.n, a.k, din, dout, cfg)
             row.update(ops=len(plan.ops), signal_ops=signal_ops(plan),
                        counts=op_counts(plan))
+            lb = link_bytes(plan)
+            row["link_us"] = round(max(lb.values(), default=0) / (a.link_gbps * 1e3), 1)
             from ddlb_amd.parallel.budget import emulate
             row["copy_mb"] = round(copy_bytes(emulate(plan, a.rccl_blocks)) / 2 ** 20, 1)
             tl = [c.strip() for c in a.timeline.split(",") if c.strip()]
@@ -171,7 +178,8 @@ def main(argv=None) -> int:
 
         print(f"{label:44s} {f('gemm_ms')} {f('plan_ms')} {f('graph_ms')} "
               f"{row.get('plan_host_us', 0.0):8.1f} {row.get('ops', 0):5d} "
-              f"{row.get('signal_ops', 0):4d} {row.get('copy_mb', 0.0):7.1f}"
+              f"{row.get('signal_ops', 0):4d} {row.get('copy_mb', 0.0):7.1f} "
+              f"{row.get('link_us', 0.0):8.1f}"
               + (f"  {row['error']}" if "error" in row else ""), flush=True)
         if "timeline" in row:
             print(row["timeline"], flush=True)

@@ -65,3 +65,28 @@ def test_emulated_plan_runs_alone(d, prim, label, cfg):
     g = gemm_only(ep)
     assert all(op.kind == OP_GEMM and op.stream == 0 and op.args["flags"] is None
                for op in g.ops)
+
+
+def test_link_bytes_model():
+    """The per-peer link model: an all-gather of a rank's m/d rows moves them to every peer; the
+    in-kernel all-gather and the direct-access GEMM move the same bytes; a direct-store GEMM
+    writes each peer's output block."""
+    from ddlb_amd.parallel.algorithms import AlgoConfig
+    from ddlb_amd.parallel.budget import link_bytes
+    from ddlb_amd.parallel.plan import DT_BF16
+
+    d, m, n, k = 8, 65536, 1024, 1024
+    shard = m // d * k * 2
+    for cfg in (AlgoConfig(algorithm="default", backend="rccl"),
+                AlgoConfig(algorithm="coll_pipeline", backend="rccl", s=8, fused=True),
+                AlgoConfig(algorithm="direct", backend="ipc"),
+                AlgoConfig(algorithm="coll_pipeline", backend="ipc", fused=True, s=4,
+                           protocol="kernel", copy_blocks=32),
+                AlgoConfig(algorithm="coll_pipeline", backend="ipc", s=4)):
+        plan, _ = build_tp_columnwise(3, d, m, n, k, DT_BF16, DT_BF16, cfg)
+        lb = link_bytes(plan)
+        assert sorted(lb) == [p for p in range(d) if p != 3]
+        assert all(v == shard for v in lb.values()), (cfg, lb)
+    plan, _ = build_tp_rowwise(0, d, 16384, 8192, 8192, DT_BF16, DT_BF16,
+                               AlgoConfig(algorithm="p2p_pipeline", backend="ipc", fused=True))
+    assert all(v == 16384 // d * 8192 * 2 for v in link_bytes(plan).values())
