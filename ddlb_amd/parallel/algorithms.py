@@ -83,6 +83,11 @@ class AlgoConfig:
     # (hipExtStreamCreateWithCUMask), stream-0 GEMMs on the complement; 0 = unmasked
     comm_cus: int = 0
     register: bool = False              # RCCL buffers from ncclMemAlloc + ncclCommRegister
+    # RCCL-fed fused GEMM: enqueue the gated GEMM BEFORE the stage collectives, so its own (never
+    # gated) tiles start at once instead of after the host has enqueued every collective (RCCL
+    # calls cost the host several us each); needs the GEMM and the comm stream on different
+    # hardware queues (GPU_MAX_HW_QUEUES >= 2; the plan builder falls back otherwise)
+    gemm_first: bool = True
 
 
 @dataclass
@@ -391,6 +396,19 @@ def _build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, do
     return plan, io
 
 
+def _gemm_first(cfg: AlgoConfig) -> bool:
+    """Enqueue an RCCL-fed gated GEMM ahead of its producers? Only with >= 2 hardware queues per
+    process: with one, the GEMM's spinning tiles would sit in front of the collectives that set
+    their flags in a single in-order queue."""
+    import os
+
+    try:
+        queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    except ValueError:
+        queues = 4
+    return cfg.gemm_first and queues >= 2
+
+
 def _col_rccl_fused_coll(plan, rank, d, m, n, k, ein, cfg, A, Bt, C, comm_dt, gdt) -> None:
     """coll_pipeline over RCCL feeding ONE persistent flag-gated GEMM over all m rows
     (``TPColumnwise/fuser.py:59-100`` semantics, SURVEY.md §7.3 hard part #1: at d = 8, s = 8 a
@@ -416,6 +434,12 @@ def _col_rccl_fused_coll(plan, rank, d, m, n, k, ein, cfg, A, Bt, C, comm_dt, gd
         for j in range(s):
             table.append(A + (rank * ml + j * rows) * k * ein if p == rank
                          else G + (j * d + p) * blk)
+    gemm = dict(M=m, N=n, K=k, lda=k, ldb=k, ldc=n, **gdt, a_shards=table, shard_rows=rows,
+                flags=flags.ref("ARRIVE", 0), flag_rows=rows, nshards=d * s, nsub=s,
+                first_shard=rank, tile_order=3, reserve_cus=cfg.reserve_cus)
+    first = _gemm_first(cfg)
+    if first:
+        plan.gemm(S_MAIN, A, Bt, C, **gemm)
     s_sig = 2  # the signal kernels run on their own stream, off the collectives' critical path
     for j in range(s):
         plan.allgather(S_COMM, A + (rank * ml + j * rows) * k * ein, G + j * d * blk, rows * k,
@@ -427,20 +451,24 @@ def _col_rccl_fused_coll(plan, rank, d, m, n, k, ein, cfg, A, Bt, C, comm_dt, gd
         # acquire the rows RCCL wrote; a stream memop has no such fence
         for c in _chunks([flags.ref("ARRIVE", p * s + j) for p in range(d) if p != rank]):
             plan.signal(s_sig, c, method=SIG_KERNEL)
-    plan.gemm(S_MAIN, A, Bt, C, M=m, N=n, K=k, lda=k, ldb=k, ldc=n, **gdt,
-              a_shards=table, shard_rows=rows, flags=flags.ref("ARRIVE", 0), flag_rows=rows,
-              nshards=d * s, nsub=s, first_shard=rank, tile_order=3,
-              reserve_cus=cfg.reserve_cus)
+    if not first:
+        plan.gemm(S_MAIN, A, Bt, C, **gemm)
 
 
 def _col_rccl_fused_p2p(plan, rank, d, m, n, k, ein, cfg, A, Bt, C, comm_dt, gdt) -> None:
     """p2p_pipeline over RCCL send / recv (``TPColumnwise/fuser.py:102-146``) feeding ONE
     flag-gated GEMM over all m rows: step j receives shard (r+j)%d into its rows of A and a
     signal kernel raises ARRIVE[(r+j)%d]; the tiles run shard by shard from the own one
-    (tile_order 1 from ``first_shard`` = rank: the order the steps deliver them)."""
+    (tile_order 3: the own shard first and never gated, then (r+1)%d, ...: the order the steps
+    deliver them); the GEMM is enqueued first (``AlgoConfig.gemm_first``)."""
     ml = m // d
     flags = _Flags(plan, d, 1, symmetric=False)
-    _signal(plan, S_MAIN, [flags.ref("ARRIVE", rank)], cfg)
+    gemm = dict(M=m, N=n, K=k, lda=k, ldb=k, ldc=n, **gdt, flags=flags.ref("ARRIVE", 0),
+                flag_rows=ml, nshards=d, first_shard=rank, tile_order=3,
+                reserve_cus=cfg.reserve_cus)
+    first = _gemm_first(cfg)
+    if first:
+        plan.gemm(S_MAIN, A, Bt, C, **gemm)
     s_sig = 2  # signal kernels off the send / recv stream (see _col_rccl_fused_coll)
     for j in range(1, d):
         to, frm = (rank - j) % d, (rank + j) % d
@@ -452,9 +480,8 @@ def _col_rccl_fused_p2p(plan, rank, d, m, n, k, ein, cfg, A, Bt, C, comm_dt, gdt
         plan.record(S_COMM, e)
         plan.wait(s_sig, e)
         plan.signal(s_sig, [flags.ref("ARRIVE", frm)], method=SIG_KERNEL)
-    plan.gemm(S_MAIN, A, Bt, C, M=m, N=n, K=k, lda=k, ldb=k, ldc=n, **gdt,
-              flags=flags.ref("ARRIVE", 0), flag_rows=ml, nshards=d, first_shard=rank,
-              tile_order=1, reserve_cus=cfg.reserve_cus)
+    if not first:
+        plan.gemm(S_MAIN, A, Bt, C, **gemm)
 
 
 def _col_push(plan, rank, d, ml, cfg, flags, arow, crow, gemm, row_bytes) -> None:

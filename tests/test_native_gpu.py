@@ -682,15 +682,18 @@ def test_a_table_gemm_world1(comm, tile, dt, mode):
     ctx.close()
 
 
+@pytest.mark.parametrize("first", [False, True])
 @pytest.mark.parametrize("dt,mode", [("bf16", 0), ("fp8", 2)])
 @pytest.mark.parametrize("s", [2, 4])
-def test_rccl_fed_gated_gemm_world1(comm, dt, mode, s):
+def test_rccl_fed_gated_gemm_world1(comm, dt, mode, s, first):
     """The RCCL-fed coll_pipeline's fused GEMM in one process: stage j's (world-1) RCCL
     all-gather lands the "peer" rows in a stage-major gather buffer, a signal kernel on the comm
     stream raises their ARRIVE flag, and ONE gated persistent pt4 reads A through a row-block
     table: the own blocks in place (never gated, dispatched first: tile_order 3), the peer
     blocks from the gather buffer (NaN-filled before every run, so a tile that did not wait
-    fails). Two junk GEMMs hold the comm stream back while the gated GEMM starts."""
+    fails). Two junk GEMMs hold the comm stream back while the gated GEMM starts; ``first``:
+    the gated GEMM is enqueued BEFORE its producers (AlgoConfig.gemm_first; no junk GEMMs then:
+    a persistent kernel queued behind the spinning tiles needs more CUs than they leave)."""
     from ddlb_amd.parallel.context import NativeContext
     from ddlb_amd.parallel.plan import DT_BF16, DT_FP8, DT_U8, Plan, SIG_KERNEL
 
@@ -708,17 +711,23 @@ def test_rccl_fed_gated_gemm_world1(comm, dt, mode, s):
     c = plan.buffer("c", M * N * 2)
     junk = plan.buffer("junk", M * N * 2)
     fl = plan.buffer("flags", 256, zero=True)
-    for _ in range(2):
-        plan.gemm(1, own, bt, junk, M=ml, N=N, K=K, lda=K, ldb=K, ldc=N, din=din, dout=DT_BF16)
+    table = [own + j * rows * K * es for j in range(s)] + [G + j * rows * K * es
+                                                           for j in range(s)]
+    gated = dict(M=M, N=N, K=K, lda=K, ldb=K, ldc=N, din=din, dout=DT_BF16, tile=19, mode=mode,
+                 a_shards=table, shard_rows=rows, flags=fl, flag_rows=rows, nshards=2 * s,
+                 nsub=s, first_shard=0, tile_order=3, reserve_cus=32)
+    if first:
+        plan.gemm(0, own, bt, c, **gated)
+    else:
+        for _ in range(2):
+            plan.gemm(1, own, bt, junk, M=ml, N=N, K=K, lda=K, ldb=K, ldc=N, din=din,
+                      dout=DT_BF16)
     for j in range(s):
         plan.allgather(1, peer + j * rows * K * es, G + j * rows * K * es, rows * K,
                        DT_U8 if es == 1 else din)
         plan.signal(1, [fl + 4 * (s + j)], method=SIG_KERNEL)
-    table = [own + j * rows * K * es for j in range(s)] + [G + j * rows * K * es
-                                                           for j in range(s)]
-    plan.gemm(0, own, bt, c, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, din=din, dout=DT_BF16, tile=19,
-              mode=mode, a_shards=table, shard_rows=rows, flags=fl, flag_rows=rows,
-              nshards=2 * s, nsub=s, first_shard=0, tile_order=3, reserve_cus=32)
+    if not first:
+        plan.gemm(0, own, bt, c, **gated)
     ctx = NativeContext(comm)
     bound = ctx.bind(plan)
     A = (torch.rand(M, K, device="cuda") * 2 - 1).to(tdt)
