@@ -161,6 +161,15 @@ def _finish(plan: Plan, cfg: AlgoConfig) -> None:
                 op.args["reserve_cus"] = max(op.args.get("reserve_cus", 0), cfg.comm_cus)
 
 
+def _unique(events):
+    """Events in first-seen order without repeats (a wait per distinct event is enough)."""
+    seen: List[int] = []
+    for e in events:
+        if e not in seen:
+            seen.append(e)
+    return seen
+
+
 def _chunks(flags: List[Ref], n: int = 16):
     for i in range(0, len(flags), n):
         yield flags[i:i + n]
@@ -276,9 +285,8 @@ def _build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, do
         done = _ipc_pull_shards(plan, rank, d, cfg, flags, [(p, [(p * ml, ml)]) for p in
                                                              _peer_order(rank, d, cfg.ring)],
                                 lambda r0: arow(r0), k * ein)
-        for ev in done.values():
-            for e in ev:
-                plan.wait(S_MAIN, e)
+        for e in _unique(e for ev in done.values() for e in ev):
+            plan.wait(S_MAIN, e)
         gemm(S_MAIN, A, C, m)
         _wait(plan, S_MAIN, [flags.ref("ACK", p) for p in range(d) if p != rank], cfg)
     elif alg == "coll_pipeline" and be == "rccl" and cfg.fused:
@@ -344,8 +352,9 @@ def _build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, do
         jobs = [(p, [(p * ml + j * rows, rows) for j in range(cfg.s)]) for p in peers]
 
         def stage_gemm(j: int, done) -> None:  # right after chunk j of every peer is enqueued
-            for p in peers:
-                plan.wait(S_MAIN, done[p][j])
+            # (one event per block when one kernel / batch op moved every peer's chunk)
+            for e in _unique(done[p][j] for p in peers):
+                plan.wait(S_MAIN, e)
             gemm(S_MAIN, arow(j * rows), crow(j * rows), d * rows, a_grp=rows, a_gstride=ml,
                  c_grp=rows, c_gstride=ml)
 
