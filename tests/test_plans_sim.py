@@ -370,3 +370,17 @@ def test_cu_split_reserves_every_gemm(alg, fused, proto, backend):
     plan, _ = build_tp_columnwise(0, 2, 1024, 256, 64, DT_F32, DT_F32, cfg)
     g = [op for op in plan.ops if op.kind == OP_GEMM and op.stream == 0]
     assert g and all(op.args["reserve_cus"] >= 48 for op in g)
+
+
+@pytest.mark.parametrize("queues,first", [("4", True), ("1", False)])
+def test_rccl_fused_gemm_enqueued_first(monkeypatch, queues, first):
+    """The RCCL-fed gated GEMM goes ahead of its collectives (its own tiles start at once) when
+    the process has >= 2 hardware queues; with one in-order queue it stays last (its spinning
+    tiles would otherwise sit in front of the collectives that set their flags)."""
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", queues)
+    for alg in ("coll_pipeline", "p2p_pipeline"):
+        cfg = AlgoConfig(algorithm=alg, backend="rccl", fused=True, s=2)
+        plan, _ = build_tp_columnwise(0, 4, 64, 8, 8, DT_F32, DT_F32, cfg)
+        kinds = [op.kind for op in plan.ops]
+        assert (kinds[0] == OP_GEMM) == first and (kinds[-1] == OP_GEMM) == (not first)
+        _run_col(4, m=64, n=8, k=8, cfg=cfg, epochs=2)
