@@ -14,7 +14,7 @@ from __future__ import annotations
 import os
 from typing import Dict, List, Optional
 
-from ddlb_amd.parallel.plan import DT_SIZE, RCCL_OPS, Plan, Ref
+from ddlb_amd.parallel.plan import DT_SIZE, OP_GEMM, RCCL_OPS, Plan, Ref
 from ddlb_amd.parallel.sim import TORCH_DT
 
 
@@ -236,11 +236,35 @@ class BoundPlan:
         self.ex.load(words)
         if any(op.kind in RCCL_OPS for op in plan.ops):
             self.ex.set_comm(ctx.rccl())
+            if any(op.kind == OP_GEMM and op.args.get("flags") is not None for op in plan.ops):
+                self._warm_rccl()
         if plan.meta.get("comm_cus", 0):
             self.ex.set_cu_split(int(plan.meta["comm_cus"]))
         if trace or os.environ.get("DDLB_PLAN_TRACE", "0") == "1":
             self.ex.set_trace(True, plan.labels())
         torch.cuda.synchronize(dev)
+
+    def _warm_rccl(self) -> None:
+        """Run the plan's RCCL calls once, alone, before its first real run: RCCL sets up its
+        peer connections lazily inside the first collective of each kind, and a flag-gated GEMM
+        enqueued ahead of the collectives (the RCCL-fed fused pipelines) must never be on the
+        device while that setup runs (any device-wide synchronisation in it would wait for the
+        spinning tiles). Every rank binds the same plan, so every rank issues the same calls."""
+        import torch
+
+        from ddlb_amd.parallel.plan import OP_GROUP_END, OP_GROUP_START
+
+        warm = Plan(self.plan.rank, self.plan.world, nstreams=self.plan.nstreams,
+                    stream_priority=list(self.plan.stream_priority))
+        warm.ops = [op for op in self.plan.ops
+                    if op.kind in RCCL_OPS or op.kind in (OP_GROUP_START, OP_GROUP_END)]
+        ex = self.ctx.C.PlanExecutor(self.ctx.device_index, warm.nstreams, 1,
+                                     list(warm.stream_priority))
+        ex.load(warm.encode(self.resolve))
+        ex.set_comm(self.ctx.rccl())
+        ex.run(_raw_stream(self.ctx.device_index))
+        torch.cuda.synchronize()
+        del ex
 
     def resolve(self, ref: Ref) -> int:
         if ref.buf in self.sym:
