@@ -30,7 +30,8 @@ rendezvous port, a hard timeout). At N>1 a preflight (``ddlb_amd.parallel.prefli
 checks, in time-limited children, that RCCL and the IPC / xGMI mechanisms work across this
 node's GPUs; candidate families that fail are dropped, and a broken RCCL control plane makes
 the children coordinate over gloo instead. An autotuner then times each candidate (validated,
-MAX over ranks), RCCL candidates first, and the winner runs the timed measurement (falling back
+MAX over ranks) in the order of the one-GPU per-rank budget (``scripts/plan_budget.py``), and
+the winner runs the timed measurement (falling back
 to the next fastest if it fails there). The whole job runs against ONE wall-clock deadline
 (``--deadline-s``): tuning stops early enough to leave the final run its time, and every child's
 timeout is cut to what is left, so a node where candidates hang still reports inside it.
