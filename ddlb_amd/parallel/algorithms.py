@@ -814,10 +814,6 @@ def _build_tp_rowwise(rank: int, d: int, m: int, n: int, k: int, din: int, dout:
         srcs = _row_gather_sources(plan, rank, d, cfg, P + rank * blk, blk, peers, "RCV")
         plan.reduce(S_MAIN, OUT, srcs, ml * n, dout)
         _signal(plan, S_MAIN, [flags.ref("ACK", rank, owner=p) for p in peers], cfg)
-    elif alg == "coll_pipeline" and be == "rccl" and cfg.fused:
-        _col_rccl_fused_coll(plan, rank, d, m, n, k, ein, cfg, A, Bt, C, comm_dt, gdt)
-    elif alg == "p2p_pipeline" and be == "rccl" and cfg.fused:
-        _col_rccl_fused_p2p(plan, rank, d, m, n, k, ein, cfg, A, Bt, C, comm_dt, gdt)
     elif alg == "coll_pipeline" and be == "rccl":
         rows = ml // cfg.s
         for j in range(cfg.s):
