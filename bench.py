@@ -420,7 +420,9 @@ class Job:
                "--primitive", self.a.primitive, "-m", str(self.a.m), "-n", str(self.a.n),
                "-k", str(self.a.k), "--dtype", self.a.dtype,
                "--child-timeout", str(max(timeout, 1.0)), *extra]
-        proc = subprocess.Popen(cmd, env=env)
+        # the child reports through --child-out; its stdout (RCCL's version banner, library
+        # chatter) goes to stderr so the job's stdout holds the single JSON line only
+        proc = subprocess.Popen(cmd, env=env, stdout=sys.stderr.fileno())
         status = "exit"
         try:
             proc.wait(timeout=max(timeout, 1.0))
@@ -634,10 +636,21 @@ def self_launch(gpus: int, argv) -> int:
     env = dict(os.environ)
     env.setdefault("MASTER_ADDR", "127.0.0.1")
     proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
-    for line in proc.stdout:  # rank 0's JSON line (and anything else on stdout) passes through
-        sys.stdout.write(line)
-        sys.stdout.flush()
+    for line in proc.stdout:  # rank 0's JSON line to stdout, anything else to stderr
+        out = sys.stdout if line.startswith("{") else sys.stderr
+        out.write(line)
+        out.flush()
     return proc.wait()
+
+
+def json_stdout():
+    """Reserve this process's stdout for the single JSON line: returns a file on a duplicate of
+    fd 1 and points fd 1 at stderr, so whatever the libraries print to stdout (RCCL's version
+    banner at every communicator init) cannot interleave with it."""
+    sys.stdout.flush()
+    out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    return out
 
 
 def main(argv=None) -> int:
@@ -704,6 +717,7 @@ def main(argv=None) -> int:
     if a.gpus > 1 and world != a.gpus:
         sys.stderr.write(f"bench.py: --gpus {a.gpus} but the launcher started {world} ranks\n")
         return 2
+    out = json_stdout()
     job = Job(a)
     # warm the page cache for the children: the first `import torch` on a fresh box takes 1-2
     # minutes, which would otherwise land inside the first candidate's timeout (importing torch
@@ -723,7 +737,7 @@ def main(argv=None) -> int:
     pre = job.preflight(min(a.preflight_timeout, max(job.left() / 4, 10.0)))
     if a.preflight_only:
         if job.rank == 0:
-            print(json.dumps({"preflight": pre, "n_gpus": world}), flush=True)
+            print(json.dumps({"preflight": pre, "n_gpus": world}), file=out, flush=True)
         if job.pg is not None:
             job.pg.destroy_process_group()
         return 0 if all(str(v).startswith("ok") for v in pre.values()) else 1
@@ -789,7 +803,7 @@ def main(argv=None) -> int:
             "deadline_s": a.deadline_s, "job_wall_s": round(time.time() - job.t_start, 1),
             "autotune_ms": tune,
         }
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=out, flush=True)
     if job.pg is not None:
         job.pg.destroy_process_group()
     return 0 if final.get("valid") is not False else 1

@@ -30,6 +30,8 @@ def test_bench_world1_cpu():
                        capture_output=True, text=True, timeout=300, env=_env())
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json_line(r.stdout)
+    # stdout holds the JSON line only (children's and libraries' stdout goes to stderr)
+    assert [ln for ln in r.stdout.splitlines() if ln.strip()] == [r.stdout.strip()]
     for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
                 "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
         assert key in d
@@ -60,6 +62,7 @@ def test_bench_gpus2_without_launcher_cpu():
     d = _json_line(r.stdout)
     assert d["n_gpus"] == 2 and d["valid"] is True
     assert "without a launcher" in r.stderr
+    assert len([ln for ln in r.stdout.splitlines() if ln.strip()]) == 1
 
 
 def _prewarm_worker(rank, world, port, q):
