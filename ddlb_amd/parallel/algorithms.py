@@ -88,6 +88,10 @@ class AlgoConfig:
     # calls cost the host several us each); needs the GEMM and the comm stream on different
     # hardware queues (GPU_MAX_HW_QUEUES >= 2; the plan builder falls back otherwise)
     gemm_first: bool = True
+    # RCCL-fed fused GEMM: raise a stage's arrival flags from a third stream (True: the next
+    # collective never waits behind a signal kernel; the hand-off costs a cross-stream event) or
+    # from the comm stream right after the collective (False)
+    sig_side: bool = True
 
 
 @dataclass
@@ -425,8 +429,8 @@ def _col_rccl_fused_coll(plan, rank, d, m, n, k, ein, cfg, A, Bt, C, comm_dt, gd
     1024-tile persistent kernel).
 
     Stage j's ``ncclAllGather`` lands in a stage-major gather buffer G (block (j, p) = rank p's
-    stage-j rows at G row (j*d + p)*rows); a signal kernel on the comm stream then raises
-    ARRIVE[p*s + j] for every peer p. The GEMM reads A through a row-block address table
+    stage-j rows at G row (j*d + p)*rows); a signal kernel then raises
+    ARRIVE[p*s + j] for every peer p (from a third stream behind an event, ``sig_side``). The GEMM reads A through a row-block address table
     (logical block p*s + j = C rows p*m/d + j*rows: C keeps its canonical layout, no permutation)
     whose own blocks point at the rank's input shard itself, so the own tiles (dispatched first and
     never gated, tile_order 3: no signal op for them) run while stage 0 is still in flight. The
@@ -449,13 +453,15 @@ def _col_rccl_fused_coll(plan, rank, d, m, n, k, ein, cfg, A, Bt, C, comm_dt, gd
     first = _gemm_first(cfg)
     if first:
         plan.gemm(S_MAIN, A, Bt, C, **gemm)
-    s_sig = 2  # the signal kernels run on their own stream, off the collectives' critical path
+    # the signal kernels run on their own stream, off the collectives' critical path (sig_side)
+    s_sig = 2 if cfg.sig_side else S_COMM
     for j in range(s):
         plan.allgather(S_COMM, A + (rank * ml + j * rows) * k * ein, G + j * d * blk, rows * k,
                        comm_dt)
-        e = plan.event()
-        plan.record(S_COMM, e)
-        plan.wait(s_sig, e)
+        if cfg.sig_side:
+            e = plan.event()
+            plan.record(S_COMM, e)
+            plan.wait(s_sig, e)
         # a kernel (release at system scope after the collective's kernel): the gated tiles
         # acquire the rows RCCL wrote; a stream memop has no such fence
         for c in _chunks([flags.ref("ARRIVE", p * s + j) for p in range(d) if p != rank]):
@@ -478,16 +484,17 @@ def _col_rccl_fused_p2p(plan, rank, d, m, n, k, ein, cfg, A, Bt, C, comm_dt, gdt
     first = _gemm_first(cfg)
     if first:
         plan.gemm(S_MAIN, A, Bt, C, **gemm)
-    s_sig = 2  # signal kernels off the send / recv stream (see _col_rccl_fused_coll)
+    s_sig = 2 if cfg.sig_side else S_COMM  # (see _col_rccl_fused_coll)
     for j in range(1, d):
         to, frm = (rank - j) % d, (rank + j) % d
         plan.group_start(S_COMM)
         plan.send(S_COMM, A + rank * ml * k * ein, ml * k, comm_dt, to)
         plan.recv(S_COMM, A + frm * ml * k * ein, ml * k, comm_dt, frm)
         plan.group_end(S_COMM)
-        e = plan.event()
-        plan.record(S_COMM, e)
-        plan.wait(s_sig, e)
+        if cfg.sig_side:
+            e = plan.event()
+            plan.record(S_COMM, e)
+            plan.wait(s_sig, e)
         plan.signal(s_sig, [flags.ref("ARRIVE", frm)], method=SIG_KERNEL)
     if not first:
         plan.gemm(S_MAIN, A, Bt, C, **gemm)

@@ -131,7 +131,12 @@ def main(argv=None) -> int:
     ap.add_argument("--timeline", default="",
                     help="comma list of candidates whose last eager run is printed as a per-op "
                          "timeline (ddlb_amd.parallel.explain.format_timeline)")
+    ap.add_argument("--variants", default="",
+                    help="';'-separated AlgoConfig overrides measured per candidate beside the "
+                         "candidate itself, e.g. 'gemm_first=0;sig_side=0,gemm_first=0'")
     a = ap.parse_args(argv)
+
+    import dataclasses
 
     import torch
 
@@ -153,9 +158,20 @@ def main(argv=None) -> int:
           f"value)", flush=True)
     print(f"{'candidate':44s} {'gemm_ms':>8s} {'plan_ms':>8s} {'graph_ms':>8s} {'host_us':>8s} "
           f"{'ops':>5s} {'sig':>4s} {'copyMB':>7s} {'link_us':>8s}", flush=True)
+    todo = []
     for label, opts, cfg in candidate_cfgs(a.primitive, a.dtype, a.world):
         if want and label not in want:
             continue
+        todo.append((label, opts, cfg))
+        for var in [v.strip() for v in a.variants.split(";") if v.strip()]:
+            kw = {}
+            for item in var.split(","):
+                key, val = item.split("=")
+                cur = getattr(cfg, key.strip())
+                kw[key.strip()] = (type(cur)(int(val)) if isinstance(cur, (bool, int))
+                                   else type(cur)(val))
+            todo.append((f"{label}[{var}]", opts, dataclasses.replace(cfg, **kw)))
+    for label, opts, cfg in todo:
         row = {"candidate": label}
         try:
             plan, io = build(a.rank, a.world, a.m, a.n, a.k, din, dout, cfg)

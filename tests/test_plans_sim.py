@@ -7,9 +7,9 @@ import math
 import pytest
 import torch
 
-from ddlb_amd.parallel.algorithms import AlgoConfig, build_tp_columnwise, build_tp_rowwise
-from ddlb_amd.parallel.plan import (DT_BF16, DT_F32, OP_COPY, OP_COPY_MULTI, OP_GEMM, OP_SIGNAL,
-                                    SIG_KERNEL, SIG_STREAM)
+from ddlb_amd.parallel.algorithms import S_COMM, AlgoConfig, build_tp_columnwise, build_tp_rowwise
+from ddlb_amd.parallel.plan import (DT_BF16, DT_F32, OP_COPY, OP_COPY_MULTI, OP_GEMM, OP_RECORD,
+                                    OP_SIGNAL, OP_WAIT, SIG_KERNEL, SIG_STREAM)
 from ddlb_amd.parallel.sim import Simulator, make_buffers, read_tensor, write_tensor
 
 ALGS = ["default", "coll_pipeline", "p2p_pipeline"]
@@ -384,3 +384,14 @@ def test_rccl_fused_gemm_enqueued_first(monkeypatch, queues, first):
         kinds = [op.kind for op in plan.ops]
         assert (kinds[0] == OP_GEMM) == first and (kinds[-1] == OP_GEMM) == (not first)
         _run_col(4, m=64, n=8, k=8, cfg=cfg, epochs=2)
+
+
+@pytest.mark.parametrize("alg", ["coll_pipeline", "p2p_pipeline"])
+def test_rccl_fused_signal_on_comm_stream(alg):
+    """``sig_side=False``: the stage signal kernels follow their collective on the comm stream
+    (no event hand-off); the result and the race check are unchanged."""
+    cfg = AlgoConfig(algorithm=alg, backend="rccl", fused=True, s=2, sig_side=False)
+    _run_col(4, m=64, n=8, k=8, cfg=cfg, epochs=2)
+    plan, _ = build_tp_columnwise(0, 4, 64, 8, 8, DT_F32, DT_F32, cfg)
+    assert all(op.stream == S_COMM for op in plan.ops if op.kind == OP_SIGNAL)
+    assert not any(op.kind in (OP_RECORD, OP_WAIT) for op in plan.ops)
