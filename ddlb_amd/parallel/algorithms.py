@@ -88,10 +88,12 @@ class AlgoConfig:
     # calls cost the host several us each); needs the GEMM and the comm stream on different
     # hardware queues (GPU_MAX_HW_QUEUES >= 2; the plan builder falls back otherwise)
     gemm_first: bool = True
-    # RCCL-fed fused GEMM: raise a stage's arrival flags from a third stream (True: the next
-    # collective never waits behind a signal kernel; the hand-off costs a cross-stream event) or
-    # from the comm stream right after the collective (False)
-    sig_side: bool = True
+    # RCCL-fed fused GEMM: raise a stage's arrival flags from a third stream behind an event
+    # (True: the next collective never waits behind a signal kernel) or from the comm stream right
+    # after the collective (False, the default: the event hand-off cost more than the signal
+    # kernel in the queue, 0.19 vs 0.23 ms (s4) emulated at d = 8 with fast and with link-like
+    # slow collectives, profiles/r04/r4_12_ab_*)
+    sig_side: bool = False
 
 
 @dataclass
@@ -429,8 +431,9 @@ def _col_rccl_fused_coll(plan, rank, d, m, n, k, ein, cfg, A, Bt, C, comm_dt, gd
     1024-tile persistent kernel).
 
     Stage j's ``ncclAllGather`` lands in a stage-major gather buffer G (block (j, p) = rank p's
-    stage-j rows at G row (j*d + p)*rows); a signal kernel then raises
-    ARRIVE[p*s + j] for every peer p (from a third stream behind an event, ``sig_side``). The GEMM reads A through a row-block address table
+    stage-j rows at G row (j*d + p)*rows); a signal kernel then raises ARRIVE[p*s + j] for every
+    peer p (on the comm stream, or ``sig_side``: a third stream behind an event). The GEMM reads A
+    through a row-block address table
     (logical block p*s + j = C rows p*m/d + j*rows: C keeps its canonical layout, no permutation)
     whose own blocks point at the rank's input shard itself, so the own tiles (dispatched first and
     never gated, tile_order 3: no signal op for them) run while stage 0 is still in flight. The
@@ -453,7 +456,7 @@ def _col_rccl_fused_coll(plan, rank, d, m, n, k, ein, cfg, A, Bt, C, comm_dt, gd
     first = _gemm_first(cfg)
     if first:
         plan.gemm(S_MAIN, A, Bt, C, **gemm)
-    # the signal kernels run on their own stream, off the collectives' critical path (sig_side)
+    # the signal kernels run on the comm stream or, sig_side, on their own stream
     s_sig = 2 if cfg.sig_side else S_COMM
     for j in range(s):
         plan.allgather(S_COMM, A + (rank * ml + j * rows) * k * ein, G + j * d * blk, rows * k,

@@ -185,7 +185,7 @@ def test_rccl_fused_coll_plan(d, s):
     assert [t.buf for t in tab[rank * s:(rank + 1) * s]] == ["A_full"] * s
     assert all(t.buf == "G" for i, t in enumerate(tab) if i // s != rank)
     assert not plan.buffers["flags"].symmetric
-    sigs = [op for op in plan.ops if op.kind == OP_SIGNAL and op.stream == 2]
+    sigs = [op for op in plan.ops if op.kind == OP_SIGNAL and op.stream == S_COMM]
     assert all(op.args["method"] == SIG_KERNEL for op in sigs) and len(sigs) >= s
 
 
@@ -207,7 +207,7 @@ def test_rccl_fused_coll_negative_no_signal():
     built = [build_tp_columnwise(r, 2, 8, 8, 8, DT_F32, DT_F32, cfg) for r in range(2)]
     plans = [p for p, _ in built]
     for p in plans:
-        p.ops = [op for op in p.ops if not (op.kind == OP_SIGNAL and op.stream == 2)]
+        p.ops = [op for op in p.ops if op.kind != OP_SIGNAL]
     sim = Simulator(plans, make_buffers(plans))
     with pytest.raises(Deadlock):
         sim.run_epoch()
@@ -386,12 +386,14 @@ def test_rccl_fused_gemm_enqueued_first(monkeypatch, queues, first):
         _run_col(4, m=64, n=8, k=8, cfg=cfg, epochs=2)
 
 
+@pytest.mark.parametrize("side", [False, True])
 @pytest.mark.parametrize("alg", ["coll_pipeline", "p2p_pipeline"])
-def test_rccl_fused_signal_on_comm_stream(alg):
-    """``sig_side=False``: the stage signal kernels follow their collective on the comm stream
-    (no event hand-off); the result and the race check are unchanged."""
-    cfg = AlgoConfig(algorithm=alg, backend="rccl", fused=True, s=2, sig_side=False)
+def test_rccl_fused_signal_stream(alg, side):
+    """``sig_side=False`` (default): the stage signal kernels follow their collective on the comm
+    stream (no event hand-off); True: on a third stream behind one event per stage. Same result,
+    race-free either way."""
+    cfg = AlgoConfig(algorithm=alg, backend="rccl", fused=True, s=2, sig_side=side)
     _run_col(4, m=64, n=8, k=8, cfg=cfg, epochs=2)
     plan, _ = build_tp_columnwise(0, 4, 64, 8, 8, DT_F32, DT_F32, cfg)
-    assert all(op.stream == S_COMM for op in plan.ops if op.kind == OP_SIGNAL)
-    assert not any(op.kind in (OP_RECORD, OP_WAIT) for op in plan.ops)
+    assert all(op.stream == (2 if side else S_COMM) for op in plan.ops if op.kind == OP_SIGNAL)
+    assert any(op.kind in (OP_RECORD, OP_WAIT) for op in plan.ops) == side
