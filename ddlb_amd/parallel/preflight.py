@@ -59,9 +59,12 @@ PRIMITIVE_PHASES = {
     "ipc_agk": ("tp_columnwise", dict(algorithm="coll_pipeline", backend="ipc",
                                       multicast_protocol="kernel", fused=True, s=2,
                                       copy_blocks=16)),
-    "ipc_dstore": ("tp_rowwise", dict(algorithm="p2p_pipeline", backend="ipc", fused=True)),
+    "ipc_dstore": ("tp_rowwise", dict(algorithm="p2p_pipeline", backend="ipc", fused=True,
+                                      tile="pt4")),
+    # tile pt4 (ipc_dstore, rccl_fused): the kernel the bench's candidates run at their shapes
+    # (auto would pick the non-persistent t8 for these few tiles)
     "rccl_fused": ("tp_columnwise", dict(algorithm="coll_pipeline", backend="rccl", fused=True,
-                                         s=2)),
+                                         s=2, tile="pt4")),
 }
 PATTERN_BYTES = 1 << 20      # per rank and phase: 1 MiB (several xGMI packets, small enough)
 RS_COUNT = 4096              # f32 elements per rank of the reduce-scatter check
