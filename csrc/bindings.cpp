@@ -107,8 +107,6 @@ PYBIND11_MODULE(_C, m) {
           return gemm_fast_path_ok(g, din, dout);
         });
   m.def("choose_tile", &choose_tile);
-  m.def("set_pt4_stagger_ns", &set_pt4_stagger_ns);
-  m.def("pt4_stagger_ns", &pt4_stagger_ns);
   m.def("tile_rows", &tile_rows);
   m.def("tile_cols", &tile_cols);
 

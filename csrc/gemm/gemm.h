@@ -75,11 +75,6 @@ struct GemmArgs {
   // stored straight over xGMI by the GEMM epilogue). tile_order = 2 interleaves the shards.
   const uint64_t* c_table = nullptr;
   int64_t c_shard_rows = 0;
-  // Ungated pt4: every odd 8-workgroup group (one per XCD) sleeps this long before its first
-  // tile, so half the CUs run half a tile out of phase with the other half (their C-store bursts
-  // and A loads then overlap the others' MFMAs instead of all CUs hitting HBM at once). Set by
-  // launch_pt4 from set_pt4_stagger_ns(); 0 = off.
-  int stagger_ns = 0;
 };
 enum Act : int { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_SILU = 3 };
 // In-kernel all-gather variants (GemmArgs::ag_mode bits; 0 = write-through publication, 8 loads
@@ -97,8 +92,6 @@ enum AgMode : int {
 hipError_t gemm_launch(const GemmArgs& p, int din, int dout, int tile, int mode, hipStream_t s);
 bool gemm_fast_path_ok(const GemmArgs& p, int din, int dout);
 int choose_tile(int64_t M, int64_t N, int64_t K, int din);
-void set_pt4_stagger_ns(int ns);
-int pt4_stagger_ns();
 int tile_rows(int tile);
 int tile_cols(int tile);
 

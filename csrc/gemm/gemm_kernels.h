@@ -1042,13 +1042,6 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   }
   const int my_tiles = (bid < ntiles) ? (ntiles - 1 - bid) / nblk + 1 : 0;
   if (my_tiles == 0) return;
-  if constexpr (!GATED) {
-    if (p.stagger_ns > 0 && ((bid >> 3) & 1)) {  // (GemmArgs::stagger_ns; 100 MHz counter)
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      const uint64_t ticks = (uint64_t)(p.stagger_ns / 10);
-      while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(1);
-    }
-  }
 
   const int drow = lane >> 3, dpc = lane & 7;
   unsigned offA[2][2], offB[2][2];
@@ -1860,7 +1853,6 @@ hipError_t launch_pt4(const GemmArgs& p, hipStream_t s) {
   // split: the complement of the communication's CUs), so no workgroup waits for a free CU.
   if (p.reserve_cus > 0 && p.reserve_cus < grid) grid -= p.reserve_cus;
   GemmArgs q = p;
-  q.stagger_ns = pt4_stagger_ns();
   q.ag_ctas = p.flags != nullptr && p.ag_ctas > 0 ? (p.ag_ctas + 7) / 8 * 8 : 0;
   // The GEMM takes ceil(tiles / gemm_ctas) rounds of tiles; every copy workgroup that leaves that
   // count unchanged is free copy bandwidth (flagship: 1024 tiles, 224 GEMM CTAs = 5 rounds, so
@@ -1891,10 +1883,10 @@ hipError_t launch_pt4(const GemmArgs& p, hipStream_t s) {
                        dim3(512), 0, s, q);
   else if (apan && wt)
     hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false, 2, true>), dim3(grid), dim3(512), 0, s,
-                       q);
+                       p);
   else if (apan)
     hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false, 0, true>), dim3(grid), dim3(512), 0, s,
-                       q);
+                       p);
   else if (p.flags != nullptr && wt)
     hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, true, 2>), dim3(grid + q.ag_ctas), dim3(512),
                        0, s, q);
@@ -1902,11 +1894,11 @@ hipError_t launch_pt4(const GemmArgs& p, hipStream_t s) {
     hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, true>), dim3(grid + q.ag_ctas), dim3(512), 0,
                        s, q);
   else if (p.c_table != nullptr)
-    hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false, 1>), dim3(grid), dim3(512), 0, s, q);
+    hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false, 1>), dim3(grid), dim3(512), 0, s, p);
   else if (wt)
-    hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false, 2>), dim3(grid), dim3(512), 0, s, q);
+    hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false, 2>), dim3(grid), dim3(512), 0, s, p);
   else
-    hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false>), dim3(grid), dim3(512), 0, s, q);
+    hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false>), dim3(grid), dim3(512), 0, s, p);
   return hipGetLastError();
 }
 

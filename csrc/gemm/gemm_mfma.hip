@@ -57,10 +57,6 @@ bool gemm_fast_path_ok(const GemmArgs& p, int din, int dout) {
   return true;
 }
 
-static int g_pt4_stagger_ns = 0;
-void set_pt4_stagger_ns(int ns) { g_pt4_stagger_ns = ns < 0 ? 0 : ns; }
-int pt4_stagger_ns() { return g_pt4_stagger_ns; }
-
 int choose_tile(int64_t M, int64_t N, int64_t K, int din) {
   // Measured on MI355X: among the ping-pong kernels, pt4 (t4 made persistent) leads t4 / t8 / pt8
   // on every shape and dtype measured once the C stores are non-temporal
