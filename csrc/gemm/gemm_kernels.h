@@ -1860,7 +1860,8 @@ hipError_t launch_pt4(const GemmArgs& p, hipStream_t s) {
   if (q.ag_ctas > 0 && (p.ag_mode & AG_FILL_ROUNDS)) q.ag_ctas = ag_fill_ctas(grid, q.ag_ctas, tiles);
   grid -= q.ag_ctas;
   grid = (grid / 8) * 8;  // blockIdx % 8 == XCD group for every virtual tile id
-  if (p.flags != nullptr && q.ag_ctas == 0 && grid >= 8) {
+  static const bool no_shrink = getenv("DDLB_PT4_NO_SHRINK") != nullptr;  // A/B knob (host)
+  if (p.flags != nullptr && q.ag_ctas == 0 && grid >= 8 && !no_shrink) {
     // a gated GEMM fed by other kernels (RCCL, copy kernels, signal kernels): shrink the grid to
     // the fewest workgroups that keep its number of tile rounds, so every CU it does not need is
     // free for the producers (flagship with 32 reserved: 1024 tiles in 5 rounds on 208, not 224)
