@@ -1860,15 +1860,11 @@ hipError_t launch_pt4(const GemmArgs& p, hipStream_t s) {
   if (q.ag_ctas > 0 && (p.ag_mode & AG_FILL_ROUNDS)) q.ag_ctas = ag_fill_ctas(grid, q.ag_ctas, tiles);
   grid -= q.ag_ctas;
   grid = (grid / 8) * 8;  // blockIdx % 8 == XCD group for every virtual tile id
-  static const bool no_shrink = getenv("DDLB_PT4_NO_SHRINK") != nullptr;  // A/B knob (host)
-  if (p.flags != nullptr && q.ag_ctas == 0 && grid >= 8 && !no_shrink) {
-    // a gated GEMM fed by other kernels (RCCL, copy kernels, signal kernels): shrink the grid to
-    // the fewest workgroups that keep its number of tile rounds, so every CU it does not need is
-    // free for the producers (flagship with 32 reserved: 1024 tiles in 5 rounds on 208, not 224)
-    const int rounds = (tiles + grid - 1) / grid;
-    const int need = ((tiles + rounds - 1) / rounds + 7) / 8 * 8;
-    if (need < grid) grid = need;
-  }
+  // (A gated GEMM fed by other kernels keeps the whole num_cus - reserve_cus grid. Shrinking it
+  // to the fewest workgroups that keep its tile-round count looked free, but when the transfers
+  // are the bottleneck the last stage's tiles arrive at once and a smaller grid takes an extra
+  // round for them: RCCL-fed s4 plan 0.202 -> 0.181 ms emulated at d = 8 without the shrink,
+  // no plan slower, profiles/r04/r4_18_*.)
   if (grid > tiles) grid = tiles;
   if (grid < 1) grid = 1;
   // write-through stores address C from a per-tile scalar row (the tile's rows contiguous)
