@@ -167,6 +167,44 @@ def _finish(plan: Plan, cfg: AlgoConfig) -> None:
                 op.args["reserve_cus"] = max(op.args.get("reserve_cus", 0), cfg.comm_cus)
 
 
+def _split_k(plan: Plan, M: int, N: int, K: int, ein: int, cfg: AlgoConfig) -> int:
+    """K-slices for ONE full GEMM whose 256x256 grid would leave most of the 256 CUs idle
+    (e.g. 8192 x 1024 x 8192, BASELINE config #2: 128 tiles): S slices of K run as S persistent
+    GEMMs on S streams at once (S x tiles workgroups fill the chip), their partials summed by one
+    reduce op. Only for long K (each slice keeps >= 16 K-tiles: the fixed per-tile cost stays a
+    small share), auto tiles and no fused activation. 1 = no split."""
+    if cfg.tile != 0 or cfg.act or M % 256 or N % 256:
+        return 1
+    tiles = (M // 256) * (N // 256)
+    nk = K * ein // 128
+    for S in (4, 2):
+        if S <= plan.nstreams and tiles * S <= 256 and nk % (2 * S) == 0 and nk // S >= 16:
+            return S
+    return 1
+
+
+def _full_gemm(plan: Plan, a_ref: Ref, Bt: Ref, c_ref: Ref, M: int, N: int, K: int, ein: int,
+               eout: int, cfg: AlgoConfig, gdt: dict, tag: str = "KS") -> None:
+    """C[M, N] = A[M, K] Bt^T on stream 0 (after everything before it there), K-split when
+    :func:`_split_k` says so: slice s (K/S columns of A and Bt) -> partial s on stream s (slice 0
+    on stream 0), then a reduce op sums the partials into C on stream 0."""
+    S = _split_k(plan, M, N, K, ein, cfg)
+    if S == 1:
+        plan.gemm(S_MAIN, a_ref, Bt, c_ref, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, **gdt)
+        return
+    ks = K // S
+    part = plan.buffer(tag, S * M * N * eout)
+    g = dict(gdt, tile=TILE_PT4)
+    for j in range(1, S):
+        plan.edge(S_MAIN, j)
+    for j in range(S):
+        plan.gemm(j, a_ref + j * ks * ein, Bt + j * ks * ein, part + j * M * N * eout, M=M, N=N,
+                  K=ks, lda=K, ldb=K, ldc=N, **g)
+    for j in range(1, S):
+        plan.edge(j, S_MAIN)
+    plan.reduce(S_MAIN, c_ref, [part + j * M * N * eout for j in range(S)], M * N, gdt["dout"])
+
+
 def _unique(events):
     """Events in first-seen order without repeats (a wait per distinct event is enough)."""
     seen: List[int] = []
@@ -277,7 +315,7 @@ def _build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, do
         plan.gemm(stream, a_ref, Bt, c_ref, M=M, N=n, K=k, lda=k, ldb=k, ldc=n, **gdt, **kw)
 
     if d == 1:
-        gemm(S_MAIN, A, C, m)
+        _full_gemm(plan, A, Bt, C, m, n, k, ein, eout, cfg, gdt)
         return plan, io
 
     alg, be = cfg.algorithm, cfg.backend
@@ -286,14 +324,14 @@ def _build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, do
         return plan, io
     if alg == "default" and be == "rccl":
         plan.allgather(S_MAIN, arow(rank * ml), A, ml * k, comm_dt)
-        gemm(S_MAIN, A, C, m)
+        _full_gemm(plan, A, Bt, C, m, n, k, ein, eout, cfg, gdt)
     elif alg == "default" and be == "ipc":
         done = _ipc_pull_shards(plan, rank, d, cfg, flags, [(p, [(p * ml, ml)]) for p in
                                                              _peer_order(rank, d, cfg.ring)],
                                 lambda r0: arow(r0), k * ein)
         for e in _unique(e for ev in done.values() for e in ev):
             plan.wait(S_MAIN, e)
-        gemm(S_MAIN, A, C, m)
+        _full_gemm(plan, A, Bt, C, m, n, k, ein, eout, cfg, gdt)
         _wait(plan, S_MAIN, [flags.ref("ACK", p) for p in range(d) if p != rank], cfg)
     elif alg == "coll_pipeline" and be == "rccl" and cfg.fused:
         _col_rccl_fused_coll(plan, rank, d, m, n, k, ein, cfg, A, Bt, C, comm_dt, gdt)

@@ -768,6 +768,28 @@ def test_rccl_fused_plans_world1_native(comm, s):
         impl.close()
 
 
+@pytest.mark.parametrize("dtype,mode", [("bfloat16", "auto"), ("float8_e4m3fn", "mx")])
+def test_split_k_world1_native(comm, dtype, mode):
+    """BASELINE config #2's full GEMM (8192 x 1024 x 8192: 128 tiles of 256²) runs as two
+    K-slices on two streams (persistent kernel each) summed by the reduce op; validated by the
+    primitive (fp32 reference) and repeat-identical."""
+    from ddlb_amd.parallel.plan import OP_GEMM, OP_REDUCE
+    from ddlb_amd.primitives.tp_columnwise.native import NativeTPColumnwise
+
+    impl = NativeTPColumnwise(m=8192, n=1024, k=8192, dtype=dtype, gemm_mode=mode)
+    ops = impl.bound.plan.ops
+    assert sum(op.kind == OP_GEMM for op in ops) == 2 and sum(op.kind == OP_REDUCE for op in ops) == 1
+    out = impl.run()
+    torch.cuda.synchronize()
+    impl.validate(out)
+    first = out.clone()
+    for _ in range(5):
+        out = impl.run()
+    torch.cuda.synchronize()
+    assert torch.equal(out, first)
+    impl.close()
+
+
 @pytest.mark.parametrize("tile,mode", [(0, 0), (18, 0), (4, 0)])
 def test_direct_store_gemm_world1(comm, tile, mode):
     """Direct-store C (c_shards): row block q of one GEMM lands in its own buffer (the peers'

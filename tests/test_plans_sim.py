@@ -9,7 +9,7 @@ import torch
 
 from ddlb_amd.parallel.algorithms import S_COMM, AlgoConfig, build_tp_columnwise, build_tp_rowwise
 from ddlb_amd.parallel.plan import (DT_BF16, DT_F32, OP_COPY, OP_COPY_MULTI, OP_GEMM, OP_RECORD,
-                                    OP_SIGNAL, OP_WAIT, SIG_KERNEL, SIG_STREAM)
+                                    OP_REDUCE, OP_SIGNAL, OP_WAIT, SIG_KERNEL, SIG_STREAM)
 from ddlb_amd.parallel.sim import Simulator, make_buffers, read_tensor, write_tensor
 
 ALGS = ["default", "coll_pipeline", "p2p_pipeline"]
@@ -397,3 +397,31 @@ def test_rccl_fused_signal_stream(alg, side):
     plan, _ = build_tp_columnwise(0, 4, 64, 8, 8, DT_F32, DT_F32, cfg)
     assert all(op.stream == (2 if side else S_COMM) for op in plan.ops if op.kind == OP_SIGNAL)
     assert any(op.kind in (OP_RECORD, OP_WAIT) for op in plan.ops) == side
+
+
+@pytest.mark.parametrize("d,be", [(1, "rccl"), (2, "rccl"), (2, "ipc"), (4, "rccl"), (4, "ipc")])
+def test_split_k_full_gemm(d, be):
+    """A full GEMM whose 256x256 grid covers few CUs and whose K is long runs as S K-slices on S
+    streams (persistent kernel forced), summed by one reduce op; exact result, race-free."""
+    m, n, k = 256 * d, 256, 2048
+    cfg = AlgoConfig(algorithm="default", backend=be)
+    plan, _ = build_tp_columnwise(0, d, m, n, k, DT_F32, DT_F32, cfg)
+    g = [op for op in plan.ops if op.kind == OP_GEMM]
+    S = 4 if plan.nstreams >= 4 else 2
+    assert len(g) == S and {op.stream for op in g} == set(range(S))
+    assert all(op.args["K"] == k // S and op.args["lda"] == k and op.args["tile"] == 19 for op in g)
+    assert sum(op.kind == OP_REDUCE for op in plan.ops) == 1
+    _run_col(d, m, n, k, cfg, epochs=2)
+
+
+def test_split_k_not_for_full_machine_or_short_k():
+    """The flagship (1024 tiles), a short K, an explicit tile and a fused activation keep one
+    GEMM."""
+    for (m, n, k, kw) in [(65536, 1024, 1024, {}), (8192, 1024, 1024, {}),
+                          (8192, 1024, 8192, dict(tile=18)), (8192, 1024, 8192, dict(act=1))]:
+        cfg = AlgoConfig(algorithm="default", backend="rccl", **kw)
+        plan, _ = build_tp_columnwise(0, 1, m, n, k, DT_BF16, DT_BF16, cfg)
+        assert sum(op.kind == OP_GEMM for op in plan.ops) == 1, (m, n, k, kw)
+    plan, _ = build_tp_columnwise(0, 1, 8192, 1024, 8192, DT_BF16, DT_BF16,
+                                  AlgoConfig(algorithm="default", backend="rccl"))
+    assert sum(op.kind == OP_GEMM for op in plan.ops) == 2  # BASELINE config #2's full GEMM
