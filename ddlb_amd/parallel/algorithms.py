@@ -173,7 +173,8 @@ def _split_k(plan: Plan, M: int, N: int, K: int, ein: int, cfg: AlgoConfig) -> i
     GEMMs on S streams at once (S x tiles workgroups fill the chip), their partials summed by one
     reduce op. Only for long K (each slice keeps >= 16 K-tiles: the fixed per-tile cost stays a
     small share), auto tiles and no fused activation. 1 = no split."""
-    if cfg.tile != 0 or cfg.act or M % 256 or N % 256:
+    # (MX-fp8: the slices measured slower than one t4 launch, r4_20)
+    if cfg.tile != 0 or cfg.act or cfg.mode == 2 or M % 256 or N % 256:
         return 1
     tiles = (M // 256) * (N // 256)
     nk = K * ein // 128

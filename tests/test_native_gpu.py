@@ -768,7 +768,7 @@ def test_rccl_fused_plans_world1_native(comm, s):
         impl.close()
 
 
-@pytest.mark.parametrize("dtype,mode", [("bfloat16", "auto"), ("float8_e4m3fn", "mx")])
+@pytest.mark.parametrize("dtype,mode", [("bfloat16", "auto"), ("float8_e4m3fn", "auto")])
 def test_split_k_world1_native(comm, dtype, mode):
     """BASELINE config #2's full GEMM (8192 x 1024 x 8192: 128 tiles of 256²) runs as two
     K-slices on two streams (persistent kernel each) summed by the reduce op; validated by the

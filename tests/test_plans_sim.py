@@ -418,7 +418,8 @@ def test_split_k_not_for_full_machine_or_short_k():
     """The flagship (1024 tiles), a short K, an explicit tile and a fused activation keep one
     GEMM."""
     for (m, n, k, kw) in [(65536, 1024, 1024, {}), (8192, 1024, 1024, {}),
-                          (8192, 1024, 8192, dict(tile=18)), (8192, 1024, 8192, dict(act=1))]:
+                          (8192, 1024, 8192, dict(tile=18)), (8192, 1024, 8192, dict(act=1)),
+                          (8192, 1024, 8192, dict(mode=2))]:
         cfg = AlgoConfig(algorithm="default", backend="rccl", **kw)
         plan, _ = build_tp_columnwise(0, 1, m, n, k, DT_BF16, DT_BF16, cfg)
         assert sum(op.kind == OP_GEMM for op in plan.ops) == 1, (m, n, k, kw)
