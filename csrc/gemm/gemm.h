@@ -75,6 +75,11 @@ struct GemmArgs {
   // stored straight over xGMI by the GEMM epilogue). tile_order = 2 interleaves the shards.
   const uint64_t* c_table = nullptr;
   int64_t c_shard_rows = 0;
+  // K-split (optional): ksplit slices of K columns each (K is the SLICE length; lda / ldb the
+  // full rows); slice s reads A / B columns [s K, (s + 1) K) and writes its partial product at
+  // c + s * M * ldc elements (the caller sums the partials). pt4 runs every (slice, tile) in one
+  // launch; other kernels run the slices one after another.
+  int ksplit = 1;
 };
 enum Act : int { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_SILU = 3 };
 // In-kernel all-gather variants (GemmArgs::ag_mode bits; 0 = write-through publication, 8 loads

@@ -1001,7 +1001,11 @@ __global__ __launch_bounds__(512) void gemm_tn_t4_kernel(const GemmArgs p) {
 // 2 GiB: 32-bit offsets)
 // APAN: A panels through grouped rows or a row-block table (a separate instantiation: deriving
 // the panel base in the plain kernel cost it 6-16 more spilled SGPRs)
-template <class Mma, int OUT, bool GATED, int CMODE = 0, bool APAN = false>
+// KS: K-split (GemmArgs::ksplit slices, ungated, plain rows, CMODE 2): the virtual tiles are
+// (slice, tile) pairs, slice-major; slice s reads A / B columns [s K, (s + 1) K) (K = the slice's
+// length, lda / ldb the full rows) and stores its partial C at c + s * M * ldc (summed by the
+// caller): a few-tile long-K GEMM fills the chip in ONE launch
+template <class Mma, int OUT, bool GATED, int CMODE = 0, bool APAN = false, bool KS = false>
 __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   constexpr int ROWB = 128, UNIT = 128 * ROWB;
   constexpr int NS = 4 * Store8<OUT>::kStores;
@@ -1027,6 +1031,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   const int tiles_n = p.N / 256, ntiles = (p.M / 256) * tiles_n;
+  const int nvt = KS ? ntiles * p.ksplit : ntiles;  // virtual tiles
   const int esz = Mma::kElem;
   const int nk = p.K * esz / ROWB;  // even (pt4_ok)
   int bid = (int)blockIdx.x, nblk = (int)gridDim.x;
@@ -1040,7 +1045,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
       nblk -= p.ag_ctas;
     }
   }
-  const int my_tiles = (bid < ntiles) ? (ntiles - 1 - bid) / nblk + 1 : 0;
+  const int my_tiles = (bid < nvt) ? (nvt - 1 - bid) / nblk + 1 : 0;
   if (my_tiles == 0) return;
 
   const int drow = lane >> 3, dpc = lane & 7;
@@ -1076,8 +1081,16 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     return p.a_table != nullptr ? m0 : map_row(m0, p.a_grp, p.a_gstride);
   };
   const char* na = nullptr;  // APAN: the next tile's A panel
+  int64_t nko = 0;           // KS: the next tile's K-slice byte offset into the A / B rows
+  unsigned ncs = 0, ccs = 0;  // KS: the next / current tile's partial-C byte offset
   auto origin = [&](int ti, int64_t& m0, int64_t& n0) __attribute__((always_inline)) {
-    const int wg = tile_index_virtual<OWN>(p, bid + ti * nblk, ntiles);
+    int wg = tile_index_virtual<OWN>(p, bid + ti * nblk, nvt);
+    if constexpr (KS) {
+      const int ks = wg / ntiles;
+      wg -= ks * ntiles;
+      nko = (int64_t)ks * p.K * esz;
+      ncs = (unsigned)((int64_t)ks * p.M * p.ldc * OSZ);
+    }
     int tm_, tn_;
     tile_mn(p, wg, p.M / 256, tiles_n, tm_, tn_);
     m0 = (int64_t)tm_ * 256;
@@ -1098,10 +1111,11 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   auto uoff = [](int X, int buf, int q) constexpr { return X * 65536 + buf * 32768 + q * 16384; };
   auto stage = [&](int X, int q, int buf, Cur c) __attribute__((always_inline)) {
     if (c.ti != src_tile) {  // always the next tile (nm0, nn0)
-      rsA = __builtin_amdgcn_make_buffer_rsrc((void*)(APAN ? na : a_panel(nm0)), 0, 0x7FFFFFF0,
-                                              0x00020000);
-      rsB = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.b + nn0 * p.ldb * esz), 0,
-                                              0x7FFFFFF0, 0x00020000);
+      rsA = __builtin_amdgcn_make_buffer_rsrc((void*)((APAN ? na : a_panel(nm0)) + (KS ? nko : 0)),
+                                              0, 0x7FFFFFF0, 0x00020000);
+      rsB = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)((const char*)p.b + nn0 * p.ldb * esz + (KS ? nko : 0)), 0, 0x7FFFFFF0,
+          0x00020000);
       src_tile = c.ti;
     }
     const unsigned* off = X == 0 ? offA[q] : offB[q];
@@ -1196,7 +1210,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
       if constexpr (CMODE == 2) {
         // grouped C rows: a tile's 256 rows stay contiguous (launch_pt4: c_grp % 256 == 0)
         const int64_t prow = m0 + mq * 64 + f * 16;  // cm0: already the physical row
-        const unsigned soff = (unsigned)((prow * p.ldc + n0 + nq * 32) * OSZ);
+        const unsigned soff = (unsigned)((prow * p.ldc + n0 + nq * 32) * OSZ) + (KS ? ccs : 0u);
         store8_wt<OUT>(crc, c_lane, v0, v1, soff);
       } else {
         const int64_t row = m0 + wr * 128 + mq * 64 + f * 16 + frow;
@@ -1355,6 +1369,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   auto tile_body = [&](auto first_kind) __attribute__((always_inline)) {
     cm0 = nm0;  // this tile (C rows: physical, grouped C rows keep a tile contiguous)
     cn0 = nn0;
+    if constexpr (KS) ccs = ncs;
     if constexpr (CMODE == 2) cm0 = map_row(cm0, p.c_grp, p.c_gstride);
     if (ti + 1 < my_tiles) origin(ti + 1, nm0, nn0);
     iter(B0{}, first_kind);  // K-tile 0
@@ -1865,12 +1880,21 @@ hipError_t launch_pt4(const GemmArgs& p, hipStream_t s) {
   // are the bottleneck the last stage's tiles arrive at once and a smaller grid takes an extra
   // round for them: RCCL-fed s4 plan 0.202 -> 0.181 ms emulated at d = 8 without the shrink,
   // no plan slower, profiles/r04/r4_18_*.)
-  if (grid > tiles) grid = tiles;
+  const int vtiles = p.ksplit > 1 ? tiles * p.ksplit : tiles;  // (slice, tile) pairs
+  if (grid > vtiles) grid = vtiles;
   if (grid < 1) grid = 1;
   // write-through stores address C from a per-tile scalar row (the tile's rows contiguous)
   const bool wt = c_fits_wt(p, out_size<OUT>()) && p.c_grp % 256 == 0;
   // A through grouped rows / a row-block table: the APAN instantiations (no C row table with them)
   const bool apan = p.a_table != nullptr || p.a_grp != p.M;
+  if (p.ksplit > 1) {  // (gemm_launch routes only eligible K-splits here: plain rows, ungated)
+    if (p.flags != nullptr || apan || p.c_table != nullptr || p.c_grp != p.M || !wt ||
+        (int64_t)p.ksplit * p.M * p.ldc * out_size<OUT>() >= 0x7FFFFFF0LL)
+      return hipErrorNotSupported;
+    hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false, 2, false, true>), dim3(grid),
+                       dim3(512), 0, s, q);
+    return hipGetLastError();
+  }
   if (apan && p.c_table != nullptr) return hipErrorNotSupported;
   if (apan && p.flags != nullptr && wt)
     hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, true, 2, true>), dim3(grid + q.ag_ctas),
@@ -1922,6 +1946,7 @@ hipError_t launch_cfg(const GemmArgs& p, int tile, hipStream_t s) {
     case TILE_PT4:
       if (pt4_ok(p, Mma::kElem) && !(p.c_table && (p.a_table || p.a_grp != p.M)))
         return launch_pt4<Mma, OUT>(p, s);
+      if (p.ksplit > 1) return hipErrorNotSupported;  // only pt4 runs (slice, tile) pairs
       if (t8_ok(p)) return launch_t4<Mma, OUT>(p, s);
       return launch_tiled<Mma, OUT, 256, 256, 2, 4, true>(p, s);
     case TILE_T4:
@@ -1947,6 +1972,7 @@ hipError_t launch_mx_cfg(const GemmArgs& p, int tile, hipStream_t s) {
   // whole 256x256 tiles: the ping-pong schedules (persistent with >= 2 tiles per CU)
   if (tile == TILE_PT4 && pt4_ok(p, 1) && !(p.c_table && (p.a_table || p.a_grp != p.M)))
     return launch_pt4<MmaMX, OUT>(p, s);
+  if (p.ksplit > 1) return hipErrorNotSupported;  // only pt4 runs (slice, tile) pairs
   if ((tile == TILE_T4 || tile == TILE_PT4) && t8_ok(p)) return launch_t4<MmaMX, OUT>(p, s);
   if ((tile == TILE_T8 || tile == TILE_PT8 || tile == TILE_AUTO) && t8_ok(p)) {
     const int tiles = (p.M / 256) * (p.N / 256);

@@ -92,6 +92,33 @@ hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mo
     default: return hipErrorInvalidValue;
   }
   if (p.M == 0 || p.N == 0) return hipSuccess;
+  if (p.ksplit > 1) {
+    // K-split: slice j of K columns -> partial j at c + j * M * ldc (the caller sums them). pt4
+    // runs every (slice, tile) pair in one launch; any other kernel runs the slices one by one.
+    if (p.flags != nullptr || p.a_table != nullptr || p.c_table != nullptr || p.ag_ctas > 0 ||
+        p.ag_mode != 0 || p.act != ACT_NONE || p.a_grp != p.M || p.c_grp != p.M || p.ksplit > 64)
+      return hipErrorNotSupported;
+    if (tile == TILE_AUTO || tile == TILE_PT4) {
+      GemmArgs q = p;
+      q.tile_order = 0;
+      const bool fast = mode != GEMM_MODE_GENERIC && gemm_fast_path_ok(q, din, dout);
+      hipError_t e = hipErrorNotSupported;
+      if (fast && din == DT_FP8 && mode == GEMM_MODE_MX) e = launch_fast_mx(q, dout, TILE_PT4, s);
+      else if (fast) e = launch_fast(q, din, dout, TILE_PT4, s);
+      if (e != hipErrorNotSupported && e != hipErrorInvalidValue) return e;
+    }
+    const int esz = dtype_size(din), osz = dtype_size(dout);
+    for (int j = 0; j < p.ksplit; ++j) {
+      GemmArgs q = p;
+      q.ksplit = 1;
+      q.a = (const char*)p.a + (int64_t)j * p.K * esz;
+      q.b = (const char*)p.b + (int64_t)j * p.K * esz;
+      q.c = (char*)p.c + (int64_t)j * p.M * p.ldc * osz;
+      const hipError_t e = gemm_launch(q, din, dout, tile == TILE_PT4 ? TILE_AUTO : tile, mode, s);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
   if (p.a_table != nullptr) {
     // A through a row-block address table (direct access to the peers' shards, or the blocks of
     // a stage-major gather buffer): the ping-pong kernels (pt4 / t4 / t8 / pt8, whole 256-row

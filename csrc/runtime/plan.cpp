@@ -555,6 +555,7 @@ GemmArgs PlanExecutor::gemm_args(const int64_t* o) const {
   g.shard_rows = o[26];
   g.c_table = (const uint64_t*)o[32];
   g.c_shard_rows = o[33];
+  g.ksplit = o[31] > 1 ? (int)o[31] : 1;
   g.timeout_word = d_timeout_;
   g.epoch_ptr = graph_on_ ? d_epoch_ : nullptr;
   return g;

@@ -29,7 +29,7 @@ enum OpKind : int64_t {
                       // 23 tile_order, 24 fused epilogue activation, 25 A shard table,
                       // 26 A shard rows, 27 nsub, 28 reserve_cus, 29 in-kernel all-gather
                       // (ctas | parts << 20 | rank << 40 | mode << 56), 30 its table,
-                      // 32 C shard table (direct store), 33 C shard rows
+                      // 31 K-split slices, 32 C shard table (direct store), 33 C shard rows
   OP_RECORD = 2,      // 2 event
   OP_WAIT = 3,        // 2 event
   OP_ALLGATHER = 4,   // 2 send, 3 recv, 4 count per rank, 5 dtype

@@ -168,41 +168,34 @@ def _finish(plan: Plan, cfg: AlgoConfig) -> None:
 
 
 def _split_k(plan: Plan, M: int, N: int, K: int, ein: int, cfg: AlgoConfig) -> int:
-    """K-slices for ONE full GEMM whose 256x256 grid would leave most of the 256 CUs idle
-    (e.g. 8192 x 1024 x 8192, BASELINE config #2: 128 tiles): S slices of K run as S persistent
-    GEMMs on S streams at once (S x tiles workgroups fill the chip), their partials summed by one
-    reduce op. Only for long K (each slice keeps >= 16 K-tiles: the fixed per-tile cost stays a
-    small share), auto tiles and no fused activation. 1 = no split."""
-    # (MX-fp8: the slices measured slower than one t4 launch, r4_20)
-    if cfg.tile != 0 or cfg.act or cfg.mode == 2 or M % 256 or N % 256:
+    """K-slices for ONE full GEMM whose 256x256 grid would leave most of the 256 CUs idle (e.g.
+    8192 x 1024 x 8192, BASELINE config #2: 128 tiles): the persistent kernel runs every (slice,
+    tile) pair in one launch (GemmArgs::ksplit) and a reduce op sums the partials. Only for long K
+    (each slice keeps >= 16 K-tiles, so the fixed per-tile cost stays a small share), auto tiles
+    and no fused activation. 1 = no split."""
+    if cfg.tile != 0 or cfg.act or M % 256 or N % 256:
         return 1
     tiles = (M // 256) * (N // 256)
     nk = K * ein // 128
     for S in (4, 2):
-        if S <= plan.nstreams and tiles * S <= 256 and nk % (2 * S) == 0 and nk // S >= 16:
+        if tiles * S <= 256 and nk % (2 * S) == 0 and nk // S >= 16:
             return S
     return 1
 
 
 def _full_gemm(plan: Plan, a_ref: Ref, Bt: Ref, c_ref: Ref, M: int, N: int, K: int, ein: int,
                eout: int, cfg: AlgoConfig, gdt: dict, tag: str = "KS") -> None:
-    """C[M, N] = A[M, K] Bt^T on stream 0 (after everything before it there), K-split when
-    :func:`_split_k` says so: slice s (K/S columns of A and Bt) -> partial s on stream s (slice 0
-    on stream 0), then a reduce op sums the partials into C on stream 0."""
+    """C[M, N] = A[M, K] Bt^T on stream 0, K-split when :func:`_split_k` says so: ONE launch
+    writes the S partials (slice s = K/S columns of A and Bt) to a scratch buffer, then a reduce
+    op sums them into C (the partials in the output dtype, summed in f32: the rowwise
+    reduce-scatter's rule)."""
     S = _split_k(plan, M, N, K, ein, cfg)
     if S == 1:
         plan.gemm(S_MAIN, a_ref, Bt, c_ref, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, **gdt)
         return
-    ks = K // S
     part = plan.buffer(tag, S * M * N * eout)
-    g = dict(gdt, tile=TILE_PT4)
-    for j in range(1, S):
-        plan.edge(S_MAIN, j)
-    for j in range(S):
-        plan.gemm(j, a_ref + j * ks * ein, Bt + j * ks * ein, part + j * M * N * eout, M=M, N=N,
-                  K=ks, lda=K, ldb=K, ldc=N, **g)
-    for j in range(1, S):
-        plan.edge(j, S_MAIN)
+    plan.gemm(S_MAIN, a_ref, Bt, part, M=M, N=N, K=K // S, lda=K, ldb=K, ldc=N, ksplit=S,
+              **dict(gdt, tile=TILE_PT4))
     plan.reduce(S_MAIN, c_ref, [part + j * M * N * eout for j in range(S)], M * N, gdt["dout"])
 
 

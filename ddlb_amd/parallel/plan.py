@@ -126,7 +126,8 @@ class Plan:
              first_shard: int = 0, tile_order: int = 0, act: int = 0,
              a_shards: Optional[Sequence[Ref]] = None, shard_rows: int = 0,
              nsub: int = 1, reserve_cus: int = 0, ag: Optional[dict] = None,
-             c_shards: Optional[Sequence[Ref]] = None, c_shard_rows: int = 0) -> Op:
+             c_shards: Optional[Sequence[Ref]] = None, c_shard_rows: int = 0,
+             ksplit: int = 1) -> Op:
         """``a_shards``: A row block s (``shard_rows`` rows each) is read from ``a_shards[s]``
         (a peer's copy for a direct-access GEMM that pulls its operand over xGMI).
         ``flags`` (arrival-gated tiles): shard ``i`` = rows ``[i*flag_rows, (i+1)*flag_rows)`` may
@@ -142,7 +143,14 @@ class Plan:
         ``c_shards`` (direct-store C): C row block s (``c_shard_rows`` rows) is written at
         ``c_shards[s]`` — e.g. the peers' receive slots, so the epilogue stores a reduce-scatter's
         partials straight over xGMI; ``tile_order=2`` interleaves the blocks (every destination's
-        tiles in flight at once)."""
+        tiles in flight at once). ``ksplit`` > 1: K-split, ``K`` is the slice length (``lda`` /
+        ``ldb`` the full rows); slice s reads A / B columns ``[s K, (s + 1) K)`` and writes its
+        partial product at ``c + s * M * ldc`` elements (plain rows only; the caller sums them)."""
+        if ksplit < 1 or (ksplit > 1 and (flags is not None or a_shards is not None or
+                                          c_shards is not None or ag is not None or act or
+                                          a_grp not in (0, M) or c_grp not in (0, M))):
+            raise ValueError("ksplit > 1 takes plain rows only (no flags, tables, all-gather, "
+                             "activation or grouped rows)")
         if nsub < 1 or nshards % nsub:
             raise ValueError(f"nsub ({nsub}) must divide nshards ({nshards})")
         if ag is not None:
@@ -181,7 +189,7 @@ class Plan:
                          shard_rows=shard_rows, a_table=a_table, nsub=nsub,
                          reserve_cus=reserve_cus, ag=ag,
                          c_shards=list(c_shards) if c_shards is not None else None,
-                         c_shard_rows=c_shard_rows, c_table=c_table)
+                         c_shard_rows=c_shard_rows, c_table=c_table, ksplit=ksplit)
 
     def table(self, name: str, refs: Sequence[Ref]) -> Ref:
         """Device array of 64-bit addresses of ``refs`` (written once when the plan is bound)."""
@@ -284,6 +292,7 @@ class Plan:
                     w[30] = resolve(g["table"])
                 if a.get("c_table") is not None:
                     w[32], w[33] = resolve(a["c_table"]), a["c_shard_rows"]
+                w[31] = a.get("ksplit", 1)
             elif k in (OP_RECORD, OP_WAIT):
                 w[2] = a["event"]
             elif k in (OP_ALLGATHER, OP_REDUCE_SCATTER):

@@ -178,6 +178,14 @@ class Simulator:
         what = f"r{r}.s{op.stream}.{OP_NAMES[k]}"
         if k == OP_GEMM and a.get("ag") is not None:
             self._exec_ag(r, op, vc, what)
+        if k == OP_GEMM and a.get("ksplit", 1) > 1:
+            # K-split: slice s = A / B columns [s K, (s + 1) K) -> partial s at c + s * M * ldc
+            ein, eout = DT_SIZE[a["din"]], DT_SIZE[a["dout"]]
+            for sl in range(a["ksplit"]):
+                sub = dict(a, ksplit=1, a=a["a"] + sl * a["K"] * ein, b=a["b"] + sl * a["K"] * ein,
+                           c=a["c"] + sl * a["M"] * a["ldc"] * eout)
+                self._exec_local(r, type(op)(k, op.stream, sub), vc)
+            return
         if k == OP_GEMM:
             ein, eout = DT_SIZE[a["din"]], DT_SIZE[a["dout"]]
             shards = a.get("a_shards")

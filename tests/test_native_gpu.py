@@ -768,17 +768,65 @@ def test_rccl_fused_plans_world1_native(comm, s):
         impl.close()
 
 
-@pytest.mark.parametrize("dtype,mode", [("bfloat16", "auto"), ("float8_e4m3fn", "auto")])
+@pytest.mark.parametrize("S", [2, 4])
+@pytest.mark.parametrize("tile,dt,mode", [(0, "bf16", 0), (19, "bf16", 0), (18, "bf16", 0),
+                                          (0, "fp8", 2), (0, "fp8", 0)])
+def test_ksplit_gemm_partials(comm, S, tile, dt, mode):
+    """GemmArgs::ksplit: slice s of K (columns [s K, (s + 1) K) of A and Bt) lands at
+    c + s * M * ldc. pt4 (auto / 19) runs every (slice, tile) pair in one launch; t4 (18) runs
+    the slices one by one. Each partial against its fp32 slice product (tight bound), and the
+    launch repeat-identical."""
+    from ddlb_amd.parallel.context import NativeContext
+    from ddlb_amd.parallel.plan import DT_BF16, DT_FP8, Plan
+
+    din = DT_FP8 if dt == "fp8" else DT_BF16
+    tdt = torch.float8_e4m3fn if dt == "fp8" else torch.bfloat16
+    es = 1 if dt == "fp8" else 2
+    M, N, K = 1024, 512, 4096
+    ks = K // S
+    plan = Plan(0, 1, nstreams=1, stream_priority=[0])
+    a = plan.buffer("a", M * K * es)
+    b = plan.buffer("b", N * K * es)
+    c = plan.buffer("c", S * M * N * 2)
+    plan.gemm(0, a, b, c, M=M, N=N, K=ks, lda=K, ldb=K, ldc=N, din=din, dout=DT_BF16, tile=tile,
+              mode=mode, ksplit=S)
+    ctx = NativeContext(comm)
+    bound = ctx.bind(plan)
+    A = (torch.rand(M, K, device="cuda") * 2 - 1).to(tdt)
+    W = (torch.rand(N, K, device="cuda") * 2 - 1).to(tdt)
+    bound.buffer("a").view(tdt).view(M, K).copy_(A)
+    bound.buffer("b").view(tdt).view(N, K).copy_(W)
+    out = bound.buffer("c").view(torch.bfloat16).view(S, M, N)
+    out.fill_(float("nan"))
+    bound.run()
+    torch.cuda.synchronize()
+    first = out.clone()
+    for j in range(S):
+        ref = A[:, j * ks:(j + 1) * ks].float() @ W[:, j * ks:(j + 1) * ks].float().T
+        err = float((first[j].float() - ref).abs().max())
+        assert err <= _tight(ref, ks), (j, err)
+    for _ in range(5):
+        bound.run()
+    torch.cuda.synchronize()
+    assert torch.equal(out, first)
+    bound.close()
+    ctx.close()
+
+
+@pytest.mark.parametrize("dtype,mode", [("bfloat16", "auto"), ("float8_e4m3fn", "auto"),
+                                        ("float8_e4m3fn", "mx")])
 def test_split_k_world1_native(comm, dtype, mode):
-    """BASELINE config #2's full GEMM (8192 x 1024 x 8192: 128 tiles of 256²) runs as two
-    K-slices on two streams (persistent kernel each) summed by the reduce op; validated by the
-    primitive (fp32 reference) and repeat-identical."""
+    """BASELINE config #2's full GEMM (8192 x 1024 x 8192: 128 tiles of 256²) runs K-split: ONE
+    pt4 launch over (slice, tile) pairs writing two partials, summed by the reduce op; validated
+    by the primitive (fp32 reference) and repeat-identical."""
     from ddlb_amd.parallel.plan import OP_GEMM, OP_REDUCE
     from ddlb_amd.primitives.tp_columnwise.native import NativeTPColumnwise
 
     impl = NativeTPColumnwise(m=8192, n=1024, k=8192, dtype=dtype, gemm_mode=mode)
     ops = impl.bound.plan.ops
-    assert sum(op.kind == OP_GEMM for op in ops) == 2 and sum(op.kind == OP_REDUCE for op in ops) == 1
+    g = [op for op in ops if op.kind == OP_GEMM]
+    assert len(g) == 1 and g[0].args["ksplit"] == 2
+    assert sum(op.kind == OP_REDUCE for op in ops) == 1
     out = impl.run()
     torch.cuda.synchronize()
     impl.validate(out)

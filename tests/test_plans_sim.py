@@ -401,28 +401,42 @@ def test_rccl_fused_signal_stream(alg, side):
 
 @pytest.mark.parametrize("d,be", [(1, "rccl"), (2, "rccl"), (2, "ipc"), (4, "rccl"), (4, "ipc")])
 def test_split_k_full_gemm(d, be):
-    """A full GEMM whose 256x256 grid covers few CUs and whose K is long runs as S K-slices on S
-    streams (persistent kernel forced), summed by one reduce op; exact result, race-free."""
+    """A full GEMM whose 256x256 grid covers few CUs and whose K is long runs K-split: ONE
+    persistent launch over (slice, tile) pairs writing S partials, summed by one reduce op;
+    exact result, race-free."""
     m, n, k = 256 * d, 256, 2048
     cfg = AlgoConfig(algorithm="default", backend=be)
     plan, _ = build_tp_columnwise(0, d, m, n, k, DT_F32, DT_F32, cfg)
     g = [op for op in plan.ops if op.kind == OP_GEMM]
-    S = 4 if plan.nstreams >= 4 else 2
-    assert len(g) == S and {op.stream for op in g} == set(range(S))
-    assert all(op.args["K"] == k // S and op.args["lda"] == k and op.args["tile"] == 19 for op in g)
+    assert len(g) == 1 and g[0].stream == 0 and g[0].args["ksplit"] == 4
+    assert g[0].args["K"] == k // 4 and g[0].args["lda"] == k and g[0].args["tile"] == 19
     assert sum(op.kind == OP_REDUCE for op in plan.ops) == 1
     _run_col(d, m, n, k, cfg, epochs=2)
 
 
 def test_split_k_not_for_full_machine_or_short_k():
     """The flagship (1024 tiles), a short K, an explicit tile and a fused activation keep one
-    GEMM."""
+    unsplit GEMM; BASELINE config #2's full GEMM (128 tiles, K = 8192) splits in two."""
     for (m, n, k, kw) in [(65536, 1024, 1024, {}), (8192, 1024, 1024, {}),
-                          (8192, 1024, 8192, dict(tile=18)), (8192, 1024, 8192, dict(act=1)),
-                          (8192, 1024, 8192, dict(mode=2))]:
+                          (8192, 1024, 8192, dict(tile=18)), (8192, 1024, 8192, dict(act=1))]:
         cfg = AlgoConfig(algorithm="default", backend="rccl", **kw)
         plan, _ = build_tp_columnwise(0, 1, m, n, k, DT_BF16, DT_BF16, cfg)
-        assert sum(op.kind == OP_GEMM for op in plan.ops) == 1, (m, n, k, kw)
+        g = [op for op in plan.ops if op.kind == OP_GEMM]
+        assert len(g) == 1 and g[0].args["ksplit"] == 1, (m, n, k, kw)
     plan, _ = build_tp_columnwise(0, 1, 8192, 1024, 8192, DT_BF16, DT_BF16,
                                   AlgoConfig(algorithm="default", backend="rccl"))
-    assert sum(op.kind == OP_GEMM for op in plan.ops) == 2  # BASELINE config #2's full GEMM
+    g = [op for op in plan.ops if op.kind == OP_GEMM]
+    assert len(g) == 1 and g[0].args["ksplit"] == 2
+
+
+def test_ksplit_rejects_tables_and_flags():
+    from ddlb_amd.parallel.plan import Plan, Ref
+
+    plan = Plan(0, 1)
+    a = plan.buffer("a", 1 << 20)
+    with pytest.raises(ValueError):
+        plan.gemm(0, a, a, a, M=256, N=256, K=256, lda=512, ldb=512, ldc=256, din=DT_F32,
+                  dout=DT_F32, ksplit=2, flags=Ref("a", 0))
+    with pytest.raises(ValueError):
+        plan.gemm(0, a, a, a, M=256, N=256, K=256, lda=512, ldb=512, ldc=256, din=DT_F32,
+                  dout=DT_F32, ksplit=2, a_grp=128, a_gstride=256)
