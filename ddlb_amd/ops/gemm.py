@@ -84,11 +84,31 @@ def _phys_rows(M: int, grp: int, gstride: int, base_rows: int = 0) -> int:
     return (last // grp) * gstride + (last % grp) + 1
 
 
+def split_k_factor(M: int, N: int, K: int, esz: int, ncu: int = 256) -> int:
+    """K-slices for a GEMM whose 256x256 grid covers at most half the CUs and whose K is long
+    (e.g. 8192 x 1024 x 8192: 128 tiles): ``S`` slices run as (slice, tile) pairs of ONE pt4
+    launch (``GemmArgs::ksplit``) and their partials are summed by one reduce kernel. Each slice
+    keeps >= 16 K-tiles (the fixed per-tile cost stays small, profiles/r04/r4_15_*); measured
+    on the config #2 shape: 0.1009 ms vs 0.1338 unsplit (profiles/r04/r4_22_*). 1 = no split."""
+    if M % 256 or N % 256 or M <= 0 or N <= 0:
+        return 1
+    tiles = (M // 256) * (N // 256)
+    nk = K * esz // 128
+    if K * esz % 128:
+        return 1
+    for S in (4, 2):
+        if tiles * S <= ncu and nk % (2 * S) == 0 and nk // S >= 16:
+            return S
+    return 1
+
+
 def gemm(a, w, out=None, *, out_dtype=None, tile: str = "auto", mode: str = "auto",
          M: Optional[int] = None, a_grp: int = 0, a_gstride: int = 0, c_grp: int = 0,
-         c_gstride: int = 0, stream=None, act: str = "none"):
+         c_gstride: int = 0, stream=None, act: str = "none", ksplit: int = 0):
     """``out[:M] = act(a[:M] @ w.T)`` on the current HIP stream (grouped-row addressing and a
-    fused epilogue activation — none / gelu (tanh) / relu / silu — optional)."""
+    fused epilogue activation — none / gelu (tanh) / relu / silu — optional). ``ksplit``: 0 =
+    auto (:func:`split_k_factor` for plain-row auto-tile GEMMs with no activation and a dense
+    output), 1 = never, S > 1 = S slices."""
     import torch
 
     C = load()
@@ -110,6 +130,23 @@ def gemm(a, w, out=None, *, out_dtype=None, tile: str = "auto", mode: str = "aut
     if M >= 2 ** 31 or N >= 2 ** 31 or K >= 2 ** 31:
         raise ValueError("dimensions must fit in 32 bits")
     s = stream if stream is not None else torch.cuda.current_stream(a.device).cuda_stream
+    plain = (a_grp in (0, M) and c_grp in (0, M) and ACTS[act] == 0 and out.stride(0) == N
+             and mode != "generic" and a.dtype != torch.float64)
+    S = int(ksplit)
+    if S == 0:
+        S = split_k_factor(M, N, K, a.element_size()) if plain and tile == "auto" else 1
+    if S > 1:
+        if not plain or K % S:
+            raise ValueError("ksplit needs plain rows, no activation, a dense output and S | K")
+        part = torch.empty((S, M, N), dtype=out.dtype, device=a.device)
+        C.gemm(a.data_ptr(), w.data_ptr(), part.data_ptr(), a.stride(0), w.stride(0), N, M, N,
+               K // S, dtype_code(a.dtype), dtype_code(out.dtype),
+               TILES["pt4" if tile == "auto" else tile], MODES[mode], 0, 0, 0, 0, s, 0, S)
+        C.reduce_sum(out.data_ptr(), [part[j].data_ptr() for j in range(S)], M * N,
+                     dtype_code(out.dtype), s)
+        if stream is not None:  # the workspace stays allocated until that stream reaches it
+            part.record_stream(torch.cuda.ExternalStream(s))
+        return out
     C.gemm(a.data_ptr(), w.data_ptr(), out.data_ptr(), a.stride(0), w.stride(0), out.stride(0),
            M, N, K, dtype_code(a.dtype), dtype_code(out.dtype), TILES[tile], MODES[mode],
            a_grp, a_gstride, c_grp, c_gstride, s, ACTS[act])

@@ -169,18 +169,14 @@ def _finish(plan: Plan, cfg: AlgoConfig) -> None:
 
 def _split_k(plan: Plan, M: int, N: int, K: int, ein: int, cfg: AlgoConfig) -> int:
     """K-slices for ONE full GEMM whose 256x256 grid would leave most of the 256 CUs idle (e.g.
-    8192 x 1024 x 8192, BASELINE config #2: 128 tiles): the persistent kernel runs every (slice,
-    tile) pair in one launch (GemmArgs::ksplit) and a reduce op sums the partials. Only for long K
-    (each slice keeps >= 16 K-tiles, so the fixed per-tile cost stays a small share), auto tiles
-    and no fused activation. 1 = no split."""
-    if cfg.tile != 0 or cfg.act or M % 256 or N % 256:
+    8192 x 1024 x 8192, BASELINE config #2: 128 tiles; ``ops.gemm.split_k_factor``): the
+    persistent kernel runs every (slice, tile) pair in one launch (GemmArgs::ksplit) and a
+    reduce op sums the partials. Auto tiles and no fused activation only. 1 = no split."""
+    from ddlb_amd.ops.gemm import split_k_factor
+
+    if cfg.tile != 0 or cfg.act:
         return 1
-    tiles = (M // 256) * (N // 256)
-    nk = K * ein // 128
-    for S in (4, 2):
-        if tiles * S <= 256 and nk % (2 * S) == 0 and nk // S >= 16:
-            return S
-    return 1
+    return split_k_factor(M, N, K, ein)
 
 
 def _full_gemm(plan: Plan, a_ref: Ref, Bt: Ref, c_ref: Ref, M: int, N: int, K: int, ein: int,

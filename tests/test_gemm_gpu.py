@@ -432,3 +432,31 @@ def test_pt4_grouped_a_rows(dt, grp, cgrp, gen):
         gemm(A, w, C, **kw)
     torch.cuda.synchronize()
     assert torch.equal(C, first)
+
+
+@pytest.mark.parametrize("ksplit", [0, 2, 4])
+@pytest.mark.parametrize("dt", [(torch.bfloat16, "auto"), (torch.float16, "auto"),
+                                (torch.float8_e4m3fn, "mx"), (torch.float8_e4m3fn, "auto")],
+                         ids=lambda d: f"{str(d[0])[6:]}-{d[1]}")
+def test_gemm_ksplit(dt, ksplit, gen):
+    """K-split through ops.gemm (0 = the automatic rule, 4 slices for 2048 x 1024 x 8192's 32
+    tiles; 2 / 4 explicit): one pt4 launch over (slice, tile) pairs + one reduce kernel, the
+    tight bound at K = 8192 and repeat-identical."""
+    from ddlb_amd.ops.gemm import gemm, split_k_factor
+
+    dtype, mode = dt
+    M, N, K = 2048, 1024, 8192
+    assert split_k_factor(M, N, K, torch.tensor([], dtype=dtype).element_size()) == 4
+    a, w = _rand((M, K), dtype, gen), _rand((N, K), dtype, gen)
+    odt = torch.bfloat16 if dtype == torch.float8_e4m3fn else dtype
+    out = torch.full((M, N), float("nan"), dtype=odt, device=DEV)
+    gemm(a, w, out, mode=mode, ksplit=ksplit)
+    torch.cuda.synchronize()
+    ref = _ref(a, w)
+    err = float((out.float() - ref).abs().max())
+    assert err <= _tight_bound(ref, K), err
+    first = out.clone()
+    for _ in range(5):
+        gemm(a, w, out, mode=mode, ksplit=ksplit)
+    torch.cuda.synchronize()
+    assert torch.equal(out, first)
