@@ -84,7 +84,17 @@ def _phys_rows(M: int, grp: int, gstride: int, base_rows: int = 0) -> int:
     return (last // grp) * gstride + (last % grp) + 1
 
 
-def split_k_factor(M: int, N: int, K: int, esz: int, ncu: int = 256) -> int:
+def device_cus() -> int:
+    """CUs of the current device (256 on a whole MI355X; fewer in a compute partition), 256 when
+    no GPU is visible (plans built on the CPU)."""
+    import torch
+
+    if not torch.cuda.is_available():
+        return 256
+    return int(torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count)
+
+
+def split_k_factor(M: int, N: int, K: int, esz: int, ncu: int = 0) -> int:
     """K-slices for a GEMM whose 256x256 grid covers at most half the CUs and whose K is long
     (e.g. 8192 x 1024 x 8192: 128 tiles): ``S`` slices run as (slice, tile) pairs of ONE pt4
     launch (``GemmArgs::ksplit``) and their partials are summed by one reduce kernel. Each slice
@@ -92,6 +102,7 @@ def split_k_factor(M: int, N: int, K: int, esz: int, ncu: int = 256) -> int:
     on the config #2 shape: 0.1009 ms vs 0.1338 unsplit (profiles/r04/r4_22_*). 1 = no split."""
     if M % 256 or N % 256 or M <= 0 or N <= 0:
         return 1
+    ncu = ncu or device_cus()
     tiles = (M // 256) * (N // 256)
     nk = K * esz // 128
     if K * esz % 128:
