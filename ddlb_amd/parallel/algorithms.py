@@ -304,6 +304,9 @@ def _build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, do
     def gemm(stream, a_ref, c_ref, M, **kw):
         plan.gemm(stream, a_ref, Bt, c_ref, M=M, N=n, K=k, lda=k, ldb=k, ldc=n, **gdt, **kw)
 
+    def shard_gemm(p):  # shard p's rows on stream 0 (K-split when few tiles and long K)
+        _full_gemm(plan, arow(p * ml), Bt, crow(p * ml), ml, n, k, ein, eout, cfg, gdt, tag="KSP")
+
     if d == 1:
         _full_gemm(plan, A, Bt, C, m, n, k, ein, eout, cfg, gdt)
         return plan, io
@@ -403,9 +406,7 @@ def _build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, do
         done = _ipc_pull_shards(plan, rank, d, cfg, flags, [(p, [(p * ml, ml)]) for p in peers],
                                 lambda r0: arow(r0), k * ein,
                                 arrive=flags.ref if cfg.fused else None,
-                                after_ready=(lambda: gemm(S_MAIN, arow(rank * ml),
-                                                          crow(rank * ml), ml))
-                                if own_first else None)
+                                after_ready=(lambda: shard_gemm(rank)) if own_first else None)
         if cfg.fused:
             _signal(plan, S_MAIN, [flags.ref("ARRIVE", rank)], cfg)
             gemm(S_MAIN, A, C, m, flags=flags.ref("ARRIVE", 0), flag_rows=ml, nshards=d,
@@ -416,7 +417,7 @@ def _build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, do
                     continue
                 if p != rank:
                     plan.wait(S_MAIN, done[p][0])
-                gemm(S_MAIN, arow(p * ml), crow(p * ml), ml)
+                shard_gemm(p)
         _wait(plan, S_MAIN, [flags.ref("ACK", p) for p in range(d) if p != rank], cfg)
     elif alg == "p2p_pipeline" and be == "rccl":
         # pairwise exchange steps: step j sends my shard to r-j, receives shard r+j
@@ -433,7 +434,7 @@ def _build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, do
         for p in [(rank + j) % d for j in range(d)]:
             if p != rank:
                 plan.wait(S_MAIN, evs[p])
-            gemm(S_MAIN, arow(p * ml), crow(p * ml), ml)
+            shard_gemm(p)
     else:  # pragma: no cover
         raise ValueError(f"unsupported combination {alg}/{be}")
     return plan, io

@@ -440,3 +440,17 @@ def test_ksplit_rejects_tables_and_flags():
     with pytest.raises(ValueError):
         plan.gemm(0, a, a, a, M=256, N=256, K=256, lda=512, ldb=512, ldc=256, din=DT_F32,
                   dout=DT_F32, ksplit=2, a_grp=128, a_gstride=256)
+
+
+@pytest.mark.parametrize("be", ["rccl", "ipc"])
+def test_split_k_p2p_shard_gemms(be):
+    """p2p_pipeline's per-shard GEMMs (plain C rows) take the K-split too when each shard has
+    few tiles and K is long (BASELINE 4b: m = 65536, k = 8192 at d = 8); one scratch buffer is
+    reused on stream 0 between shards, race-free."""
+    d, m, n, k = 2, 512, 256, 2048
+    cfg = AlgoConfig(algorithm="p2p_pipeline", backend=be)
+    plan, _ = build_tp_columnwise(0, d, m, n, k, DT_F32, DT_F32, cfg)
+    g = [op for op in plan.ops if op.kind == OP_GEMM]
+    assert len(g) == d and all(op.args["ksplit"] == 4 for op in g)
+    assert sum(op.kind == OP_REDUCE for op in plan.ops) == d
+    _run_col(d, m, n, k, cfg, epochs=2)
