@@ -454,3 +454,17 @@ def test_split_k_p2p_shard_gemms(be):
     assert len(g) == d and all(op.args["ksplit"] == 4 for op in g)
     assert sum(op.kind == OP_REDUCE for op in plan.ops) == d
     _run_col(d, m, n, k, cfg, epochs=2)
+
+
+def test_split_k_factor_rule():
+    """The K-split rule (ops.gemm.split_k_factor): S slices only while S x tiles fit the CUs and
+    every slice keeps >= 16 K-tiles of an even count; a compute partition's fewer CUs split less."""
+    from ddlb_amd.ops.gemm import split_k_factor as f
+
+    assert f(8192, 1024, 8192, 2, 256) == 2          # BASELINE config #2: 128 tiles
+    assert f(2048, 1024, 8192, 2, 256) == 4          # 32 tiles
+    assert f(2048, 1024, 8192, 1, 256) == 4          # fp8: 64 K-tiles of 128 B
+    assert f(65536, 1024, 1024, 2, 256) == 1         # the flagship fills the chip
+    assert f(8192, 1024, 1024, 2, 256) == 1          # short K: 8 K-tiles per slice is too few
+    assert f(8192, 1024, 8192, 2, 32) == 1           # a 32-CU partition: 128 tiles already fill it
+    assert f(1000, 1024, 8192, 2, 256) == 1          # ragged M
