@@ -18,6 +18,11 @@ EMULATED: local HBM copies stand in for xGMI links and no peer is ever late, so 
 
     python scripts/plan_budget.py --world 8 [--primitive tp_columnwise] [-m 65536 -n 1024 -k 1024]
            [--dtype bfloat16] [--candidates a,b] [--iters 20] [--out gpurun_out/budget.json]
+           [--timeline a,b] [--rccl-blocks 6] [--variants "sig_side=1;gemm_first=0,s=8"]
+
+``--rccl-blocks``: CU budget of the copy kernels standing in for RCCL (6 makes the stand-in
+collectives link-slow, 32 HBM-fast); ``--variants``: ';'-separated AlgoConfig overrides, each
+measured as an extra row ``<candidate>[<overrides>]`` beside the candidate itself.
 """
 
 from __future__ import annotations
