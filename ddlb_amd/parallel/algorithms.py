@@ -195,6 +195,16 @@ def _full_gemm(plan: Plan, a_ref: Ref, Bt: Ref, c_ref: Ref, M: int, N: int, K: i
     plan.reduce(S_MAIN, c_ref, [part + j * M * N * eout for j in range(S)], M * N, gdt["dout"])
 
 
+# A flag-gated persistent GEMM fed by other kernels (RCCL, copy / signal kernels) leaves at least
+# this many CUs free: the emulated RCCL-fed s4 plan hung with 24 or 16 reserved (grids of 232 /
+# 240 workgroups) and ran with 32 or more (profiles/r04/r4_33_*), so smaller requests are raised.
+MIN_GATE_RESERVE = 32
+
+
+def _gate_reserve(cfg: AlgoConfig) -> int:
+    return max(cfg.reserve_cus, MIN_GATE_RESERVE)
+
+
 def _unique(events):
     """Events in first-seen order without repeats (a wait per distinct event is enough)."""
     seen: List[int] = []
@@ -381,7 +391,7 @@ def _build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, do
         # enqueued after the pulls (every dependency points backwards in enqueue order)
         _signal(plan, S_MAIN, [flags.ref("ARRIVE", rank * cfg.s + j) for j in range(cfg.s)], cfg)
         gemm(S_MAIN, A, C, m, flags=flags.ref("ARRIVE", 0), flag_rows=rows, nshards=d * cfg.s,
-             nsub=cfg.s, first_shard=rank, tile_order=1, reserve_cus=cfg.reserve_cus)
+             nsub=cfg.s, first_shard=rank, tile_order=1, reserve_cus=_gate_reserve(cfg))
         _wait(plan, S_MAIN, [flags.ref("ACK", p) for p in range(d) if p != rank], cfg)
     elif alg == "coll_pipeline" and be == "ipc":
         rows = ml // cfg.s
@@ -410,7 +420,7 @@ def _build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, do
         if cfg.fused:
             _signal(plan, S_MAIN, [flags.ref("ARRIVE", rank)], cfg)
             gemm(S_MAIN, A, C, m, flags=flags.ref("ARRIVE", 0), flag_rows=ml, nshards=d,
-                 first_shard=order[0], tile_order=1, reserve_cus=cfg.reserve_cus)
+                 first_shard=order[0], tile_order=1, reserve_cus=_gate_reserve(cfg))
         else:
             for p in order:
                 if p == rank and own_first:
@@ -481,7 +491,7 @@ def _col_rccl_fused_coll(plan, rank, d, m, n, k, ein, cfg, A, Bt, C, comm_dt, gd
                          else G + (j * d + p) * blk)
     gemm = dict(M=m, N=n, K=k, lda=k, ldb=k, ldc=n, **gdt, a_shards=table, shard_rows=rows,
                 flags=flags.ref("ARRIVE", 0), flag_rows=rows, nshards=d * s, nsub=s,
-                first_shard=rank, tile_order=3, reserve_cus=cfg.reserve_cus)
+                first_shard=rank, tile_order=3, reserve_cus=_gate_reserve(cfg))
     first = _gemm_first(cfg)
     if first:
         plan.gemm(S_MAIN, A, Bt, C, **gemm)
@@ -512,7 +522,7 @@ def _col_rccl_fused_p2p(plan, rank, d, m, n, k, ein, cfg, A, Bt, C, comm_dt, gdt
     flags = _Flags(plan, d, 1, symmetric=False)
     gemm = dict(M=m, N=n, K=k, lda=k, ldb=k, ldc=n, **gdt, flags=flags.ref("ARRIVE", 0),
                 flag_rows=ml, nshards=d, first_shard=rank, tile_order=3,
-                reserve_cus=cfg.reserve_cus)
+                reserve_cus=_gate_reserve(cfg))
     first = _gemm_first(cfg)
     if first:
         plan.gemm(S_MAIN, A, Bt, C, **gemm)

@@ -468,3 +468,15 @@ def test_split_k_factor_rule():
     assert f(8192, 1024, 1024, 2, 256) == 1          # short K: 8 K-tiles per slice is too few
     assert f(8192, 1024, 8192, 2, 32) == 1           # a 32-CU partition: 128 tiles already fill it
     assert f(1000, 1024, 8192, 2, 256) == 1          # ragged M
+
+
+def test_gate_reserve_floor():
+    """A gated GEMM fed by other kernels never leaves fewer than 32 CUs free (smaller reserves
+    hung the emulated RCCL-fed plan, profiles/r04/r4_33_*); larger requests pass through."""
+    for alg, be in [("coll_pipeline", "rccl"), ("p2p_pipeline", "rccl"), ("coll_pipeline", "ipc"),
+                    ("p2p_pipeline", "ipc")]:
+        for req, want in [(0, 32), (16, 32), (48, 48)]:
+            cfg = AlgoConfig(algorithm=alg, backend=be, fused=True, s=2, reserve_cus=req)
+            plan, _ = build_tp_columnwise(0, 4, 64, 8, 8, DT_F32, DT_F32, cfg)
+            g = [op for op in plan.ops if op.kind == OP_GEMM and op.args["flags"] is not None]
+            assert g and all(op.args["reserve_cus"] == want for op in g), (alg, be, req)
