@@ -66,6 +66,11 @@ PRIMITIVE_PHASES = {
     "rccl_fused": ("tp_columnwise", dict(algorithm="coll_pipeline", backend="rccl", fused=True,
                                          s=2, tile="pt4")),
 }
+# phases whose check needs the candidates' CU pressure: the RCCL-fed gated GEMM must fill every
+# CU it may take (a grid of num_cus - reserve) while RCCL runs beside it, or a collective that
+# cannot get the CUs it needs would pass here and hang in the bench (profiles/r04/r4_33_*)
+# (m = 512 d q: whole 256-row blocks per rank and stage at s = 2, >= 256 tiles of 256x256)
+PRIMITIVE_SHAPES = {"rccl_fused": lambda d: (512 * d * -(-128 // d), 256, 128 * d)}
 PATTERN_BYTES = 1 << 20      # per rank and phase: 1 MiB (several xGMI packets, small enough)
 RS_COUNT = 4096              # f32 elements per rank of the reduce-scatter check
 
@@ -85,7 +90,7 @@ def run_primitive_check(comm, phase: str, epochs: int = 2) -> None:
     from ddlb_amd.primitives.registry import resolve
 
     prim, opts = PRIMITIVE_PHASES[phase]
-    m, n, k = primitive_shape(comm.world_size)
+    m, n, k = PRIMITIVE_SHAPES.get(phase, primitive_shape)(comm.world_size)
     cls, o, _ = resolve(prim, "native", dict(opts))
     impl = cls(m=m, n=n, k=k, dtype="bfloat16", **o)
     try:

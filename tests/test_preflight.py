@@ -106,6 +106,8 @@ def test_primitive_phases_simulate(d, phase):
     build = build_tp_columnwise if prim == "tp_columnwise" else build_tp_rowwise
     for r in range(d):  # the shape passes every builder check at every rank
         build(r, d, m, n, k, DT_F32, DT_F32, cfg)
+        if phase in pf.PRIMITIVE_SHAPES:  # the phase's own (larger, CU-filling) shape too
+            build(r, d, *pf.PRIMITIVE_SHAPES[phase](d), DT_F32, DT_F32, cfg)
     from test_plans_sim import _run_col, _run_row
 
     (_run_col if prim == "tp_columnwise" else _run_row)(d, m, n, k, cfg, epochs=2)
