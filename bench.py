@@ -94,6 +94,10 @@ CANDIDATES = [
     # one GEMM reading every peer's shard in place over xGMI (pt4 through a shard table)
     ("direct/ipc", "native", dict(algorithm="direct", backend="ipc")),
     ("coll_pipeline/rccl/s8/fused", "native", dict(_COLL4, s=8, fused=True)),
+    # the same on a CU split (RCCL on 32 CUs of its own, the gated GEMM on the other 224): a
+    # collective with more workgroups than the reserve cannot be starved by the spinning tiles
+    # (profiles/r04/r4_34_*); its own preflight phase, so a plain fused hang does not drop it
+    ("coll_pipeline/rccl/s4/fused/cumask", "native", dict(_COLL4, fused=True, comm_cus=32)),
     ("coll_pipeline/rccl/s4", "native", _COLL4),
     ("coll_pipeline/ipc/agk32/s8/graph", "native", _graph(_AGK)),
     ("default/rccl", "native", _DEF),

@@ -52,7 +52,7 @@ from ddlb_amd.parallel.plan import (COPY_ENGINE, DT_F32, DT_U8, SIG_KERNEL, SIG_
                                     Ref)
 
 IPC_PHASES = ("ipc", "ipc_ksig", "ipc_kernel", "ipc_sdma", "ipc_push", "ipc_agk", "ipc_dstore")
-RCCL_PHASES = ("torch_nccl", "rccl", "rccl_fused")
+RCCL_PHASES = ("torch_nccl", "rccl", "rccl_fused", "rccl_fused_cm")
 # phases that run a whole primitive (the real plan builder) instead of a data-movement plan:
 # (primitive, options); the shape is PRIMITIVE_SHAPE(d)
 PRIMITIVE_PHASES = {
@@ -65,12 +65,17 @@ PRIMITIVE_PHASES = {
     # (auto would pick the non-persistent t8 for these few tiles)
     "rccl_fused": ("tp_columnwise", dict(algorithm="coll_pipeline", backend="rccl", fused=True,
                                          s=2, tile="pt4")),
+    # the same with a CU split: RCCL and the signal kernels on 32 CUs of their own, the gated GEMM
+    # on the complement (a collective with more workgroups than the reserve cannot starve then)
+    "rccl_fused_cm": ("tp_columnwise", dict(algorithm="coll_pipeline", backend="rccl", fused=True,
+                                            s=2, tile="pt4", comm_cus=32)),
 }
 # phases whose check needs the candidates' CU pressure: the RCCL-fed gated GEMM must fill every
 # CU it may take (a grid of num_cus - reserve) while RCCL runs beside it, or a collective that
 # cannot get the CUs it needs would pass here and hang in the bench (profiles/r04/r4_33_*)
 # (m = 512 d q: whole 256-row blocks per rank and stage at s = 2, >= 256 tiles of 256x256)
-PRIMITIVE_SHAPES = {"rccl_fused": lambda d: (512 * d * -(-128 // d), 256, 128 * d)}
+PRIMITIVE_SHAPES = {ph: (lambda d: (512 * d * -(-128 // d), 256, 128 * d))
+                    for ph in ("rccl_fused", "rccl_fused_cm")}
 PATTERN_BYTES = 1 << 20      # per rank and phase: 1 MiB (several xGMI packets, small enough)
 RS_COUNT = 4096              # f32 elements per rank of the reduce-scatter check
 
@@ -339,7 +344,9 @@ def needs(impl: str, opts: Dict, primitive: str = "tp_columnwise") -> List[str]:
     alg = opts.get("algorithm", "default")
     fused = bool(opts.get("fused", False))
     if backend in ("rccl", "nccl"):
-        return ["rccl", "rccl_fused"] if fused else ["rccl"]
+        if not fused:
+            return ["rccl"]
+        return ["rccl", "rccl_fused_cm" if int(opts.get("comm_cus", 0)) > 0 else "rccl_fused"]
     out = ["ipc"]
     # a missing "graph" key is the option default "auto" (graph replay whenever capturable, and
     # graph mode always signals with the kernels); the rowwise IPC plans send READY with the

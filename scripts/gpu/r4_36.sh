@@ -1,0 +1,7 @@
+# round 4 / 36: CU-split RCCL-fed fused candidate at world 1; native suite subset
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r4_36
+mkdir -p $O
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_native_gpu.py > $O/tests.txt 2>&1 || { echo "tests failed"; tail -30 $O/tests.txt; exit 1; }
+tail -n 1 $O/tests.txt

@@ -752,6 +752,24 @@ def test_rccl_fed_gated_gemm_world1(comm, dt, mode, s, first, shape):
     ctx.close()
 
 
+def test_rccl_fused_cumask_world1_native(comm):
+    """The CU-split RCCL-fed candidate (``comm_cus=32``) through the primitive at world 1: the
+    GEMM on the masked compute stream (224 CUs), validated, repeat-identical."""
+    from ddlb_amd.primitives.tp_columnwise.native import NativeTPColumnwise
+
+    impl = NativeTPColumnwise(m=65536, n=1024, k=1024, dtype="bfloat16", algorithm="coll_pipeline",
+                              backend="rccl", s=4, fused=True, comm_cus=32)
+    out = impl.run()
+    torch.cuda.synchronize()
+    impl.validate(out)
+    first = out.clone()
+    for _ in range(3):
+        out = impl.run()
+    torch.cuda.synchronize()
+    assert torch.equal(out, first)
+    impl.close()
+
+
 @pytest.mark.parametrize("s", [2, 4])
 def test_rccl_fused_plans_world1_native(comm, s):
     """The coll_pipeline / p2p_pipeline fused=True RCCL options through the primitive at world 1

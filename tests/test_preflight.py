@@ -60,6 +60,8 @@ def test_needs_maps_candidates_to_checks():
     assert pf.needs("pytorch", {}) == ["torch_nccl"]
     assert pf.needs("native", {"backend": "rccl"}) == ["rccl"]
     assert pf.needs("native", {"backend": "rccl", "fused": True}) == ["rccl", "rccl_fused"]
+    assert pf.needs("native", {"backend": "rccl", "fused": True, "comm_cus": 32}) == \
+        ["rccl", "rccl_fused_cm"]
     assert pf.needs("native", {"backend": "ipc", "multicast_protocol": "memcpy",
                                "graph": False}) == ["ipc", "ipc_sdma"]
     # no "graph" key = the option default "auto": graph replay signals with the kernels
