@@ -94,10 +94,6 @@ CANDIDATES = [
     # one GEMM reading every peer's shard in place over xGMI (pt4 through a shard table)
     ("direct/ipc", "native", dict(algorithm="direct", backend="ipc")),
     ("coll_pipeline/rccl/s8/fused", "native", dict(_COLL4, s=8, fused=True)),
-    # the same on a CU split (RCCL on 32 CUs of its own, the gated GEMM on the other 224): a
-    # collective with more workgroups than the reserve cannot be starved by the spinning tiles
-    # (profiles/r04/r4_34_*); its own preflight phase, so a plain fused hang does not drop it
-    ("coll_pipeline/rccl/s4/fused/cumask", "native", dict(_COLL4, fused=True, comm_cus=32)),
     ("coll_pipeline/rccl/s4", "native", _COLL4),
     ("coll_pipeline/ipc/agk32/s8/graph", "native", _graph(_AGK)),
     ("default/rccl", "native", _DEF),
@@ -132,6 +128,11 @@ CANDIDATES = [
     ("coll_pipeline/rccl/s4/cumask", "native", dict(_COLL4, comm_cus=32, register=True)),
     ("coll_pipeline/rccl/s8/cumask", "native", dict(_COLL4, s=8, comm_cus=32, register=True)),
     ("coll_pipeline/rccl/s4/cumask64", "native", dict(_COLL4, comm_cus=64)),
+    # the RCCL-fed fused GEMM on a CU split (RCCL on 32 CUs of its own, the gated GEMM on the
+    # other 224): immune to a collective starved by the spinning tiles, but the masked GEMM runs
+    # 1.5x slower (emulated 0.302 vs 0.181 ms, profiles/r04/r4_36_*): a fallback, with its own
+    # preflight phase so a plain fused hang does not drop it
+    ("coll_pipeline/rccl/s4/fused/cumask", "native", dict(_COLL4, fused=True, comm_cus=32)),
     ("p2p_pipeline/ipc/memcpy/cs2", "native", dict(_P2P, copy_streams=2)),
     # each peer's chunks split over 2 copy streams (2 copy engines per link)
     ("coll_pipeline/ipc/memcpy/s8/cs2/graph", "native",
