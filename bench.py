@@ -74,70 +74,84 @@ def _graph(opts):
     return dict(opts, graph=True)
 
 
-# N > 1 pool, ordered by the one-GPU per-rank budget (scripts/plan_budget.py --world 8,
-# profiles/r04/r4_6_budget_col8.txt: rank 0's d = 8 plan replayed on one GPU, transfers as local
-# copies -- an emulated lower bound): each family's best form first, the RCCL and IPC / xGMI
-# families interleaved, dominated variants last (the tuning deadline cuts the tail). The
-# preflight (RCCL, IPC, in-kernel all-gather, direct store, RCCL-fed gated GEMM, across the real
-# peers) drops whatever this node cannot run.
+# N > 1 pool. Order: the forms that cannot hang by construction first (direct/ipc: one ungated
+# GEMM reading the peers' shards in place; the in-kernel all-gather: a gated GEMM fed only by its
+# own launch's copy workgroups), then the RCCL-fed gated GEMMs (their communicator capped at the
+# GEMM's CU reserve, so a collective always fits beside the spinning tiles) and the plain RCCL
+# pipelines, interleaved with the next IPC forms; within a family, the one-GPU per-rank budget's
+# order (scripts/plan_budget.py --world 8, profiles/r04/r4_6_budget_col8.txt: rank 0's d = 8 plan
+# replayed on one GPU, transfers as local copies -- an emulated lower bound that cannot see the
+# links, so it never outranks the no-hang forms). The preflight (RCCL, IPC, in-kernel all-gather,
+# direct store, RCCL-fed gated GEMM, across the real peers) drops whatever this node cannot run.
+# Sized so that every candidate plus two hangs fits the tuning budget (tests/test_bench_cpu.py
+# test_pool_fits_tuning_budget): dominated and host-bound forms live in CANDIDATES_EXTRA.
 # "/graph": the whole plan is captured once and replayed with one hipGraphLaunch per run (the IPC
 # pipelines issue ~200 HIP calls per run at d = 8 otherwise, profiles/r02/r2_13_*).
 CANDIDATES = [
+    # one GEMM reading every peer's shard in place over xGMI (pt4 through a shard table)
+    ("direct/ipc", "native", dict(algorithm="direct", backend="ipc")),
+    # in-kernel all-gather: budget 0.128 ms (graph), GEMM work 0.085 ms
+    ("coll_pipeline/ipc/agk32/s4/graph", "native", _graph(dict(_AGK, s=4))),
     # RCCL stage all-gathers feeding ONE flag-gated persistent GEMM over all m rows (the
     # flagship's 1024-tile pt4 kernel at m = 65536; per stage a signal kernel raises the
     # arrival flags, the own rows run first, ungated): no under-filled stage GEMMs (at d = 8,
     # s = 8 a stage GEMM has 128 tiles of 256^2 for 256 CUs). Budget 0.196 ms (s4), GEMM work
-    # 0.116-0.119 ms (5 tile rounds on the CUs RCCL leaves)
+    # 0.116-0.119 ms (5 tile rounds on the CUs RCCL leaves); RCCL capped at 32 workgroups
     ("coll_pipeline/rccl/s4/fused", "native", dict(_COLL4, fused=True)),
-    # in-kernel all-gather: budget 0.128 ms (graph), GEMM work 0.085 ms
-    ("coll_pipeline/ipc/agk32/s4/graph", "native", _graph(dict(_AGK, s=4))),
-    # one GEMM reading every peer's shard in place over xGMI (pt4 through a shard table)
-    ("direct/ipc", "native", dict(algorithm="direct", backend="ipc")),
-    ("coll_pipeline/rccl/s8/fused", "native", dict(_COLL4, s=8, fused=True)),
     ("coll_pipeline/rccl/s4", "native", _COLL4),
-    ("coll_pipeline/ipc/agk32/s8/graph", "native", _graph(_AGK)),
     ("default/rccl", "native", _DEF),
     ("p2p_pipeline/rccl/fused", "native", dict(algorithm="p2p_pipeline", backend="rccl",
                                                fused=True)),
-    ("coll_pipeline/ipc/agk64/s8/graph", "native", _graph(dict(_AGK, copy_blocks=64))),
+    ("coll_pipeline/ipc/agk32/s8/graph", "native", _graph(_AGK)),
+    ("coll_pipeline/rccl/s8/fused", "native", dict(_COLL4, s=8, fused=True)),
     ("default/ipc/kernel", "native", _DEF_K),
     ("coll_pipeline/rccl/s8", "native", dict(_COLL4, s=8)),
     ("p2p_pipeline/rccl", "native", dict(algorithm="p2p_pipeline", backend="rccl")),
-    ("coll_pipeline/ipc/kernel/s4", "native", dict(_COLL_IPC, multicast_protocol="kernel",
-                                                   copy_blocks=128, tile="128x128")),
+    ("default/ipc/push", "native", dict(_P2P, algorithm="default", direction="push")),
+    ("coll_pipeline/ipc/agk64/s8/graph", "native", _graph(dict(_AGK, copy_blocks=64))),
     ("p2p_pipeline/ipc/memcpy/graph", "native", _graph(_P2P)),
     ("coll_pipeline/ipc/memcpy/s4/graph", "native", _graph(_COLL_IPC)),
-    ("default/ipc/push", "native", dict(_P2P, algorithm="default", direction="push")),
-    ("coll_pipeline/ipc/push/s4", "native", dict(_COLL_IPC, direction="push")),
     # the stage GEMMs next to RCCL's CU-resident kernels: 128x128 tiles (4x as many, dispatched
     # dynamically) let the CUs busy with RCCL simply take fewer of them
-    ("coll_pipeline/rccl/s4/128", "native", dict(_COLL4, tile="128x128")),
     ("coll_pipeline/rccl/s4/128/c16", "native", dict(_COLL4, tile="128x128",
                                                       _env={"NCCL_MAX_NCHANNELS": "16"})),
-    ("coll_pipeline/ipc/kernel/s8/graph", "native", _graph(dict(
-        _COLL_IPC, s=8, multicast_protocol="kernel", copy_blocks=128, tile="128x128"))),
-    ("coll_pipeline/ipc/batch/s8/graph", "native", _graph(dict(
-        _COLL_IPC, s=8, multicast_protocol="batch_memcpy"))),
-    ("coll_pipeline/ipc/memcpy/s8/graph", "native", _graph(dict(_COLL_IPC, s=8))),
-    # one flag-gated GEMM fed by copy-engine pulls: eager only (a graph would have to order the
-    # gated GEMM after every copy stream, see PlanExecutor::graph_capturable)
-    ("coll_pipeline/ipc/memcpy/s8/fused", "native", dict(_COLL_IPC, s=8, fused=True)),
-    # RCCL's kernels on a CU-masked comm stream (csrc/comm: hipExtStreamCreateWithCUMask), the
-    # stage GEMMs sized to the complement; buffers registered with ncclCommRegister (budget:
-    # 3.5x the unmasked plans: the masked GEMMs lose 32-64 CUs for the whole run)
-    ("coll_pipeline/rccl/s4/cumask", "native", dict(_COLL4, comm_cus=32, register=True)),
-    ("coll_pipeline/rccl/s8/cumask", "native", dict(_COLL4, s=8, comm_cus=32, register=True)),
-    ("coll_pipeline/rccl/s4/cumask64", "native", dict(_COLL4, comm_cus=64)),
+    ("coll_pipeline/ipc/kernel/s4", "native", dict(_COLL_IPC, multicast_protocol="kernel",
+                                                   copy_blocks=128, tile="128x128")),
     # the RCCL-fed fused GEMM on a CU split (RCCL on 32 CUs of its own, the gated GEMM on the
     # other 224): immune to a collective starved by the spinning tiles, but the masked GEMM runs
     # 1.5x slower (emulated 0.302 vs 0.181 ms, profiles/r04/r4_36_*): a fallback, with its own
-    # preflight phase so a plain fused hang does not drop it
+    # preflight phase so a plain fused hang does not drop it. CU-masked streams carry no priority
+    # (HIP's hipExtStreamCreateWithCUMask takes none): its comm stream runs at normal priority,
+    # which a CU split does not need (test_rccl_data_plane_world1 asserts what HIP gives)
     ("coll_pipeline/rccl/s4/fused/cumask", "native", dict(_COLL4, fused=True, comm_cus=32)),
-    ("p2p_pipeline/ipc/memcpy/cs2", "native", dict(_P2P, copy_streams=2)),
-    # each peer's chunks split over 2 copy streams (2 copy engines per link)
+]
+# Measured but dominated at d = 8, or host-bound: not in the default pool (each costs tuning
+# time on the 8-GPU node), still selectable with --candidates / --algorithm. Host cost per run
+# (eager) and the emulated plan time from profiles/r04/r4_6_budget_col8.txt:
+CANDIDATES_EXTRA = [
+    ("coll_pipeline/rccl/s4/128", "native", dict(_COLL4, tile="128x128")),   # 0.263 ms
+    ("coll_pipeline/ipc/kernel/s8/graph", "native", _graph(dict(             # 0.330 ms graph
+        _COLL_IPC, s=8, multicast_protocol="kernel", copy_blocks=128, tile="128x128"))),
+    ("coll_pipeline/ipc/push/s4", "native", dict(_COLL_IPC, direction="push")),  # host 411 us
+    # batch_memcpy: hipMemcpyBatchAsync is absent from torch's HIP 7.0 runtime, so every "batch"
+    # is per-segment copies (the ipc_batch preflight phase fails there and drops it anyway)
+    ("coll_pipeline/ipc/batch/s8/graph", "native", _graph(dict(
+        _COLL_IPC, s=8, multicast_protocol="batch_memcpy"))),
+    ("coll_pipeline/ipc/memcpy/s8/graph", "native", _graph(dict(_COLL_IPC, s=8))),  # 0.779 ms
+    # one flag-gated GEMM fed by copy-engine pulls: eager only (a graph would have to order the
+    # gated GEMM after every copy stream, see PlanExecutor::graph_capturable); host 682 us
+    ("coll_pipeline/ipc/memcpy/s8/fused", "native", dict(_COLL_IPC, s=8, fused=True)),
+    # RCCL's kernels on a CU-masked comm stream (csrc/comm: hipExtStreamCreateWithCUMask), the
+    # stage GEMMs sized to the complement (the masked GEMMs lose 32-64 CUs for the whole run:
+    # 0.73-1.51 ms emulated)
+    ("coll_pipeline/rccl/s4/cumask", "native", dict(_COLL4, comm_cus=32, register=True)),
+    ("coll_pipeline/rccl/s8/cumask", "native", dict(_COLL4, s=8, comm_cus=32, register=True)),
+    ("coll_pipeline/rccl/s4/cumask64", "native", dict(_COLL4, comm_cus=64)),
+    ("p2p_pipeline/ipc/memcpy/cs2", "native", dict(_P2P, copy_streams=2)),        # host 337 us
+    # each peer's chunks split over 2 copy streams (2 copy engines per link): 1.17 ms graph
     ("coll_pipeline/ipc/memcpy/s8/cs2/graph", "native",
      dict(_COLL_IPC, s=8, copy_streams=2, graph=True)),
-    ("coll_pipeline/ipc/memcpy/s8", "native", dict(_COLL_IPC, s=8)),
+    ("coll_pipeline/ipc/memcpy/s8", "native", dict(_COLL_IPC, s=8)),             # host 562 us
 ]
 VENDOR = [
     ("pytorch(rccl+hipblaslt)", "pytorch", dict(backend="nccl", empty_cache=False)),
@@ -190,18 +204,28 @@ ROW_WORLD1_VENDOR = [
 ]
 
 
-def candidate_pool(primitive: str, dtype: str, world: int):
+FP8_NON_MX = 3  # N > 1 fp8: non-scaled fp8 (the bf16 MFMA rate) kept for the first few forms only
+
+
+def candidate_pool(primitive: str, dtype: str, world: int, extra: bool = False):
     """(label, impl, options) list for one primitive / dtype / world size: our native
     candidates first, then the vendor-library slots (measured for ``vendor_ms``). fp8 inputs add
-    the block-scaled MX-fp8 MFMA (2x the bf16 rate) to every native candidate."""
+    the block-scaled MX-fp8 MFMA (2x the bf16 rate) to every native candidate; at N > 1 the
+    non-scaled fp8 forms (the bf16 rate) are kept for the first ``FP8_NON_MX`` only, so the pool
+    stays inside the tuning budget. ``extra``: also the dominated forms (``CANDIDATES_EXTRA``)."""
     row = primitive == "tp_rowwise"
     if world == 1:
         native, vendor = (ROW_WORLD1, ROW_WORLD1_VENDOR) if row else (WORLD1, WORLD1_VENDOR)
     else:
         native, vendor = (ROW_CANDIDATES, ROW_VENDOR) if row else (CANDIDATES, VENDOR)
+        if extra and not row:
+            native = native + CANDIDATES_EXTRA
     if dtype == "float8_e4m3fn":
-        native = native + [(lbl + "/mx", impl, dict(opts, gemm_mode="mx"))
-                           for lbl, impl, opts in native]
+        mx = [(lbl + "/mx", impl, dict(opts, gemm_mode="mx")) for lbl, impl, opts in native]
+        if world == 1 or extra:
+            native = native + mx
+        else:  # MX first: twice the MFMA rate of every non-scaled form
+            native = mx + native[:FP8_NON_MX]
         vendor = [c for c in vendor if c[1] != "compute_only"]  # torch.matmul has no fp8
     return list(native) + list(vendor)
 
@@ -732,7 +756,8 @@ def main(argv=None) -> int:
     job.log(f"import torch {time.time() - t0:.1f} s")
     tune = {}
     pool = candidate_pool(a.primitive, a.dtype, world)
-    every = candidate_pool(a.primitive, a.dtype, 1) + candidate_pool(a.primitive, a.dtype, 2)
+    every = (candidate_pool(a.primitive, a.dtype, 1) +
+             candidate_pool(a.primitive, a.dtype, 2, extra=True))
     if a.candidates:
         want = [c.strip() for c in a.candidates.split(",") if c.strip()]
         unknown = [w for w in want if w not in [c[0] for c in every]]

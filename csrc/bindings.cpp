@@ -163,14 +163,17 @@ PYBIND11_MODULE(_C, m) {
 
   py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
       .def_static("unique_id", []() { return py::bytes(RcclComm::unique_id()); })
-      .def(py::init([](py::bytes uid, int nranks, int rank, int device) {
-             return std::make_shared<RcclComm>(std::string(uid), nranks, rank, device);
+      // (the id arrives as std::string: converted from bytes before the GIL is released)
+      .def(py::init([](const std::string& uid, int nranks, int rank, int device, int max_ctas) {
+             return std::make_shared<RcclComm>(uid, nranks, rank, device, max_ctas);
            }),
-           py::call_guard<py::gil_scoped_release>())
+           py::arg("uid"), py::arg("nranks"), py::arg("rank"), py::arg("device"),
+           py::arg("max_ctas") = 0, py::call_guard<py::gil_scoped_release>())
       .def("destroy", &RcclComm::destroy)
       .def("async_error", &RcclComm::async_error)
       .def_property_readonly("rank", &RcclComm::rank)
-      .def_property_readonly("nranks", &RcclComm::nranks);
+      .def_property_readonly("nranks", &RcclComm::nranks)
+      .def_property_readonly("max_ctas", &RcclComm::max_ctas);
 
   py::class_<RcclMem, std::shared_ptr<RcclMem>>(m, "RcclMem")
       .def(py::init<std::shared_ptr<RcclComm>, size_t, int>(), py::arg("comm"), py::arg("bytes"),

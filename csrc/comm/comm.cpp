@@ -16,13 +16,23 @@ std::string RcclComm::unique_id() {
   return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
 }
 
-RcclComm::RcclComm(const std::string& uid, int nranks, int rank, int device)
-    : rank_(rank), nranks_(nranks) {
+RcclComm::RcclComm(const std::string& uid, int nranks, int rank, int device, int max_ctas)
+    : rank_(rank), nranks_(nranks), max_ctas_(max_ctas > 0 ? max_ctas : 0) {
   if (uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("bad ncclUniqueId size");
   ncclUniqueId id;
   std::memcpy(&id, uid.data(), sizeof(id));
   DDLB_HIP(hipSetDevice(device));
-  DDLB_NCCL(ncclCommInitRank(&comm_, nranks, id, rank));
+  if (max_ctas_ == 0) {
+    DDLB_NCCL(ncclCommInitRank(&comm_, nranks, id, rank));
+    return;
+  }
+  // The CTA cap is a communicator attribute (the layout up to maxCTAs is the same in every
+  // ncclConfig_t version); minCTAs is lowered with it so the pair stays valid. A library that
+  // refuses the config fails loudly: a capped communicator is a safety property, never a hint.
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.maxCTAs = max_ctas_;
+  cfg.minCTAs = 1;
+  DDLB_NCCL(ncclCommInitRankConfig(&comm_, nranks, id, rank, &cfg));
 }
 
 RcclComm::~RcclComm() {

@@ -32,17 +32,22 @@ namespace ddlb {
 class RcclComm {
  public:
   static std::string unique_id();  // 128 raw bytes
-  RcclComm(const std::string& uid, int nranks, int rank, int device);
+  // max_ctas > 0: the communicator's kernels launch at most that many workgroups (ncclConfig_t
+  // maxCTAs, one workgroup per channel). A flag-gated persistent GEMM fed by this communicator's
+  // collectives leaves `reserve_cus` CUs free; with max_ctas <= reserve_cus the collective can
+  // always be resident beside the spinning tiles (ddlb_amd/parallel/algorithms.py).
+  RcclComm(const std::string& uid, int nranks, int rank, int device, int max_ctas = 0);
   ~RcclComm();
   void destroy();
   ncclComm_t get() const { return comm_; }
   int rank() const { return rank_; }
   int nranks() const { return nranks_; }
+  int max_ctas() const { return max_ctas_; }
   std::string async_error() const;
 
  private:
   ncclComm_t comm_ = nullptr;
-  int rank_ = 0, nranks_ = 1;
+  int rank_ = 0, nranks_ = 1, max_ctas_ = 0;
 };
 
 ncclDataType_t nccl_dtype(int dt);  // DT_* -> ncclDataType_t

@@ -1896,6 +1896,10 @@ hipError_t launch_pt4(const GemmArgs& p, hipStream_t s) {
     return hipGetLastError();
   }
   if (apan && p.c_table != nullptr) return hipErrorNotSupported;
+  // tile_order 3 promises that the first producer's rows are never gated; only the table / grouped
+  // A (APAN) gated instantiation implements that skip (OWN), so anything else is refused rather
+  // than left to spin on a flag nobody raises
+  if (p.flags != nullptr && p.tile_order == 3 && !apan) return hipErrorNotSupported;
   if (apan && p.flags != nullptr && wt)
     hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, true, 2, true>), dim3(grid + q.ag_ctas),
                        dim3(512), 0, s, q);

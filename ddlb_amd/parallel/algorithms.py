@@ -450,17 +450,37 @@ def _build_tp_columnwise(rank: int, d: int, m: int, n: int, k: int, din: int, do
     return plan, io
 
 
-def _gemm_first(cfg: AlgoConfig) -> bool:
-    """Enqueue an RCCL-fed gated GEMM ahead of its producers? Only with >= 2 hardware queues per
-    process: with one, the GEMM's spinning tiles would sit in front of the collectives that set
-    their flags in a single in-order queue."""
+def _gemm_first(plan: Plan, cfg: AlgoConfig, producers=(S_COMM,)) -> bool:
+    """Enqueue an RCCL-fed gated GEMM ahead of its producers? Only when its stream can never share
+    an in-order hardware queue with theirs: HIP pools hardware queues per stream priority (the
+    executor's stream-0 ops run on a normal-priority pool stream, the comm streams are created at
+    high priority) and a CU-masked stream gets a queue of its own, so the GEMM's spinning tiles
+    can then never sit in front of a collective or signal kernel that sets their flags.
+    Otherwise (a producer on a normal-priority stream, or one hardware queue per process) the GEMM
+    goes after the producers: correct in any queue mapping, at the cost of starting after the host
+    has enqueued the collectives. The decision is recorded in ``plan.meta['gemm_first']``."""
     import os
 
     try:
         queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
     except ValueError:
         queues = 4
-    return cfg.gemm_first and queues >= 2
+    prio = plan.stream_priority
+    separate = (cfg.comm_cus > 0 or
+                all(p < len(prio) and prio[p] > 0 for p in producers) and prio[S_MAIN] == 0)
+    first = bool(cfg.gemm_first and queues >= 2 and separate)
+    plan.meta["gemm_first"] = first
+    return first
+
+
+def _rccl_gate(plan: Plan, cfg: AlgoConfig) -> int:
+    """Reserve of an RCCL-fed gated GEMM and the CTA cap of the communicator feeding it: the
+    collectives launch at most ``reserve`` workgroups (``rccl_max_ctas``, applied when the plan is
+    bound: ``context.rccl_gate_cap``), so GEMM grid + RCCL grid <= num_cus by construction. With
+    a CU split the collectives run on CUs of their own and keep RCCL's default."""
+    reserve = _gate_reserve(cfg)
+    plan.meta["rccl_max_ctas"] = 0 if cfg.comm_cus > 0 else reserve
+    return reserve
 
 
 def _col_rccl_fused_coll(plan, rank, d, m, n, k, ein, cfg, A, Bt, C, comm_dt, gdt) -> None:
@@ -491,12 +511,12 @@ def _col_rccl_fused_coll(plan, rank, d, m, n, k, ein, cfg, A, Bt, C, comm_dt, gd
                          else G + (j * d + p) * blk)
     gemm = dict(M=m, N=n, K=k, lda=k, ldb=k, ldc=n, **gdt, a_shards=table, shard_rows=rows,
                 flags=flags.ref("ARRIVE", 0), flag_rows=rows, nshards=d * s, nsub=s,
-                first_shard=rank, tile_order=3, reserve_cus=_gate_reserve(cfg))
-    first = _gemm_first(cfg)
-    if first:
-        plan.gemm(S_MAIN, A, Bt, C, **gemm)
+                first_shard=rank, tile_order=3, reserve_cus=_rccl_gate(plan, cfg))
     # the signal kernels run on the comm stream or, sig_side, on their own stream
     s_sig = 2 if cfg.sig_side else S_COMM
+    first = _gemm_first(plan, cfg, (S_COMM, s_sig))
+    if first:
+        plan.gemm(S_MAIN, A, Bt, C, **gemm)
     for j in range(s):
         plan.allgather(S_COMM, A + (rank * ml + j * rows) * k * ein, G + j * d * blk, rows * k,
                        comm_dt)
@@ -517,16 +537,22 @@ def _col_rccl_fused_p2p(plan, rank, d, m, n, k, ein, cfg, A, Bt, C, comm_dt, gdt
     flag-gated GEMM over all m rows: step j receives shard (r+j)%d into its rows of A and a
     signal kernel raises ARRIVE[(r+j)%d]; the tiles run shard by shard from the own one
     (tile_order 3: the own shard first and never gated, then (r+1)%d, ...: the order the steps
-    deliver them); the GEMM is enqueued first (``AlgoConfig.gemm_first``)."""
+    deliver them); the GEMM is enqueued first when that is safe (:func:`_gemm_first`).
+
+    A is read through a row-block table (shard p = rows p*m/d of A itself): tile_order 3's "own
+    shard never gated" lives in the table-A (APAN) instantiation of the persistent kernel, and
+    ARRIVE[rank] is never raised (with plain A rows the own tiles spun until the
+    timeout). The launcher refuses tile_order 3 on any kernel that would gate the own shard."""
     ml = m // d
     flags = _Flags(plan, d, 1, symmetric=False)
     gemm = dict(M=m, N=n, K=k, lda=k, ldb=k, ldc=n, **gdt, flags=flags.ref("ARRIVE", 0),
                 flag_rows=ml, nshards=d, first_shard=rank, tile_order=3,
-                reserve_cus=_gate_reserve(cfg))
-    first = _gemm_first(cfg)
+                a_shards=[A + p * ml * k * ein for p in range(d)], shard_rows=ml,
+                reserve_cus=_rccl_gate(plan, cfg))
+    s_sig = 2 if cfg.sig_side else S_COMM  # (see _col_rccl_fused_coll)
+    first = _gemm_first(plan, cfg, (S_COMM, s_sig))
     if first:
         plan.gemm(S_MAIN, A, Bt, C, **gemm)
-    s_sig = 2 if cfg.sig_side else S_COMM  # (see _col_rccl_fused_coll)
     for j in range(1, d):
         to, frm = (rank - j) % d, (rank + j) % d
         plan.group_start(S_COMM)

@@ -109,20 +109,29 @@ class NativeContext:
         self.rank = communicator.rank
         self.world = communicator.world_size
         self.device_index = communicator.device.index
-        self._rccl = None
+        self._rccl: Dict[int, object] = {}   # CTA cap (0 = RCCL's default) -> communicator
         self._owned: List = []
         self._single_node_checked = False
 
-    def rccl(self):
-        """Our own RCCL communicator (lazily created, collective over all ranks)."""
+    def rccl(self, max_ctas: int = 0):
+        """Our own RCCL communicator (lazily created, collective over all ranks). ``max_ctas`` > 0:
+        a communicator whose kernels launch at most that many workgroups (``ncclConfig_t``
+        maxCTAs), the one a plan with an RCCL-fed flag-gated GEMM binds (see
+        :func:`rccl_gate_cap`); one communicator per cap, created in bind order (identical on
+        every rank)."""
         import torch.distributed as dist
 
-        if self._rccl is None:
+        cap = max(int(max_ctas), 0)
+        if cap not in self._rccl:
             obj = [bytes(self.C.RcclComm.unique_id()) if self.rank == 0 else None]
             if self.world > 1:
                 dist.broadcast_object_list(obj, src=0)
-            self._rccl = self.C.RcclComm(obj[0], self.world, self.rank, self.device_index)
-        return self._rccl
+            comm = self.C.RcclComm(obj[0], self.world, self.rank, self.device_index, cap)
+            if int(comm.max_ctas) != cap:
+                raise RuntimeError(f"RCCL communicator: asked for a {cap}-CTA cap, got "
+                                   f"{comm.max_ctas}")
+            self._rccl[cap] = comm
+        return self._rccl[cap]
 
     def symmetric(self, nbytes: int, uncached: bool = False) -> SymmetricBuffer:
         if not self._single_node_checked:
@@ -152,11 +161,9 @@ class NativeContext:
         for b in self._owned:
             b.close()
         self._owned = []
-        if self._rccl is not None:
-            try:
-                self._rccl.destroy()
-            finally:
-                self._rccl = None
+        comms, self._rccl = list(self._rccl.values()), {}
+        for c in comms:
+            c.destroy()
 
 
 def rccl_buffers(plan: Plan) -> List[str]:
@@ -169,6 +176,32 @@ def rccl_buffers(plan: Plan) -> List[str]:
                 if ref is not None and ref.buf not in names:
                     names.append(ref.buf)
     return names
+
+
+def rccl_gate_cap(plan: Plan) -> int:
+    """CTA cap of the RCCL communicator a plan must bind (0 = RCCL's default).
+
+    A plan whose flag-gated GEMM is fed by RCCL collectives (the RCCL-fed fused pipelines) is
+    deadlock-free only if the collectives can always be resident beside the spinning tiles. The
+    gated persistent GEMM takes ``num_cus - reserve_cus`` CUs (one workgroup each, a whole CU's
+    register file), so the builder records ``rccl_max_ctas`` <= ``reserve_cus`` in the plan and the
+    communicator is created with that cap (``ncclConfig_t`` maxCTAs): GEMM grid + RCCL grid <=
+    num_cus holds by construction, whatever RCCL's default channel count is on the node. A CU split
+    (``comm_cus`` > 0: the collectives on CUs of their own) needs no cap. Anything else is refused
+    here, before a launch could hang."""
+    gated = [op for op in plan.ops if op.kind == OP_GEMM and op.args.get("flags") is not None
+             and op.stream == 0]
+    if not gated or not any(op.kind in RCCL_OPS for op in plan.ops):
+        return int(plan.meta.get("rccl_max_ctas", 0))
+    cap = int(plan.meta.get("rccl_max_ctas", 0))
+    if int(plan.meta.get("comm_cus", 0)) > 0:
+        return cap
+    reserve = min(int(op.args.get("reserve_cus", 0)) for op in gated)
+    if cap <= 0 or cap > reserve:
+        raise ValueError(f"RCCL-fed flag-gated GEMM: the communicator's CTA cap ({cap}) must be "
+                         f"in [1, reserve_cus = {reserve}] (or use comm_cus > 0), else a collective "
+                         "may not fit beside the spinning tiles")
+    return cap
 
 
 class BoundPlan:
@@ -191,10 +224,13 @@ class BoundPlan:
         dev = torch.device("cuda", ctx.device_index)
         externals = dict(externals or {})
         registered = set(rccl_buffers(plan)) if plan.meta.get("register") else set()
+        # an RCCL-fed flag-gated GEMM binds a CTA-capped communicator (checked, CPU-testable)
+        self.rccl_cap = rccl_gate_cap(plan)
         for name, spec in plan.buffers.items():  # dict order == identical on every rank
             if name in registered and name not in externals and not spec.symmetric:
                 # zero-copy RCCL buffer: ncclMemAlloc + ncclCommRegister on our communicator
-                mem = ctx.C.RcclMem(ctx.rccl(), max(spec.nbytes, 16), ctx.device_index)
+                mem = ctx.C.RcclMem(ctx.rccl(self.rccl_cap), max(spec.nbytes, 16),
+                                    ctx.device_index)
                 self.rmem[name] = mem
                 self.local[name] = torch.from_dlpack(ctx.C.rccl_mem_dlpack(mem, ctx.device_index))
                 continue
@@ -235,7 +271,7 @@ class BoundPlan:
                                  list(plan.stream_priority))
         self.ex.load(words)
         if any(op.kind in RCCL_OPS for op in plan.ops):
-            self.ex.set_comm(ctx.rccl())
+            self.ex.set_comm(ctx.rccl(self.rccl_cap))
             if any(op.kind == OP_GEMM and op.args.get("flags") is not None for op in plan.ops):
                 self._warm_rccl()
         if plan.meta.get("comm_cus", 0):
@@ -261,7 +297,7 @@ class BoundPlan:
         ex = self.ctx.C.PlanExecutor(self.ctx.device_index, warm.nstreams, 1,
                                      list(warm.stream_priority))
         ex.load(warm.encode(self.resolve))
-        ex.set_comm(self.ctx.rccl())
+        ex.set_comm(self.ctx.rccl(self.rccl_cap))
         ex.run(_raw_stream(self.ctx.device_index))
         torch.cuda.synchronize()
         del ex

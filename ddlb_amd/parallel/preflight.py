@@ -22,6 +22,9 @@ check           what it proves (every rank, every peer, two epochs)
 ``ipc_sdma``    copy-engine pull (``hipMemcpyAsync`` from IPC-mapped peer memory, one stream per
                 peer) of every peer's pattern
 ``ipc_push``    copy-engine push (posted writes into each peer's receive slot) + DONE flag
+``ipc_batch``   every peer's pattern pulled in ONE batched copy-engine submission
+                (``hipMemcpyBatchAsync``); fails where the runtime lacks that API, since a
+                ``batch_memcpy`` candidate would then time per-segment copies under its name
 ``ipc_agk``     the in-kernel all-gather: ONE gated persistent GEMM launch whose copy workgroups
                 pull every peer's row blocks over xGMI (write-through publication, agent-scope
                 gate acquire, ACK stores across the link), validated against fp32
@@ -51,7 +54,8 @@ from typing import Callable, Dict, List, Optional
 from ddlb_amd.parallel.plan import (COPY_ENGINE, DT_F32, DT_U8, SIG_KERNEL, SIG_STREAM, Plan,
                                     Ref)
 
-IPC_PHASES = ("ipc", "ipc_ksig", "ipc_kernel", "ipc_sdma", "ipc_push", "ipc_agk", "ipc_dstore")
+IPC_PHASES = ("ipc", "ipc_ksig", "ipc_kernel", "ipc_sdma", "ipc_push", "ipc_batch", "ipc_agk",
+              "ipc_dstore")
 RCCL_PHASES = ("torch_nccl", "rccl", "rccl_fused", "rccl_fused_cm")
 # phases that run a whole primitive (the real plan builder) instead of a data-movement plan:
 # (primitive, options); the shape is PRIMITIVE_SHAPE(d)
@@ -156,6 +160,10 @@ def build_ipc_plan(rank: int, d: int, phase: str, nbytes: int = PATTERN_BYTES) -
             evs.append(e)
         for e in evs:
             plan.wait(0, e)
+    elif phase == "ipc_batch":
+        segs = [(R + p * nbytes, X.at(p), nbytes) for p in peers]
+        for i in range(0, len(segs), 8):
+            plan.copy_batch(0, segs[i:i + 8])
     elif phase == "ipc_push":
         for idx, p in enumerate(peers):
             st = 2 + idx
@@ -238,94 +246,126 @@ def _check_eq(got, want, what: str) -> None:
         raise AssertionError(f"{what}: {bad} of {want.numel()} words differ")
 
 
-def run_ipc_checks(comm, phases=IPC_PHASES, progress_path: Optional[str] = None,
-                   nbytes: int = PATTERN_BYTES, epochs: int = 2) -> Dict[str, str]:
+def _ipc_phase(comm, phase: str, nbytes: int, epochs: int) -> Callable[[], None]:
+    """The check of one IPC phase (a data-movement plan on the native executor)."""
     import torch
 
-    ctx = comm.native()
+    def one():
+        ctx = comm.native()
+        r, d, dev = comm.rank, comm.world_size, comm.device
+        plan = build_ipc_plan(r, d, phase, nbytes)
+        bound = ctx.bind(plan)
+        try:
+            for ep in range(1, epochs + 1):
+                x = bound.buffer("X").view(torch.int32)
+                x.copy_(pattern(r, nbytes, ep).to(dev))
+                bound.buffer("R").view(torch.int32).fill_(-1)
+                torch.cuda.synchronize(dev)
+                comm.barrier()  # every rank's X of this epoch is in place
+                bound.run()
+                torch.cuda.synchronize(dev)
+                bound.check_health()
+                if phase == "ipc_batch":
+                    status = ctx.C.copy_batch_status()
+                    if status != "hipMemcpyBatchAsync":
+                        raise RuntimeError(f"batched copies: {status}")
+                if phase in ("ipc_kernel", "ipc_sdma", "ipc_push", "ipc_batch"):
+                    rv = bound.buffer("R").view(torch.int32)
+                    for p in range(d):
+                        if p != r:
+                            _check_eq(rv[p * nbytes // 4:(p + 1) * nbytes // 4],
+                                      pattern(p, nbytes, ep), f"{phase} slot of rank {p}")
+                comm.barrier()  # nobody refills X while a peer may still read it
+        finally:
+            bound.close()
+
+    return one
+
+
+def phase_checks(comm, family: str, nbytes: int = PATTERN_BYTES, count: int = RS_COUNT,
+                 epochs: int = 2) -> Dict[str, Callable[[], None]]:
+    """phase -> check for one family (``rccl`` | ``ipc``): every declared phase has exactly one
+    check here (``tests/test_preflight.py`` asserts it), so a phase missing from a progress file
+    can only mean that its child was killed mid-phase (a timeout), never an unimplemented phase."""
+    fns: Dict[str, Callable[[], None]] = {}
+    phases = RCCL_PHASES if family == "rccl" else IPC_PHASES
+    for ph in phases:
+        if ph in PRIMITIVE_PHASES:
+            fns[ph] = (lambda ph=ph: run_primitive_check(comm, ph, epochs))
+        elif family == "ipc":
+            fns[ph] = _ipc_phase(comm, ph, nbytes, epochs)
+    if family == "rccl":
+        fns["torch_nccl"] = lambda: _torch_nccl_check(comm)
+        fns["rccl"] = lambda: _own_rccl_check(comm, nbytes, count)
+    return fns
+
+
+def _run_family(comm, family: str, phases, progress_path, **kw) -> Dict[str, str]:
     prog = _Progress(progress_path)
-    r, d = comm.rank, comm.world_size
-    dev = comm.device
-    for phase in phases:
-        if phase in PRIMITIVE_PHASES:
-            _run_checked(phase, prog, lambda: run_primitive_check(comm, phase))
+    fns = phase_checks(comm, family, **kw)
+    for ph in phases:
+        fn = fns.get(ph)
+        if fn is None:  # (a caller asking for a phase of the other family)
+            prog.put(ph, "failed: no such preflight check")
             continue
-
-        def one():
-            plan = build_ipc_plan(r, d, phase, nbytes)
-            bound = ctx.bind(plan)
-            try:
-                for ep in range(1, epochs + 1):
-                    x = bound.buffer("X").view(torch.int32)
-                    x.copy_(pattern(r, nbytes, ep).to(dev))
-                    bound.buffer("R").view(torch.int32).fill_(-1)
-                    torch.cuda.synchronize(dev)
-                    comm.barrier()  # every rank's X of this epoch is in place
-                    bound.run()
-                    torch.cuda.synchronize(dev)
-                    bound.check_health()
-                    if phase in ("ipc_kernel", "ipc_sdma", "ipc_push"):
-                        rv = bound.buffer("R").view(torch.int32)
-                        for p in range(d):
-                            if p != r:
-                                _check_eq(rv[p * nbytes // 4:(p + 1) * nbytes // 4],
-                                          pattern(p, nbytes, ep), f"{phase} slot of rank {p}")
-                    comm.barrier()  # nobody refills X while a peer may still read it
-            finally:
-                bound.close()
-
-        _run_checked(phase, prog, one)
+        _run_checked(ph, prog, fn)
     return prog.res
+
+
+def run_ipc_checks(comm, phases=IPC_PHASES, progress_path: Optional[str] = None,
+                   nbytes: int = PATTERN_BYTES, epochs: int = 2) -> Dict[str, str]:
+    return _run_family(comm, "ipc", phases, progress_path, nbytes=nbytes, epochs=epochs)
+
+
+def _torch_nccl_check(comm) -> None:
+    """torch's RCCL process group: a SUM all-reduce of rank-dependent values."""
+    import torch
+    import torch.distributed as dist
+
+    r, d, dev = comm.rank, comm.world_size, comm.device
+    if dist.get_backend() == "nccl":
+        grp = None
+    else:  # control plane forced to gloo: build a separate RCCL group
+        grp = dist.new_group(backend="nccl")
+    t = torch.full((1024,), float(r + 1), device=dev)
+    dist.all_reduce(t, group=grp)
+    torch.cuda.synchronize(dev)
+    want = torch.full((1024,), float(d * (d + 1) // 2))
+    _check_eq(t, want, "all_reduce")
+    if grp is not None:
+        dist.destroy_process_group(grp)
+
+
+def _own_rccl_check(comm, nbytes: int, count: int) -> None:
+    """Our own communicator on our streams: all-gather + reduce-scatter, two epochs."""
+    import torch
+
+    r, d, dev = comm.rank, comm.world_size, comm.device
+    ctx = comm.native()
+    bound = ctx.bind(build_rccl_plan(r, d, nbytes, count))
+    try:
+        for ep in (1, 2):
+            bound.buffer("SEND").view(torch.int32).copy_(pattern(r, nbytes, ep).to(dev))
+            bound.buffer("RSIN").view(torch.float32).copy_(rs_input(r, d, count).to(dev))
+            torch.cuda.synchronize(dev)
+            bound.run()
+            torch.cuda.synchronize(dev)
+            ag = bound.buffer("AG").view(torch.int32)
+            for q in range(d):
+                _check_eq(ag[q * nbytes // 4:(q + 1) * nbytes // 4],
+                          pattern(q, nbytes, ep), f"all-gather slot of rank {q}")
+            _check_eq(bound.buffer("RSOUT").view(torch.float32)[:count],
+                      rs_expected(r, d, count), "reduce-scatter")
+            comm.barrier()
+    finally:
+        bound.close()
 
 
 def run_rccl_checks(comm, phases=RCCL_PHASES, progress_path: Optional[str] = None,
                     nbytes: int = PATTERN_BYTES, count: int = RS_COUNT) -> Dict[str, str]:
-    import torch
-    import torch.distributed as dist
-
-    prog = _Progress(progress_path)
-    r, d = comm.rank, comm.world_size
-    dev = comm.device
-    if "torch_nccl" in phases:
-        def torch_pg():
-            if dist.get_backend() == "nccl":
-                grp = None
-            else:  # control plane forced to gloo: build a separate RCCL group
-                grp = dist.new_group(backend="nccl")
-            t = torch.full((1024,), float(r + 1), device=dev)
-            dist.all_reduce(t, group=grp)
-            torch.cuda.synchronize(dev)
-            want = torch.full((1024,), float(d * (d + 1) // 2))
-            _check_eq(t, want, "all_reduce")
-            if grp is not None:
-                dist.destroy_process_group(grp)
-
-        _run_checked("torch_nccl", prog, torch_pg)
-    if "rccl" in phases:
-        def own():
-            ctx = comm.native()
-            bound = ctx.bind(build_rccl_plan(r, d, nbytes, count))
-            try:
-                for ep in (1, 2):
-                    bound.buffer("SEND").view(torch.int32).copy_(pattern(r, nbytes, ep).to(dev))
-                    bound.buffer("RSIN").view(torch.float32).copy_(rs_input(r, d, count).to(dev))
-                    torch.cuda.synchronize(dev)
-                    bound.run()
-                    torch.cuda.synchronize(dev)
-                    ag = bound.buffer("AG").view(torch.int32)
-                    for q in range(d):
-                        _check_eq(ag[q * nbytes // 4:(q + 1) * nbytes // 4],
-                                  pattern(q, nbytes, ep), f"all-gather slot of rank {q}")
-                    _check_eq(bound.buffer("RSOUT").view(torch.float32)[:count],
-                              rs_expected(r, d, count), "reduce-scatter")
-                    comm.barrier()
-            finally:
-                bound.close()
-
-        _run_checked("rccl", prog, own)
-    if "rccl_fused" in phases:
-        _run_checked("rccl_fused", prog, lambda: run_primitive_check(comm, "rccl_fused"))
-    return prog.res
+    """Every RCCL phase, in ``RCCL_PHASES`` order: torch's group, our communicator, the RCCL-fed
+    gated GEMM and its CU-split form (``rccl_fused_cm``: a plain fused hang must not drop it)."""
+    return _run_family(comm, "rccl", phases, progress_path, nbytes=nbytes, count=count)
 
 
 def families_ok(results: Dict[str, str]) -> Dict[str, bool]:
@@ -357,6 +397,8 @@ def needs(impl: str, opts: Dict, primitive: str = "tp_columnwise") -> List[str]:
     proto = opts.get("multicast_protocol", "memcpy")
     if alg == "direct" or proto == "kernel":
         out.append("ipc_kernel")   # peer HBM read by CUs (copy kernel, in-kernel AG, LDS-DMA)
+    elif proto == "batch_memcpy":
+        out.append("ipc_batch")
     elif opts.get("direction") == "push":
         out.append("ipc_push")
     else:

@@ -130,11 +130,15 @@ def test_candidate_pools():
 
     col8 = bench.candidate_pool("tp_columnwise", "bfloat16", 8)
     assert any(c[0] == "direct/ipc" for c in col8) and all(c[0][:4] != "row/" for c in col8)
-    # the families interleaved by the per-rank budget: the RCCL-fed fused GEMM, the in-kernel
-    # all-gather and direct/ipc lead; the vendor slot last; no vendor-library GEMM behind native
+    # the forms that cannot hang by construction lead (direct/ipc, the in-kernel all-gather),
+    # then the CTA-capped RCCL-fed fused GEMM; the vendor slot last; no vendor-library GEMM
+    # behind native; dominated / host-bound forms only on request (extra)
     natives = [c for c in col8 if c[1] == "native"]
-    assert [c[0] for c in natives[:3]] == ["coll_pipeline/rccl/s4/fused",
-                                           "coll_pipeline/ipc/agk32/s4/graph", "direct/ipc"]
+    assert [c[0] for c in natives[:3]] == ["direct/ipc", "coll_pipeline/ipc/agk32/s4/graph",
+                                           "coll_pipeline/rccl/s4/fused"]
+    assert not any(c[2].get("multicast_protocol") == "batch_memcpy" for c in col8)
+    extra = bench.candidate_pool("tp_columnwise", "bfloat16", 8, extra=True)
+    assert len(extra) > len(col8) and {c[0] for c in col8} <= {c[0] for c in extra}
     assert col8[-1][1] == "pytorch"
     assert {c[2]["backend"] for c in natives[:5]} == {"rccl", "ipc"}
     for pool in (col8, bench.candidate_pool("tp_rowwise", "bfloat16", 8),
@@ -348,3 +352,52 @@ def test_fused_rccl_hangs_do_not_drop_plain_rccl():
     chosen, _ = bench.autotune(job, pool, _args(), 8, tune, {})
     assert chosen[0] == "r"
     assert "rccl_fused candidates timed out twice" in tune["f3"]
+
+
+def _budget_run(pool, hang, t_ok=10.0, t_hang=45.0, budget=300.0, world=8, primitive=None):
+    """autotune over ``pool`` on a scripted clock: every candidate takes t_ok s, the ``hang``
+    labels time out after t_hang s."""
+    import bench
+
+    clock = [0.0]
+    job = _FakeJob(pool, {})
+
+    def measure(impl, opts, steps, warmup, validate, timeout, prewarm_ms=0.0, harness_iters=0):
+        label = job.by_opts[json.dumps(opts, sort_keys=True)]
+        job.calls.append((label, validate))
+        if label in hang:
+            clock[0] += t_hang
+            return {"ok": False, "error": f"timeout after {t_hang:.0f}s"}
+        clock[0] += t_ok
+        return _ok(1.0 + 0.01 * len(job.calls))
+
+    job.measure = measure
+    kw = dict(tune_budget_s=budget, tune_cap_s=360.0, final_reserve_s=100.0)
+    if primitive:
+        kw["primitive"] = primitive
+    orig = bench.time.time
+    bench.time.time = lambda: clock[0]
+    try:
+        tune = {}
+        bench.autotune(job, pool, _args(**kw), world, tune, {})
+    finally:
+        bench.time.time = orig
+    return tune, clock[0]
+
+
+def test_pool_fits_tuning_budget():
+    """at N = 8 every default pool (columnwise bf16 / fp8, rowwise) is tried in full
+    inside --tune-budget-s (300 s) even when two candidates hang for the whole candidate timeout
+    (45 s) and every other one takes 10 s (2-rank rehearsals: ~3 s per candidate)."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    for prim, dt in [("tp_columnwise", "bfloat16"), ("tp_columnwise", "float8_e4m3fn"),
+                     ("tp_rowwise", "bfloat16")]:
+        pool = bench.candidate_pool(prim, dt, 8)
+        natives = [c[0] for c in pool if c[1] == "native"]
+        # worst case: the two hangs are the last natives (nothing is skipped after them)
+        tune, spent = _budget_run(pool, set(natives[-2:]), primitive=prim)
+        skipped = [k for k, v in tune.items() if isinstance(v, str) and "deadline" in v]
+        assert not skipped, (prim, dt, len(pool), spent, skipped)
+        assert spent <= 300.0 + 45.0, (prim, dt, spent)

@@ -390,6 +390,11 @@ def test_rccl_data_plane_world1(comm, mode):
         info = {i: (fl, pr) for i, fl, pr in bound.ex.stream_info()}
         assert set(info) == {1, -1}, info
         print("cu-masked stream flags / priority:", info)
+        # hipExtStreamCreateWithCUMask takes no flags or priority: masked streams are default
+        # (blocking) streams at normal priority. The executor relies on neither (fork / join by
+        # events, nothing on the legacy null stream inside a run) and the cumask candidates say
+        # so (bench.py); the priority an unmasked comm stream gets is absent here by construction
+        assert all(pr == 0 for _, pr in info.values()), info
     if graph:  # RCCL plans are not captured (replaying captured RCCL calls crashed here)
         assert not bound.ex.graph_capturable()
         with pytest.raises(RuntimeError):
@@ -682,12 +687,64 @@ def test_a_table_gemm_world1(comm, tile, dt, mode):
     ctx.close()
 
 
+def test_gemm_first_queue_pools():
+    """The premise of ``algorithms._gemm_first``: HIP keeps separate hardware-queue
+    pools per stream priority, so a gated GEMM on a normal-priority stream enqueued BEFORE the
+    signal kernel that raises its flags on a high-priority stream completes even with ONE
+    hardware queue per pool (GPU_MAX_HW_QUEUES=1); the same order on two normal-priority streams
+    sharing that queue is what the rule avoids (reported, not asserted: its bounded spins only
+    give up after seconds)."""
+    from conftest import free_port
+
+    res = {}
+    for prio in ("0,1", "0,0"):
+        env = dict(os.environ, GPU_MAX_HW_QUEUES="1", DDLB_TEST_PRIO=prio,
+                   DDLB_CHILD_INIT_METHOD=f"tcp://127.0.0.1:{free_port()}")
+        for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+            env.pop(k, None)
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "_queue_prio_worker.py")],
+                           capture_output=True, text=True, timeout=100, env=env)
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        assert r.returncode == 0 and lines, (prio, r.stdout[-2000:], r.stderr[-3000:])
+        res[prio] = json.loads(lines[-1])
+    print("gated GEMM first, one HW queue per pool:", res)
+    assert res["0,1"]["timeout"] == 0 and res["0,1"]["err"] < 0.5, res
+
+
+@pytest.mark.parametrize("s", [1, 2])
+def test_gated_pt4_own_shard_needs_table_a(comm, s):
+    """tile_order 3 ("own rows never gated") exists only in the table-A gated pt4 kernel: on
+    plain A rows the launch is refused instead of spinning on an own flag nobody raises
+    (the p2p RCCL-fed plan before its row table)."""
+    from ddlb_amd.parallel.context import NativeContext
+    from ddlb_amd.parallel.plan import DT_BF16, Plan
+
+    M, N, K = 2048, 256, 256
+    plan = Plan(0, 1, nstreams=1)
+    a = plan.buffer("a", M * K * 2)
+    bt = plan.buffer("bt", N * K * 2)
+    c = plan.buffer("c", M * N * 2)
+    fl = plan.buffer("flags", 256, zero=True)
+    plan.gemm(0, a, bt, c, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, din=DT_BF16, dout=DT_BF16,
+              tile=19, flags=fl, flag_rows=M // (2 * s), nshards=2 * s, nsub=s, tile_order=3,
+              reserve_cus=32)
+    ctx = NativeContext(comm)
+    bound = ctx.bind(plan)
+    with pytest.raises(RuntimeError):
+        bound.run()
+        torch.cuda.synchronize()
+    bound.check_health()
+    bound.close()
+    ctx.close()
+
+
 @pytest.mark.parametrize("shape", [(32768, 1024, 1024), (1024, 256, 256)])
 @pytest.mark.parametrize("first", [False, True])
 @pytest.mark.parametrize("dt,mode", [("bf16", 0), ("fp8", 2)])
-@pytest.mark.parametrize("s", [2, 4])
+@pytest.mark.parametrize("s", [1, 2, 4])
 def test_rccl_fed_gated_gemm_world1(comm, dt, mode, s, first, shape):
-    """The RCCL-fed coll_pipeline's fused GEMM in one process: stage j's (world-1) RCCL
+    """The RCCL-fed coll_pipeline's (s = 1: p2p_pipeline's) fused GEMM in one process: stage
+    j's (world-1) RCCL
     all-gather lands the "peer" rows in a stage-major gather buffer, a signal kernel on the comm
     stream raises their ARRIVE flag, and ONE gated persistent pt4 reads A through a row-block
     table: the own blocks in place (never gated, dispatched first: tile_order 3), the peer
@@ -707,6 +764,7 @@ def test_rccl_fed_gated_gemm_world1(comm, dt, mode, s, first, shape):
     if rows % 256:
         pytest.skip("the fused GEMM's stage blocks are whole 256-row tiles")
     plan = Plan(0, 1, nstreams=2, stream_priority=[0, 1])
+    plan.meta["rccl_max_ctas"] = 32  # the binder refuses an RCCL-fed gate without a CTA cap
     own = plan.buffer("own", ml * K * es)
     peer = plan.buffer("peer", ml * K * es)  # stands in for the peer's shard (its send buffer)
     G = plan.buffer("G", ml * K * es)
@@ -910,7 +968,13 @@ def test_bench_preflight_shared_gpu():
     pre = json.loads(lines[0])["preflight"]
     for ph in ("ipc", "ipc_ksig", "ipc_kernel", "ipc_sdma", "ipc_push"):
         assert pre[ph].startswith("ok"), (ph, pre, r.stderr[-3000:])
-    assert set(pre) >= {"rccl", "torch_nccl"}
+    assert set(pre) >= {"rccl", "torch_nccl", "rccl_fused", "rccl_fused_cm", "ipc_batch"}
+    # every RCCL phase ran and reports RCCL's own refusal (two ranks on one device), none is a
+    # phase that was never executed (rccl_fused_cm read 'failed: timeout')
+    for ph in ("rccl", "rccl_fused", "rccl_fused_cm"):
+        assert pre[ph] != "failed: timeout", (ph, pre)
+    # batched copies: ok where hipMemcpyBatchAsync exists, else its own reason (never a timeout)
+    assert pre["ipc_batch"].startswith("ok") or "batched copies" in pre["ipc_batch"], pre
 
 
 def test_side_stream_cycle_is_not_captured():

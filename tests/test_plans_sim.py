@@ -242,7 +242,8 @@ def test_invalid_configs():
 
 
 def _bench_native_cfgs():
-    """(primitive, label, AlgoConfig) of every native candidate bench.py can pick at world > 1."""
+    """(primitive, label, AlgoConfig) of every native candidate bench.py can pick at world > 1
+    (the default pool and the --candidates extras)."""
     import os
     import sys
 
@@ -253,7 +254,7 @@ def _bench_native_cfgs():
 
     out = []
     for prim in ("tp_columnwise", "tp_rowwise"):
-        for label, impl, opts in bench.candidate_pool(prim, "bfloat16", 8):
+        for label, impl, opts in bench.candidate_pool(prim, "bfloat16", 8, extra=True):
             if impl != "native":
                 continue
             cls, o, _ = resolve(prim, impl, dict(opts))
@@ -480,3 +481,65 @@ def test_gate_reserve_floor():
             plan, _ = build_tp_columnwise(0, 4, 64, 8, 8, DT_F32, DT_F32, cfg)
             g = [op for op in plan.ops if op.kind == OP_GEMM and op.args["flags"] is not None]
             assert g and all(op.args["reserve_cus"] == want for op in g), (alg, be, req)
+
+
+@pytest.mark.parametrize("alg,s", [("coll_pipeline", 2), ("coll_pipeline", 4), ("p2p_pipeline", 1)])
+@pytest.mark.parametrize("reserve", [0, 32, 48])
+def test_rccl_fed_gate_caps_the_communicator(alg, s, reserve):
+    """The RCCL-fed gated GEMM's communicator launches at most reserve_cus workgroups: the plan
+    records the cap, the binder's check derives it (GEMM grid + RCCL grid <= num_cus by
+    construction) and refuses a plan whose cap is missing or above the reserve."""
+    import copy
+
+    from ddlb_amd.parallel.context import rccl_gate_cap
+
+    cfg = AlgoConfig(algorithm=alg, backend="rccl", fused=True, s=s, reserve_cus=reserve)
+    for d in (2, 8):
+        plan, _ = build_tp_columnwise(1, d, 512 * d, 256, 256, DT_F32, DT_F32, cfg)
+        want = max(reserve, 32)
+        assert plan.meta["rccl_max_ctas"] == want
+        assert rccl_gate_cap(plan) == want
+        for bad in (0, want + 1):
+            p2 = copy.copy(plan)
+            p2.meta = dict(plan.meta, rccl_max_ctas=bad)
+            with pytest.raises(ValueError, match="CTA cap"):
+                rccl_gate_cap(p2)
+    # a CU split keeps RCCL's default (the collectives own their CUs)
+    cm = AlgoConfig(algorithm=alg, backend="rccl", fused=True, s=s, comm_cus=32)
+    plan, _ = build_tp_columnwise(0, 4, 2048, 256, 256, DT_F32, DT_F32, cm)
+    assert plan.meta["rccl_max_ctas"] == 0 and rccl_gate_cap(plan) == 0
+    # plans without a gated GEMM fed by RCCL need no cap
+    for c in (AlgoConfig(algorithm=alg, backend="rccl", s=s),
+              AlgoConfig(algorithm=alg, backend="ipc", fused=True, s=s)):
+        plan, _ = build_tp_columnwise(0, 4, 2048, 256, 256, DT_F32, DT_F32, c)
+        assert rccl_gate_cap(plan) == 0
+
+
+def test_rccl_fed_p2p_reads_a_through_a_table():
+    """the p2p RCCL-fed gated GEMM's own shard is never gated only in the
+    table-A kernel; the plan gives it a row-block table and never raises ARRIVE[rank]."""
+    d, m = 4, 4096
+    cfg = AlgoConfig(algorithm="p2p_pipeline", backend="rccl", fused=True)
+    for r in range(d):
+        plan, _ = build_tp_columnwise(r, d, m, 256, 256, DT_F32, DT_F32, cfg)
+        g = [op for op in plan.ops if op.kind == OP_GEMM]
+        assert len(g) == 1 and g[0].args["tile_order"] == 3 and g[0].args["first_shard"] == r
+        assert g[0].args["shard_rows"] == m // d and len(g[0].args["a_shards"]) == d
+        raised = [ref for op in plan.ops if op.kind == OP_SIGNAL for ref in op.args["flags"]]
+        assert raised and all(ref.off != 4 * (2 * d + 2 * d + r) for ref in raised)
+
+
+def test_gemm_first_only_on_separate_queues(monkeypatch):
+    """the gated GEMM goes ahead of its producers only when its stream (normal
+    priority) and theirs (high priority: another hardware-queue pool) cannot share a queue."""
+    cfg = AlgoConfig(algorithm="coll_pipeline", backend="rccl", fused=True, s=2)
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    plan, _ = build_tp_columnwise(0, 2, 2048, 256, 256, DT_F32, DT_F32, cfg)
+    assert plan.meta["gemm_first"] and plan.ops[0].kind == OP_GEMM
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "1")
+    plan, _ = build_tp_columnwise(0, 2, 2048, 256, 256, DT_F32, DT_F32, cfg)
+    assert not plan.meta["gemm_first"] and plan.ops[-1].kind == OP_GEMM
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    off = AlgoConfig(algorithm="p2p_pipeline", backend="rccl", fused=True, gemm_first=False)
+    plan, _ = build_tp_columnwise(0, 2, 2048, 256, 256, DT_F32, DT_F32, off)
+    assert not plan.meta["gemm_first"] and plan.ops[-1].kind == OP_GEMM

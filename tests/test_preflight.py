@@ -22,7 +22,7 @@ def test_ipc_plan_moves_every_peers_pattern(d, phase):
             bufs[r]["X"].view(torch.int32)[:] = pf.pattern(r, NB, ep)
             bufs[r]["R"].view(torch.int32).fill_(-1)
         sim.run_epoch()
-        if phase in ("ipc_kernel", "ipc_sdma", "ipc_push"):
+        if phase in ("ipc_kernel", "ipc_sdma", "ipc_push", "ipc_batch"):
             for r in range(d):
                 rv = bufs[r]["R"].view(torch.int32)
                 for p in range(d):
@@ -75,6 +75,8 @@ def test_needs_maps_candidates_to_checks():
     assert dstore == ["ipc", "ipc_ksig", "ipc_sdma", "ipc_dstore"]
     assert "ipc_kernel" in pf.needs("native", {"backend": "ipc", "algorithm": "direct"})
     assert "ipc_push" in pf.needs("native", {"backend": "ipc", "direction": "push"})
+    assert pf.needs("native", {"backend": "ipc", "multicast_protocol": "batch_memcpy",
+                               "graph": False}) == ["ipc", "ipc_batch"]
     assert pf.needs("compute_only", {}) == []
 
 
@@ -113,3 +115,49 @@ def test_primitive_phases_simulate(d, phase):
     from test_plans_sim import _run_col, _run_row
 
     (_run_col if prim == "tp_columnwise" else _run_row)(d, m, n, k, cfg, epochs=2)
+
+
+@pytest.mark.parametrize("family,phases", [("rccl", pf.RCCL_PHASES), ("ipc", pf.IPC_PHASES)])
+def test_every_declared_phase_has_a_check(family, phases):
+    """A declared phase without a check would be reported 'failed: timeout' on every node and
+    silently drop the candidates that need it (rccl_fused_cm)."""
+    assert sorted(pf.phase_checks(None, family)) == sorted(phases)
+
+
+def test_run_checks_report_every_phase(monkeypatch):
+    """Both families, native layer stubbed: every phase ends with its own status (ok or the
+    check's own error), in order, and 'failed: timeout' can only come from a killed child."""
+
+    class FakeComm:
+        rank, world_size, device = 0, 2, "cpu"
+
+        def native(self):
+            raise RuntimeError("no native layer in this test")
+
+        def barrier(self):
+            pass
+
+    ran = []
+
+    def fake_primitive(comm, phase, epochs=2):
+        ran.append(phase)
+        if phase == "rccl_fused":
+            raise TimeoutError("stand-in for RCCL's own error")
+
+    monkeypatch.setattr(pf, "run_primitive_check", fake_primitive)
+    monkeypatch.setattr(pf, "_torch_nccl_check", lambda comm: None)
+    res = pf.run_rccl_checks(FakeComm())
+    assert list(res) == list(pf.RCCL_PHASES)
+    assert res["torch_nccl"].startswith("ok")
+    assert res["rccl"].startswith("failed: RuntimeError: no native layer")
+    assert res["rccl_fused"].startswith("failed: TimeoutError: stand-in")
+    assert res["rccl_fused_cm"].startswith("ok")
+    assert "rccl_fused_cm" in ran
+    res = pf.run_ipc_checks(FakeComm())
+    assert list(res) == list(pf.IPC_PHASES)
+    for ph in pf.IPC_PHASES:
+        want = "ok" if ph in pf.PRIMITIVE_PHASES else "failed: RuntimeError"
+        assert res[ph].startswith(want), (ph, res[ph])
+        assert res[ph] != "failed: timeout"
+    merged = pf.merge([res, res], pf.IPC_PHASES)
+    assert not any(v == "failed: timeout" for v in merged.values())
