@@ -89,18 +89,21 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm",
         [](uintptr_t a, uintptr_t b, uintptr_t c, int64_t lda, int64_t ldb, int64_t ldc, int M,
            int N, int K, int din, int dout, int tile, int mode, int64_t a_grp, int64_t a_gstride,
-           int64_t c_grp, int64_t c_gstride, uintptr_t stream, int act, int ksplit) {
+           int64_t c_grp, int64_t c_gstride, uintptr_t stream, int act, int ksplit,
+           uintptr_t ks_ws, uintptr_t ks_cnt) {
           GemmArgs g = make_args(a, b, c, lda, ldb, ldc, M, N, K, a_grp, a_gstride, c_grp,
                                  c_gstride);
           g.act = act;
           g.ksplit = ksplit > 1 ? ksplit : 1;
+          g.ks_ws = (float*)ks_ws;
+          g.ks_cnt = (unsigned*)ks_cnt;
           check(gemm_launch(g, din, dout, tile, mode, (hipStream_t)stream), "gemm_launch");
         },
         py::arg("a"), py::arg("b"), py::arg("c"), py::arg("lda"), py::arg("ldb"), py::arg("ldc"),
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("din"), py::arg("dout"),
         py::arg("tile") = 0, py::arg("mode") = 0, py::arg("a_grp") = 0, py::arg("a_gstride") = 0,
         py::arg("c_grp") = 0, py::arg("c_gstride") = 0, py::arg("stream") = 0,
-        py::arg("act") = 0, py::arg("ksplit") = 1);
+        py::arg("act") = 0, py::arg("ksplit") = 1, py::arg("ks_ws") = 0, py::arg("ks_cnt") = 0);
   m.def("gemm_fast_path_ok",
         [](uintptr_t a, uintptr_t b, uintptr_t c, int64_t lda, int64_t ldb, int64_t ldc, int M,
            int N, int K, int din, int dout) {

@@ -47,6 +47,7 @@ struct GemmArgs {
   const unsigned* epoch_ptr = nullptr;  // if set: the epoch is read here (hipGraph replay)
   int64_t flag_rows = 1;            // physical A rows per shard
   unsigned* timeout_word = nullptr; // set to 1 if a spin gave up
+  unsigned spin_limit = 1u << 26;   // polls before a bounded spin gives up (~30 s on uncached flags)
   int tile_order = 0, nshards = 1, first_shard = 0;
   // Row blocks per producer (tile_order): shard index = producer * nsub + block; dispatch is
   // block-major across producers (block 0 of every producer, own first, then block 1, ...),
@@ -80,6 +81,15 @@ struct GemmArgs {
   // c + s * M * ldc elements (the caller sums the partials). pt4 runs every (slice, tile) in one
   // launch; other kernels run the slices one after another.
   int ksplit = 1;
+  // In-launch K-split reduction (optional, with ksplit > 1 on pt4): the S slices of a tile write no
+  // partial to c; each (slice, tile) workgroup counts its arrival in ks_cnt[2 tile] (monotonic
+  // across launches), every slice but the last to arrive stores its f32 partial at
+  // ks_ws + slice * M * N floats (row pitch N) and counts it done in ks_cnt[2 tile + 1]; the last
+  // arrival waits for those (already running, so deadlock-free), sums all S partials in slice order
+  // in f32 (its own from registers) and writes C once, rounded once. ks_cnt: 2 * tiles words,
+  // zeroed once and never reset.
+  float* ks_ws = nullptr;
+  unsigned* ks_cnt = nullptr;
 };
 enum Act : int { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_SILU = 3 };
 // In-kernel all-gather variants (GemmArgs::ag_mode bits; 0 = write-through publication, 8 loads

@@ -94,6 +94,7 @@ hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mo
     default: return hipErrorInvalidValue;
   }
   if (p.M == 0 || p.N == 0) return hipSuccess;
+  if (p.ks_ws != nullptr && (p.ksplit < 2 || p.ks_cnt == nullptr)) return hipErrorInvalidValue;
   if (p.ksplit > 1) {
     // K-split: slice j of K columns -> partial j at c + j * M * ldc (the caller sums them). pt4
     // runs every (slice, tile) pair in one launch; any other kernel runs the slices one by one.
@@ -109,6 +110,8 @@ hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mo
       else if (fast) e = launch_fast(q, din, dout, TILE_PT4, s);
       if (e != hipErrorNotSupported && e != hipErrorInvalidValue) return e;
     }
+    // the in-launch reduction (ks_ws) exists only in pt4: never fall back to partial slabs in C
+    if (p.ks_ws != nullptr) return hipErrorNotSupported;
     const int esz = dtype_size(din), osz = dtype_size(dout);
     for (int j = 0; j < p.ksplit; ++j) {
       GemmArgs q = p;

@@ -556,7 +556,13 @@ GemmArgs PlanExecutor::gemm_args(const int64_t* o) const {
   g.c_table = (const uint64_t*)o[32];
   g.c_shard_rows = o[33];
   g.ksplit = o[31] > 1 ? (int)o[31] : 1;
+  g.ks_ws = (float*)o[34];
+  g.ks_cnt = (unsigned*)o[35];
   g.timeout_word = d_timeout_;
+  // DDLB_SPIN_LIMIT: polls before a gated GEMM's bounded spin gives up (diagnostics that provoke
+  // a blocked producer on purpose, scripts/diag_gate_placement.py); default ~30 s
+  static const unsigned spin_env = getenv("DDLB_SPIN_LIMIT") ? (unsigned)atol(getenv("DDLB_SPIN_LIMIT")) : 0u;
+  if (spin_env > 0) g.spin_limit = spin_env;
   g.epoch_ptr = graph_on_ ? d_epoch_ : nullptr;
   return g;
 }

@@ -20,7 +20,7 @@
 namespace ddlb {
 
 // Op layout: kOpWords int64 per op. word 0 = kind, word 1 = stream index.
-constexpr int kOpWords = 34;
+constexpr int kOpWords = 36;
 enum OpKind : int64_t {
   OP_NOP = 0,
   OP_GEMM = 1,        // 2 a, 3 b, 4 c, 5 lda, 6 ldb, 7 ldc, 8 a_grp, 9 a_gstride, 10 c_grp,
@@ -29,7 +29,8 @@ enum OpKind : int64_t {
                       // 23 tile_order, 24 fused epilogue activation, 25 A shard table,
                       // 26 A shard rows, 27 nsub, 28 reserve_cus, 29 in-kernel all-gather
                       // (ctas | parts << 20 | rank << 40 | mode << 56), 30 its table,
-                      // 31 K-split slices, 32 C shard table (direct store), 33 C shard rows
+                      // 31 K-split slices, 32 C shard table (direct store), 33 C shard rows,
+                      // 34 K-split f32 workspace (in-launch reduction), 35 its tile counters
   OP_RECORD = 2,      // 2 event
   OP_WAIT = 3,        // 2 event
   OP_ALLGATHER = 4,   // 2 send, 3 recv, 4 count per rank, 5 dtype

@@ -97,7 +97,7 @@ def device_cus() -> int:
 def split_k_factor(M: int, N: int, K: int, esz: int, ncu: int = 0) -> int:
     """K-slices for a GEMM whose 256x256 grid covers at most half the CUs and whose K is long
     (e.g. 8192 x 1024 x 8192: 128 tiles): ``S`` slices run as (slice, tile) pairs of ONE pt4
-    launch (``GemmArgs::ksplit``) and their partials are summed by one reduce kernel. Each slice
+    launch (``GemmArgs::ksplit``) that also reduces them (``GemmArgs::ks_ws``). Each slice
     keeps >= 16 K-tiles (the fixed per-tile cost stays small, profiles/r04/r4_15_*); measured
     on the config #2 shape: 0.1009 ms vs 0.1338 unsplit (profiles/r04/r4_22_*). 1 = no split."""
     if M % 256 or N % 256 or M <= 0 or N <= 0:
@@ -147,16 +147,33 @@ def gemm(a, w, out=None, *, out_dtype=None, tile: str = "auto", mode: str = "aut
     if S == 0:
         S = split_k_factor(M, N, K, a.element_size()) if plain and tile == "auto" else 1
     if S > 1:
-        if not plain or K % S:
-            raise ValueError("ksplit needs plain rows, no activation, a dense output and S | K")
-        part = torch.empty((S, M, N), dtype=out.dtype, device=a.device)
-        C.gemm(a.data_ptr(), w.data_ptr(), part.data_ptr(), a.stride(0), w.stride(0), N, M, N,
+        if not plain or K % S or M % 256 or N % 256:
+            raise ValueError("ksplit needs plain rows, no activation, a dense output, whole "
+                             "256x256 tiles and S | K")
+        if tile not in ("auto", "pt4"):
+            # another kernel runs the slices one after another into output-dtype partials,
+            # summed (f32) by a reduce kernel
+            part = torch.empty((S, M, N), dtype=out.dtype, device=a.device)
+            C.gemm(a.data_ptr(), w.data_ptr(), part.data_ptr(), a.stride(0), w.stride(0), N, M,
+                   N, K // S, dtype_code(a.dtype), dtype_code(out.dtype), TILES[tile],
+                   MODES[mode], 0, 0, 0, 0, s, 0, S)
+            C.reduce_sum(out.data_ptr(), [part[j].data_ptr() for j in range(S)], M * N,
+                         dtype_code(out.dtype), s)
+            if stream is not None:
+                part.record_stream(torch.cuda.ExternalStream(s))
+            return out
+        # pt4: one launch; the slices' f32 partials meet in a workspace and the last slice of
+        # each tile writes out (csrc/gemm/gemm.h ks_ws); fresh zeroed tile counters per call,
+        # so concurrent calls on different streams never share them
+        ws = torch.empty((S, M, N), dtype=torch.float32, device=a.device)
+        cnt = torch.zeros((2 * (M // 256) * (N // 256),), dtype=torch.int32, device=a.device)
+        C.gemm(a.data_ptr(), w.data_ptr(), out.data_ptr(), a.stride(0), w.stride(0), N, M, N,
                K // S, dtype_code(a.dtype), dtype_code(out.dtype),
-               TILES["pt4" if tile == "auto" else tile], MODES[mode], 0, 0, 0, 0, s, 0, S)
-        C.reduce_sum(out.data_ptr(), [part[j].data_ptr() for j in range(S)], M * N,
-                     dtype_code(out.dtype), s)
+               TILES["pt4" if tile == "auto" else tile], MODES[mode], 0, 0, 0, 0, s, 0, S,
+               ws.data_ptr(), cnt.data_ptr())
         if stream is not None:  # the workspace stays allocated until that stream reaches it
-            part.record_stream(torch.cuda.ExternalStream(s))
+            ws.record_stream(torch.cuda.ExternalStream(s))
+            cnt.record_stream(torch.cuda.ExternalStream(s))
         return out
     C.gemm(a.data_ptr(), w.data_ptr(), out.data_ptr(), a.stride(0), w.stride(0), out.stride(0),
            M, N, K, dtype_code(a.dtype), dtype_code(out.dtype), TILES[tile], MODES[mode],

@@ -181,18 +181,19 @@ def _split_k(plan: Plan, M: int, N: int, K: int, ein: int, cfg: AlgoConfig) -> i
 
 def _full_gemm(plan: Plan, a_ref: Ref, Bt: Ref, c_ref: Ref, M: int, N: int, K: int, ein: int,
                eout: int, cfg: AlgoConfig, gdt: dict, tag: str = "KS") -> None:
-    """C[M, N] = A[M, K] Bt^T on stream 0, K-split when :func:`_split_k` says so: ONE launch
-    writes the S partials (slice s = K/S columns of A and Bt) to a scratch buffer, then a reduce
-    op sums them into C (the partials in the output dtype, summed in f32: the rowwise
-    reduce-scatter's rule)."""
+    """C[M, N] = A[M, K] Bt^T on stream 0, K-split when :func:`_split_k` says so: ONE launch runs
+    the S (slice, tile) pairs and reduces them itself (slice s = K/S columns of A and Bt): per
+    tile, the last slice to arrive sums the others' f32 partials from a workspace with its own,
+    in slice order, and writes C once (csrc/gemm/gemm.h ``ks_ws``). No reduce pass, no
+    output-dtype partials (one rounding, as an unsplit GEMM)."""
     S = _split_k(plan, M, N, K, ein, cfg)
     if S == 1:
         plan.gemm(S_MAIN, a_ref, Bt, c_ref, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, **gdt)
         return
-    part = plan.buffer(tag, S * M * N * eout)
-    plan.gemm(S_MAIN, a_ref, Bt, part, M=M, N=N, K=K // S, lda=K, ldb=K, ldc=N, ksplit=S,
-              **dict(gdt, tile=TILE_PT4))
-    plan.reduce(S_MAIN, c_ref, [part + j * M * N * eout for j in range(S)], M * N, gdt["dout"])
+    ws = plan.buffer(tag, S * M * N * 4)
+    cnt = plan.buffer(tag + "_cnt", max(256, 8 * (M // 256) * (N // 256)), zero=True)
+    plan.gemm(S_MAIN, a_ref, Bt, c_ref, M=M, N=N, K=K // S, lda=K, ldb=K, ldc=N, ksplit=S,
+              ks_ws=ws, ks_cnt=cnt, **dict(gdt, tile=TILE_PT4))
 
 
 # A flag-gated persistent GEMM fed by other kernels (RCCL, copy / signal kernels) leaves at least

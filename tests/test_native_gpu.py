@@ -889,20 +889,96 @@ def test_ksplit_gemm_partials(comm, S, tile, dt, mode):
     ctx.close()
 
 
+@pytest.mark.parametrize("S", [2, 4])
+@pytest.mark.parametrize("shape", [(1024, 512, 4096), (8192, 1024, 8192), (512, 256, 2048)])
+@pytest.mark.parametrize("dt,mode,dout", [("bf16", 0, "bf16"), ("bf16", 0, "f32"),
+                                          ("fp8", 2, "bf16"), ("fp8", 0, "bf16")])
+def test_ksplit_reduced_in_launch(comm, S, shape, dt, mode, dout):
+    """GemmArgs::ks_ws: ONE pt4 launch runs the S K-slices of every tile and reduces them itself
+    (the last slice of a tile to arrive sums the others' f32 partials with its own, in slice
+    order, and writes C once). Against the fp32 full-K product with the tight bound (one
+    rounding, as an unsplit GEMM); repeat launches on the SAME never-reset counters (epochs
+    2..11) bit-identical; every partial-slab byte of the workspace is overwritten by a run."""
+    from ddlb_amd.parallel.context import NativeContext
+    from ddlb_amd.parallel.plan import DT_BF16, DT_F32, DT_FP8, Plan
+
+    din = DT_FP8 if dt == "fp8" else DT_BF16
+    tdt = torch.float8_e4m3fn if dt == "fp8" else torch.bfloat16
+    odt, dcode = (torch.float32, DT_F32) if dout == "f32" else (torch.bfloat16, DT_BF16)
+    es = 1 if dt == "fp8" else 2
+    M, N, K = shape
+    if (K * es // 128) % (2 * S):
+        pytest.skip("each slice needs an even number of 128-byte K-tiles")
+    ks = K // S
+    tiles = (M // 256) * (N // 256)
+    plan = Plan(0, 1, nstreams=1, stream_priority=[0])
+    a = plan.buffer("a", M * K * es)
+    b = plan.buffer("b", N * K * es)
+    c = plan.buffer("c", M * N * odt.itemsize)
+    ws = plan.buffer("ws", S * M * N * 4)
+    cnt = plan.buffer("cnt", max(256, 8 * tiles), zero=True)
+    plan.gemm(0, a, b, c, M=M, N=N, K=ks, lda=K, ldb=K, ldc=N, din=din, dout=dcode, tile=19,
+              mode=mode, ksplit=S, ks_ws=ws, ks_cnt=cnt)
+    ctx = NativeContext(comm)
+    bound = ctx.bind(plan)
+    A = (torch.rand(M, K, device="cuda") * 2 - 1).to(tdt)
+    W = (torch.rand(N, K, device="cuda") * 2 - 1).to(tdt)
+    bound.buffer("a").view(tdt).view(M, K).copy_(A)
+    bound.buffer("b").view(tdt).view(N, K).copy_(W)
+    out = bound.buffer("c").view(odt).view(M, N)
+    out.fill_(float("nan"))
+    bound.buffer("ws").view(torch.float32).fill_(float("nan"))
+    bound.run()
+    torch.cuda.synchronize()
+    bound.check_health()
+    first = out.clone()
+    ref = A.float() @ W.float().T
+    err = float((first.float() - ref).abs().max())
+    assert err <= _tight(ref, K), err
+    for _ in range(10):
+        bound.run()
+    torch.cuda.synchronize()
+    bound.check_health()
+    assert torch.equal(out, first)
+    counts = bound.buffer("cnt").view(torch.int32)[:2 * tiles].view(tiles, 2).cpu()
+    assert torch.equal(counts[:, 0], torch.full((tiles,), 11 * S, dtype=torch.int32))
+    assert torch.equal(counts[:, 1], torch.full((tiles,), 11 * (S - 1), dtype=torch.int32))
+    bound.close()
+    ctx.close()
+
+
+def test_ksplit_reduced_ops_gemm(comm):
+    """The public op takes the in-launch reduction for auto-split shapes (config #2's GEMM)."""
+    from ddlb_amd.ops.gemm import gemm, split_k_factor
+
+    M, N, K = 8192, 1024, 8192
+    assert split_k_factor(M, N, K, 2) == 2
+    A = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+    W = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
+    out = gemm(A, W)
+    torch.cuda.synchronize()
+    ref = A.float() @ W.float().T
+    assert float((out.float() - ref).abs().max()) <= _tight(ref, K)
+    assert torch.equal(gemm(A, W), out)
+    t4 = gemm(A, W, tile="t4", ksplit=2)  # the slice-by-slice partial form stays available
+    torch.cuda.synchronize()
+    assert float((t4.float() - ref).abs().max()) <= _tight(ref, K)
+
+
 @pytest.mark.parametrize("dtype,mode", [("bfloat16", "auto"), ("float8_e4m3fn", "auto"),
                                         ("float8_e4m3fn", "mx")])
 def test_split_k_world1_native(comm, dtype, mode):
     """BASELINE config #2's full GEMM (8192 x 1024 x 8192: 128 tiles of 256²) runs K-split: ONE
-    pt4 launch over (slice, tile) pairs writing two partials, summed by the reduce op; validated
-    by the primitive (fp32 reference) and repeat-identical."""
+    pt4 launch over (slice, tile) pairs that also reduces them (no reduce op); validated by the
+    primitive (fp32 reference) and repeat-identical."""
     from ddlb_amd.parallel.plan import OP_GEMM, OP_REDUCE
     from ddlb_amd.primitives.tp_columnwise.native import NativeTPColumnwise
 
     impl = NativeTPColumnwise(m=8192, n=1024, k=8192, dtype=dtype, gemm_mode=mode)
     ops = impl.bound.plan.ops
     g = [op for op in ops if op.kind == OP_GEMM]
-    assert len(g) == 1 and g[0].args["ksplit"] == 2
-    assert sum(op.kind == OP_REDUCE for op in ops) == 1
+    assert len(g) == 1 and g[0].args["ksplit"] == 2 and g[0].args["ks_ws"] is not None
+    assert sum(op.kind == OP_REDUCE for op in ops) == 0
     out = impl.run()
     torch.cuda.synchronize()
     impl.validate(out)
