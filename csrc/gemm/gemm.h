@@ -85,9 +85,9 @@ struct GemmArgs {
   // partial to c; each (slice, tile) workgroup counts its arrival in ks_cnt[2 tile] (monotonic
   // across launches), every slice but the last to arrive stores its f32 partial at
   // ks_ws + slice * M * N floats (row pitch N) and counts it done in ks_cnt[2 tile + 1]; the last
-  // arrival waits for those (already running, so deadlock-free), sums all S partials in slice order
-  // in f32 (its own from registers) and writes C once, rounded once. ks_cnt: 2 * tiles words,
-  // zeroed once and never reset.
+  // arrival waits for those (already running, so deadlock-free), sums all S partials in slice
+  // order in f32 (its own from registers) and writes C once, rounded once. ks_cnt: 2 * tiles
+  // words, zeroed once and never reset.
   float* ks_ws = nullptr;
   unsigned* ks_cnt = nullptr;
 };

@@ -556,7 +556,9 @@ template <> struct Store8<DT_F32> {
 // 16384x8192x1024 0.2347 -> 0.2177 ms vs plain nt stores.
 // soff: a wave-uniform part of the offset (SGPR soffset), so a kernel can keep the per-lane part
 // fixed and move only scalars per store (pt4).
-template <int OUT, int AUX = 18>  // 18 = sc1 | nt (16 = sc1 alone: the K-split hand-off)
+// (AUX 18 = sc1 | nt; 16 = sc1 alone, the K-split hand-off. For the C tiles, r5_6 measured nt
+// alone equal to sc1 | nt and sc1 alone 2.5-12 % slower: flagship 0.1118 / 0.1111 / 0.1249 ms)
+template <int OUT, int AUX = 18>
 __device__ __forceinline__ void store8_wt(__amdgpu_buffer_rsrc_t rc, unsigned off, const f32x4 a,
                                           const f32x4 b, unsigned soff = 0) {
   typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
@@ -1406,7 +1408,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     // stored sc1 (write-through) and drained by every storing wave (vmcnt(0)), a workgroup
     // barrier, ONE lane's agent-scope add; the consumer polls the counter, joins a barrier, and
     // reads every partial byte with sc1 buffer loads. An agent release / acquire instead costs a
-    // whole-L2 write-back / invalidate per tile (r5_2: 133 us vs 114 for split + reduce pass).
+    // whole-L2 write-back / invalidate per tile.
     __shared__ unsigned ks_sh[1];  // the tile's arrival ticket, broadcast to every wave
     const int S = p.ksplit;
     const __amdgpu_buffer_rsrc_t wrc =
@@ -1435,7 +1437,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
               store8_wt<DT_F32, 16>(wrc, w_lane, acc[mq * 4 + f][nq * 2],
                                     acc[mq * 4 + f][nq * 2 + 1], w_off(mq, f, nq) + mine);
         wait_vm<0>();
-        __syncthreads();
+        __syncthreads();  // every storing wave has drained its stores
         if (tid == 0)
           __hip_atomic_fetch_add(cnt + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
@@ -1445,14 +1447,24 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
         unsigned spins = 0;
         while (__hip_atomic_load(cnt + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
           __builtin_amdgcn_s_sleep(1);
-          if (++spins > p.spin_limit) {  // (cannot happen: the others are resident) report, drain
+          if (++spins > p.spin_limit) {  // (cannot happen: the others are resident) report
             if (p.timeout_word) atomicOr(p.timeout_word, 32u);
             break;
           }
         }
       }
       __syncthreads();
-      typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
+      auto ld = [&](unsigned o, unsigned extra) __attribute__((always_inline)) {
+        return __builtin_bit_cast(  // sc1 loads: the hand-off's consumer side
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(wrc, w_lane + extra, o, 16));
+      };
+      auto store_c = [&](int mq, int f, int nq, f32x4 v0, f32x4 v1) __attribute__((always_inline)) {
+        const int64_t prow = cm0 + mq * 64 + f * 16;
+        store8_wt<OUT>(crc, c_lane, v0, v1, (unsigned)((prow * p.ldc + cn0 + nq * 32) * OSZ));
+      };
+      // the partials summed in slice order (bit-exact whichever slice arrived last), one quadrant
+      // (8 loads) at a time: a 16-load batch for S = 2 spilled (16 B of scratch) and wrote wrong
+      // rows (r5_6 diag_ksr); this form keeps every value in registers and is exact
 #pragma unroll
       for (int mq = 0; mq < 2; ++mq)
 #pragma unroll
@@ -1469,11 +1481,8 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
             } else {
 #pragma unroll
               for (int f = 0; f < 4; ++f) {
-                const unsigned o = w_off(mq, f, nq) + (unsigned)sl * slab;
-                v0[f] = __builtin_bit_cast(  // sc1 loads: the hand-off's consumer side
-                    f32x4, __builtin_amdgcn_raw_buffer_load_b128(wrc, w_lane, o, 16));
-                v1[f] = __builtin_bit_cast(
-                    f32x4, __builtin_amdgcn_raw_buffer_load_b128(wrc, w_lane + 16, o, 16));
+                v0[f] = ld(w_off(mq, f, nq) + (unsigned)sl * slab, 0);
+                v1[f] = ld(w_off(mq, f, nq) + (unsigned)sl * slab, 16);
               }
             }
 #pragma unroll
@@ -1483,11 +1492,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
             }
           }
 #pragma unroll
-          for (int f = 0; f < 4; ++f) {
-            const int64_t prow = cm0 + mq * 64 + f * 16;
-            store8_wt<OUT>(crc, c_lane, s0[f], s1[f],
-                           (unsigned)((prow * p.ldc + cn0 + nq * 32) * OSZ));
-          }
+          for (int f = 0; f < 4; ++f) store_c(mq, f, nq, s0[f], s1[f]);
         }
     };
     for (ti = 0; ti < my_tiles; ++ti) {

@@ -94,6 +94,9 @@ class AlgoConfig:
     # kernel in the queue, 0.19 vs 0.23 ms (s4) emulated at d = 8 with fast and with link-like
     # slow collectives, profiles/r04/r4_12_ab_*)
     sig_side: bool = False
+    # K-split GEMMs (few tiles, long K): reduce the slices inside the launch (one kernel, f32
+    # partials, one rounding) instead of a reduce op over output-dtype partials (see _full_gemm)
+    ks_fused: bool = False
 
 
 @dataclass
@@ -182,28 +185,59 @@ def _split_k(plan: Plan, M: int, N: int, K: int, ein: int, cfg: AlgoConfig) -> i
 def _full_gemm(plan: Plan, a_ref: Ref, Bt: Ref, c_ref: Ref, M: int, N: int, K: int, ein: int,
                eout: int, cfg: AlgoConfig, gdt: dict, tag: str = "KS") -> None:
     """C[M, N] = A[M, K] Bt^T on stream 0, K-split when :func:`_split_k` says so: ONE launch runs
-    the S (slice, tile) pairs and reduces them itself (slice s = K/S columns of A and Bt): per
-    tile, the last slice to arrive sums the others' f32 partials from a workspace with its own,
-    in slice order, and writes C once (csrc/gemm/gemm.h ``ks_ws``). No reduce pass, no
-    output-dtype partials (one rounding, as an unsplit GEMM)."""
+    the S (slice, tile) pairs (slice s = K/S columns of A and Bt).
+
+    Default: the launch writes S partials (output dtype) to a scratch buffer and a reduce op sums
+    them in f32 into C (BASELINE config #2 shape: 0.1009 ms, r4_22). ``cfg.ks_fused``: the launch
+    reduces them itself (per tile, the last slice to arrive sums the others' f32 partials from a
+    workspace with its own and writes C once: one kernel, one rounding; csrc/gemm/gemm.h
+    ``ks_ws``), measured slower on that shape (0.1249 ms bench, r5_3): every workgroup finishes
+    its single tile together, so the partial stores, the arrival poll and the partial loads
+    form one serial chain at the end of the kernel where the two-kernel form overlaps its
+    stores with the last K-tile and reads back at full bandwidth."""
     S = _split_k(plan, M, N, K, ein, cfg)
     if S == 1:
         plan.gemm(S_MAIN, a_ref, Bt, c_ref, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, **gdt)
         return
-    ws = plan.buffer(tag, S * M * N * 4)
-    cnt = plan.buffer(tag + "_cnt", max(256, 8 * (M // 256) * (N // 256)), zero=True)
-    plan.gemm(S_MAIN, a_ref, Bt, c_ref, M=M, N=N, K=K // S, lda=K, ldb=K, ldc=N, ksplit=S,
-              ks_ws=ws, ks_cnt=cnt, **dict(gdt, tile=TILE_PT4))
+    if cfg.ks_fused:
+        ws = plan.buffer(tag, S * M * N * 4)
+        cnt = plan.buffer(tag + "_cnt", max(256, 8 * (M // 256) * (N // 256)), zero=True)
+        plan.gemm(S_MAIN, a_ref, Bt, c_ref, M=M, N=N, K=K // S, lda=K, ldb=K, ldc=N, ksplit=S,
+                  ks_ws=ws, ks_cnt=cnt, **dict(gdt, tile=TILE_PT4))
+        return
+    part = plan.buffer(tag, S * M * N * eout)
+    plan.gemm(S_MAIN, a_ref, Bt, part, M=M, N=N, K=K // S, lda=K, ldb=K, ldc=N, ksplit=S,
+              **dict(gdt, tile=TILE_PT4))
+    plan.reduce(S_MAIN, c_ref, [part + j * M * N * eout for j in range(S)], M * N, gdt["dout"])
 
 
-# A flag-gated persistent GEMM fed by other kernels (RCCL, copy / signal kernels) leaves at least
-# this many CUs free: the emulated RCCL-fed s4 plan hung with 24 or 16 reserved (grids of 232 /
-# 240 workgroups) and ran with 32 or more (profiles/r04/r4_33_*), so smaller requests are raised.
-MIN_GATE_RESERVE = 32
+# A flag-gated persistent GEMM fed by other kernels (RCCL, copy / signal kernels) must leave one CU
+# free in EVERY shader array: the dispatcher places a kernel's workgroups on the shader arrays in
+# turn and does not move one to another array when its array is full, so a single feeder
+# workgroup assigned to an array whose every CU holds a spinning gated tile blocks the feeder,
+# whatever the other arrays have free. MI355X: 32 arrays (4 per XCD) of 8 active CUs (KFD topology:
+# array_count 32, cu_per_simd_array 9 of which 8 enabled); the gated grid is spread evenly (one
+# workgroup per CU, round-robin), so a reserve of one CU per array (256 / 8 = 32) leaves every array
+# a free CU. Measured (scripts/diag_gate_placement.py, profiles/r05/r5_6_gate_placement.txt): grid
+# 224 (reserve 32) ran with feeders of 32, 64 and 256 workgroups; 232 (reserve 24) blocked with 32
+# or 256 and ran with 8; 240 (reserve 16) blocked with 64, ran with 16 -- exactly the hangs of
+# profiles/r04/r4_32..r4_36. Smaller requests are raised to this floor.
+CUS_PER_SHADER_ARRAY = 8
+
+
+def min_gate_reserve(ncu: int = 0) -> int:
+    """One free CU per shader array of the device (32 on a whole MI355X; a compute partition
+    with fewer CUs has proportionally fewer arrays)."""
+    from ddlb_amd.ops.gemm import device_cus
+
+    return max(1, (ncu or device_cus()) // CUS_PER_SHADER_ARRAY)
+
+
+MIN_GATE_RESERVE = 32  # min_gate_reserve() of a whole MI355X
 
 
 def _gate_reserve(cfg: AlgoConfig) -> int:
-    return max(cfg.reserve_cus, MIN_GATE_RESERVE)
+    return max(cfg.reserve_cus, min_gate_reserve())
 
 
 def _unique(events):

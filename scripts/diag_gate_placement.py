@@ -45,20 +45,38 @@ def _free_port() -> int:
 
 
 def kfd_topology():
-    """Shader-array layout of the GPU nodes (KFD sysfs; empty off-GPU)."""
+    """Shader-array layout of the GPU (KFD sysfs where readable, else rocminfo; empty off-GPU)."""
     keys = ("simd_count", "array_count", "simd_arrays_per_engine", "cu_per_simd_array",
             "simd_per_cu", "num_xcc", "max_waves_per_simd", "lds_size_in_kb")
     out = []
     for path in sorted(glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties")):
         props = {}
-        with open(path) as fh:
-            for line in fh:
-                k, _, v = line.strip().partition(" ")
-                if k in keys:
-                    props[k] = int(v)
+        try:
+            with open(path) as fh:
+                for line in fh:
+                    k, _, v = line.strip().partition(" ")
+                    if k in keys:
+                        props[k] = int(v)
+        except OSError:
+            continue
         if props.get("simd_count", 0) > 0:
             out.append(props)
-    return out
+    if out:
+        return out
+    try:  # rocminfo: "Compute Unit", "Shader Engines", "Shader Arrs. per Eng." of each GPU agent
+        r = subprocess.run(["rocminfo"], capture_output=True, text=True, timeout=60)
+    except (OSError, subprocess.TimeoutExpired):
+        return out
+    cur = {}
+    for line in r.stdout.splitlines():
+        k, _, v = line.strip().partition(":")
+        k, v = k.strip(), v.strip().split(" ")[0]
+        if k in ("Compute Unit", "Shader Engines", "Shader Arrs. per Eng.", "SIMDs per CU"):
+            cur[k] = int(v) if v.isdigit() else v
+        if k == "Name" and v.startswith("gfx"):
+            cur = {"name": v}
+            out.append(cur)
+    return [c for c in out if "Compute Unit" in c]
 
 
 def one(reserve: int, blocks: int) -> dict:

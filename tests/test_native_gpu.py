@@ -965,20 +965,23 @@ def test_ksplit_reduced_ops_gemm(comm):
     assert float((t4.float() - ref).abs().max()) <= _tight(ref, K)
 
 
+@pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("dtype,mode", [("bfloat16", "auto"), ("float8_e4m3fn", "auto"),
                                         ("float8_e4m3fn", "mx")])
-def test_split_k_world1_native(comm, dtype, mode):
+def test_split_k_world1_native(comm, dtype, mode, fused):
     """BASELINE config #2's full GEMM (8192 x 1024 x 8192: 128 tiles of 256²) runs K-split: ONE
-    pt4 launch over (slice, tile) pairs that also reduces them (no reduce op); validated by the
-    primitive (fp32 reference) and repeat-identical."""
+    pt4 launch over (slice, tile) pairs writing two partials summed by the reduce op, or
+    (``ks_fused``) reducing them itself; validated by the primitive (fp32 reference) and
+    repeat-identical."""
     from ddlb_amd.parallel.plan import OP_GEMM, OP_REDUCE
     from ddlb_amd.primitives.tp_columnwise.native import NativeTPColumnwise
 
-    impl = NativeTPColumnwise(m=8192, n=1024, k=8192, dtype=dtype, gemm_mode=mode)
+    impl = NativeTPColumnwise(m=8192, n=1024, k=8192, dtype=dtype, gemm_mode=mode,
+                              ks_fused=fused)
     ops = impl.bound.plan.ops
     g = [op for op in ops if op.kind == OP_GEMM]
-    assert len(g) == 1 and g[0].args["ksplit"] == 2 and g[0].args["ks_ws"] is not None
-    assert sum(op.kind == OP_REDUCE for op in ops) == 0
+    assert len(g) == 1 and g[0].args["ksplit"] == 2 and (g[0].args["ks_ws"] is not None) == fused
+    assert sum(op.kind == OP_REDUCE for op in ops) == (0 if fused else 1)
     out = impl.run()
     torch.cuda.synchronize()
     impl.validate(out)

@@ -400,21 +400,24 @@ def test_rccl_fused_signal_stream(alg, side):
     assert any(op.kind in (OP_RECORD, OP_WAIT) for op in plan.ops) == side
 
 
+@pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("d,be", [(1, "rccl"), (2, "rccl"), (2, "ipc"), (4, "rccl"), (4, "ipc")])
-def test_split_k_full_gemm(d, be):
+def test_split_k_full_gemm(d, be, fused):
     """A full GEMM whose 256x256 grid covers few CUs and whose K is long runs K-split: ONE
-    persistent launch over (slice, tile) pairs that reduces them itself (f32 workspace + tile
-    counters, no reduce op); exact result, race-free."""
+    persistent launch over (slice, tile) pairs writing S partials, summed by one reduce op, or
+    (``ks_fused``) reducing them itself (f32 workspace + tile counters, no reduce op); exact
+    result, race-free."""
     m, n, k = 256 * d, 256, 2048
-    cfg = AlgoConfig(algorithm="default", backend=be)
+    cfg = AlgoConfig(algorithm="default", backend=be, ks_fused=fused)
     plan, _ = build_tp_columnwise(0, d, m, n, k, DT_F32, DT_F32, cfg)
     g = [op for op in plan.ops if op.kind == OP_GEMM]
     assert len(g) == 1 and g[0].stream == 0 and g[0].args["ksplit"] == 4
     assert g[0].args["K"] == k // 4 and g[0].args["lda"] == k and g[0].args["tile"] == 19
-    assert g[0].args["ks_ws"] is not None and g[0].args["ks_cnt"] is not None
-    assert plan.buffers[g[0].args["ks_cnt"].buf].zero  # counters zeroed once, never reset
-    assert plan.buffers[g[0].args["ks_ws"].buf].nbytes == 4 * m * n * 4
-    assert sum(op.kind == OP_REDUCE for op in plan.ops) == 0
+    if fused:
+        assert g[0].args["ks_ws"] is not None and g[0].args["ks_cnt"] is not None
+        assert plan.buffers[g[0].args["ks_cnt"].buf].zero  # counters zeroed once, never reset
+        assert plan.buffers[g[0].args["ks_ws"].buf].nbytes == 4 * m * n * 4
+    assert sum(op.kind == OP_REDUCE for op in plan.ops) == (0 if fused else 1)
     _run_col(d, m, n, k, cfg, epochs=2)
 
 
@@ -450,13 +453,13 @@ def test_ksplit_rejects_tables_and_flags():
 def test_split_k_p2p_shard_gemms(be):
     """p2p_pipeline's per-shard GEMMs (plain C rows) take the K-split too when each shard has
     few tiles and K is long (BASELINE 4b: m = 65536, k = 8192 at d = 8); one scratch buffer is
-    reused on stream 0 between shards (the never-reset counters carry across them), race-free."""
+    reused on stream 0 between shards, race-free."""
     d, m, n, k = 2, 512, 256, 2048
     cfg = AlgoConfig(algorithm="p2p_pipeline", backend=be)
     plan, _ = build_tp_columnwise(0, d, m, n, k, DT_F32, DT_F32, cfg)
     g = [op for op in plan.ops if op.kind == OP_GEMM]
     assert len(g) == d and all(op.args["ksplit"] == 4 for op in g)
-    assert sum(op.kind == OP_REDUCE for op in plan.ops) == 0  # reduced inside each launch
+    assert sum(op.kind == OP_REDUCE for op in plan.ops) == d
     _run_col(d, m, n, k, cfg, epochs=2)
 
 
