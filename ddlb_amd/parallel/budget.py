@@ -48,8 +48,12 @@ def _map_list(plan: Plan, refs):
 
 def emulate(plan: Plan, rccl_blocks: int = 32) -> Plan:
     """One-rank form of ``plan`` (see the module docstring). ``rccl_blocks``: CU budget of the
-    copy kernels standing in for RCCL's kernels."""
+    copy kernels standing in for RCCL's kernels, never above the plan's own RCCL CTA cap (an
+    RCCL-fed gated GEMM's communicator launches at most ``meta['rccl_max_ctas']`` workgroups)."""
     d = plan.world
+    cap = int(plan.meta.get("rccl_max_ctas", 0))
+    if cap > 0:
+        rccl_blocks = min(rccl_blocks, cap)
     ep = Plan(0, 1, nstreams=plan.nstreams, stream_priority=list(plan.stream_priority))
     ep.meta = dict(plan.meta, emulated_world=d, emulated_rank=plan.rank)
     ep.nevents = plan.nevents

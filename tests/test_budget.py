@@ -90,3 +90,19 @@ def test_link_bytes_model():
     plan, _ = build_tp_rowwise(0, d, 16384, 8192, 8192, DT_BF16, DT_BF16,
                                AlgoConfig(algorithm="p2p_pipeline", backend="ipc", fused=True))
     assert all(v == 16384 // d * 8192 * 2 for v in link_bytes(plan).values())
+
+
+def test_emulated_rccl_stand_in_respects_the_cta_cap():
+    """The copy kernels standing in for RCCL in the one-GPU budget never exceed the plan's RCCL
+    CTA cap (the RCCL-fed gated GEMM's reserve), whatever --rccl-blocks asks for."""
+    from ddlb_amd.parallel.algorithms import AlgoConfig, build_tp_columnwise
+    from ddlb_amd.parallel.budget import emulate
+    from ddlb_amd.parallel.plan import DT_BF16, OP_COPY
+
+    cfg = AlgoConfig(algorithm="coll_pipeline", backend="rccl", fused=True, s=4)
+    plan, _ = build_tp_columnwise(0, 8, 65536, 1024, 1024, DT_BF16, DT_BF16, cfg)
+    assert plan.meta["rccl_max_ctas"] == 32
+    for ask, want in [(6, 6), (32, 32), (64, 32)]:
+        ep = emulate(plan, rccl_blocks=ask)
+        blocks = {op.args["max_blocks"] for op in ep.ops if op.kind == OP_COPY}
+        assert blocks == {want}, (ask, blocks)
