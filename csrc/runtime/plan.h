@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <map>
 #include <string>
 #include <vector>
 
@@ -111,6 +112,10 @@ class PlanExecutor {
   hipStream_t cap_stream_ = nullptr;
   hipGraph_t graph_ = nullptr;
   hipGraphExec_t graph_exec_ = nullptr;
+  // OP_COPY_BATCH without hipMemcpyBatchAsync (eager runs): one instantiated graph of the op's
+  // independent memcpy nodes per op (keyed by its word offset), launched as one submission
+  std::map<size_t, hipGraphExec_t> batch_graphs_;
+  void clear_batch_graphs();
   hipStream_t S(int64_t idx, hipStream_t main) const {
     // (graph capture keeps stream 0 on the capture's origin stream: a cycle of dependencies
     // among NON-origin streams crashes this runtime's hipStreamEndCapture, see side_stream_cycle)

@@ -22,9 +22,9 @@ check           what it proves (every rank, every peer, two epochs)
 ``ipc_sdma``    copy-engine pull (``hipMemcpyAsync`` from IPC-mapped peer memory, one stream per
                 peer) of every peer's pattern
 ``ipc_push``    copy-engine push (posted writes into each peer's receive slot) + DONE flag
-``ipc_batch``   every peer's pattern pulled in ONE batched copy-engine submission
-                (``hipMemcpyBatchAsync``); fails where the runtime lacks that API, since a
-                ``batch_memcpy`` candidate would then time per-segment copies under its name
+``ipc_batch``   every peer's pattern pulled in ONE batched submission (``hipMemcpyBatchAsync``,
+                or where this HIP runtime lacks it, one launch of a graph of independent
+                memcpy nodes); fails if the copies went out one by one
 ``ipc_agk``     the in-kernel all-gather: ONE gated persistent GEMM launch whose copy workgroups
                 pull every peer's row blocks over xGMI (write-through publication, agent-scope
                 gate acquire, ACK stores across the link), validated against fp32
@@ -267,7 +267,7 @@ def _ipc_phase(comm, phase: str, nbytes: int, epochs: int) -> Callable[[], None]
                 bound.check_health()
                 if phase == "ipc_batch":
                     status = ctx.C.copy_batch_status()
-                    if status != "hipMemcpyBatchAsync":
+                    if not status.startswith(("hipMemcpyBatchAsync", "hipGraph")):
                         raise RuntimeError(f"batched copies: {status}")
                 if phase in ("ipc_kernel", "ipc_sdma", "ipc_push", "ipc_batch"):
                     rv = bound.buffer("R").view(torch.int32)

@@ -291,6 +291,36 @@ def test_copy_batch_moves_every_segment():
     print(f"hipMemcpyBatchAsync available: {C.copy_batch_api_available()}")
 
 
+def test_plan_copy_batch_one_submission(comm):
+    """A plan's OP_COPY_BATCH (eager) is ONE submission: hipMemcpyBatchAsync where the runtime has
+    it, else one launch of a graph of independent memcpy nodes built once per op; every segment
+    lands, on repeated runs with new data, and the status names the batched path."""
+    from ddlb_amd.parallel.context import NativeContext
+    from ddlb_amd.parallel.plan import Plan
+
+    sizes = [(1 << 20) + 256 * i for i in range(7)]
+    plan = Plan(0, 1, nstreams=1)
+    srcs = [plan.buffer(f"s{i}", n) for i, n in enumerate(sizes)]
+    dsts = [plan.buffer(f"d{i}", n) for i, n in enumerate(sizes)]
+    plan.copy_batch(0, [(d, s_, n) for d, s_, n in zip(dsts, srcs, sizes)])
+    ctx = NativeContext(comm)
+    bound = ctx.bind(plan)
+    for it in range(3):
+        for i, n in enumerate(sizes):
+            bound.buffer(f"s{i}")[:n].copy_(torch.randint(0, 255, (n,), dtype=torch.uint8,
+                                                          device="cuda"))
+            bound.buffer(f"d{i}").zero_()
+        bound.run()
+        torch.cuda.synchronize()
+        for i, n in enumerate(sizes):
+            assert torch.equal(bound.buffer(f"d{i}")[:n], bound.buffer(f"s{i}")[:n]), (it, i)
+    status = ctx.C.copy_batch_status()
+    print("copy_batch status:", status)
+    assert status.startswith(("hipMemcpyBatchAsync", "hipGraph")), status
+    bound.close()
+    ctx.close()
+
+
 def test_plan_trace_ranges(comm):
     """trace=True: every op's enqueue inside a roctx range named by Plan.labels() (the stage
     names rocprofv3 --kernel-rename gives the kernels); the run itself is unchanged."""
