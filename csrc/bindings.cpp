@@ -115,15 +115,18 @@ PYBIND11_MODULE(_C, m) {
   m.def("tile_cols", &tile_cols);
 
   m.def("reduce_sum",
-        [](uintptr_t dst, std::vector<uintptr_t> srcs, int64_t count, int dtype, uintptr_t s) {
+        [](uintptr_t dst, std::vector<uintptr_t> srcs, int64_t count, int dtype, uintptr_t s,
+           int src_dtype) {
           ReduceArgs a;
           a.dst = (void*)dst;
           a.count = count;
           a.nsrc = (int)srcs.size();
           if (a.nsrc < 1 || a.nsrc > kMaxReduceSrc) throw std::runtime_error("1..16 sources");
           for (int i = 0; i < a.nsrc; ++i) a.src[i] = (const void*)srcs[(size_t)i];
-          check(reduce_sum_launch(a, dtype, (hipStream_t)s), "reduce_sum");
-        });
+          check(reduce_sum_launch(a, dtype, (hipStream_t)s, src_dtype), "reduce_sum");
+        },
+        py::arg("dst"), py::arg("srcs"), py::arg("count"), py::arg("dtype"), py::arg("stream"),
+        py::arg("src_dtype") = -1);
   m.def("copy",
         [](uintptr_t dst, uintptr_t src, int64_t bytes, int max_blocks, uintptr_t s) {
           CopyArgs a;

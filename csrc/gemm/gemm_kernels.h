@@ -558,11 +558,30 @@ template <> struct Store8<DT_F32> {
 // fixed and move only scalars per store (pt4).
 // (AUX 18 = sc1 | nt; 16 = sc1 alone, the K-split hand-off. For the C tiles, r5_6 measured nt
 // alone equal to sc1 | nt and sc1 alone 2.5-12 % slower: flagship 0.1118 / 0.1111 / 0.1249 ms)
-template <int OUT, int AUX = 18>
+// f32 (SWZ, the pt4 fragment layout: lane group g = lane >> 4 holds columns 8g .. 8g+7 of a
+// 32-column quadrant, `off` = its own 8 columns): storing a | b as they are makes each
+// instruction write 16 of every 32 bytes of the quadrant's rows, and write-through stores then
+// reach HBM as half-filled sectors (f32 K-split partials measured 2x slower than bf16 ones,
+// r5_12). One v_permlane32_swap per dword (lanes 32-63 of a <-> lanes 0-31 of b) regroups them:
+// a then holds columns {0-3, 8-11, 4-7, 12-15} in groups 0..3 and b the same + 16, so each
+// instruction writes 64 contiguous bytes per row (cdna guide T21). Needs all 64 lanes active.
+template <int OUT, int AUX = 18, bool SWZ = true>
 __device__ __forceinline__ void store8_wt(__amdgpu_buffer_rsrc_t rc, unsigned off, const f32x4 a,
                                           const f32x4 b, unsigned soff = 0) {
   typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
-  if constexpr (OUT == DT_F32) {
+  if constexpr (OUT == DT_F32 && SWZ) {
+    u32x4_t x = __builtin_bit_cast(u32x4_t, a), y = __builtin_bit_cast(u32x4_t, b);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const auto r = __builtin_amdgcn_permlane32_swap(x[i], y[i], false, false);
+      x[i] = r[0];
+      y[i] = r[1];
+    }
+    // groups 2, 3 now store columns 4-7 / 12-15 (x) of the quadrant: 12 columns left of their own
+    const unsigned o = (__lane_id() & 32) ? off - 48 : off;
+    __builtin_amdgcn_raw_buffer_store_b128(x, rc, o, soff, AUX);
+    __builtin_amdgcn_raw_buffer_store_b128(y, rc, o + 64, soff, AUX);
+  } else if constexpr (OUT == DT_F32) {
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, a), rc, off, soff, AUX);
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, b), rc, off + 16, soff, AUX);
   } else if constexpr (OUT == DT_BF16) {
@@ -1404,11 +1423,10 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     // the last one waits for S - 1 done counts of this launch -- those workgroups have arrived,
     // i.e. are resident and storing, so the wait needs no co-residency assumption -- then sums
     // the partials in slice order (bit-exact run to run) and writes C.
-    // Hand-off without fences (MI355X guide, "Valid forms", first table row): every partial byte
-    // stored sc1 (write-through) and drained by every storing wave (vmcnt(0)), a workgroup
-    // barrier, ONE lane's agent-scope add; the consumer polls the counter, joins a barrier, and
-    // reads every partial byte with sc1 buffer loads. An agent release / acquire instead costs a
-    // whole-L2 write-back / invalidate per tile.
+    // Hand-off: every partial byte stored sc1 (write-through) and drained by every storing wave
+    // (vmcnt(0)), a workgroup barrier, ONE lane's agent release + agent-scope add; the consumer
+    // polls the counter, joins a barrier, and reads every partial byte with sc1 buffer loads
+    // (L1 bypassed, so no acquire invalidate is needed on that side).
     __shared__ unsigned ks_sh[1];  // the tile's arrival ticket, broadcast to every wave
     const int S = p.ksplit;
     const __amdgpu_buffer_rsrc_t wrc =
@@ -1438,8 +1456,13 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
                                     acc[mq * 4 + f][nq * 2 + 1], w_off(mq, f, nq) + mine);
         wait_vm<0>();
         __syncthreads();  // every storing wave has drained its stores
-        if (tid == 0)
+        if (tid == 0) {
+          // agent release (buffer_wbl2 sc1 + vmcnt(0)) before the count: the drained sc1 stores
+          // alone were not enough once they wrote whole 64-B runs (r5_14: 2 of 10 first-launch
+          // checks read a stale partial); one lane per tile, the L2 holds no dirty partial lines
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
           __hip_atomic_fetch_add(cnt + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         return;
       }
       if (tid == 0) {

@@ -39,7 +39,9 @@ struct WaitArgs {            // spin until *ptr[i] >= value for all i (bounded);
   int delta = 0;
 };
 
-hipError_t reduce_sum_launch(const ReduceArgs& a, int dtype, hipStream_t s);
+// src_dtype < 0: the sources have the destination's dtype; 0 (f32) with a f16 / bf16 destination:
+// f32 partials summed and rounded once
+hipError_t reduce_sum_launch(const ReduceArgs& a, int dtype, hipStream_t s, int src_dtype = -1);
 hipError_t copy_launch(const CopyArgs& a, int max_blocks, hipStream_t s);
 hipError_t signal_launch(const SignalArgs& a, hipStream_t s);
 hipError_t wait_launch(const WaitArgs& a, hipStream_t s);

@@ -135,6 +135,56 @@ __global__ __launch_bounds__(256) void reduce_sum_fixed_kernel(ReduceArgs a) {
   }
 }
 
+// f32 sources -> a 16-bit destination (f16 / bf16): the K-split GEMM's f32 partials summed and
+// rounded ONCE. A lane takes 8 elements: 32 B of every source (NS > 0: all loads issued before
+// the first add; NS == 0: a.nsrc sources, one at a time), 16 B out. Same source order.
+template <int DDT, int NS>
+__global__ __launch_bounds__(256) void reduce_f32_to_kernel(ReduceArgs a) {
+  using V = V8<DDT>;
+  static_assert(V::N == 8, "16-bit destinations only");
+  const int64_t nvec = a.count / 8;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    float acc[8];
+    if constexpr (NS > 0) {
+      f32x4 raw[NS][2];
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const f32x4* p = (const f32x4*)((const char*)a.src[s] + v * 32);
+        raw[s][0] = __builtin_nontemporal_load(p);
+        raw[s][1] = __builtin_nontemporal_load(p + 1);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { acc[i] = raw[0][0][i]; acc[4 + i] = raw[0][1][i]; }
+#pragma unroll
+      for (int s = 1; s < NS; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { acc[i] += raw[s][0][i]; acc[4 + i] += raw[s][1][i]; }
+    } else {
+      for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+      for (int s = 0; s < a.nsrc; ++s) {
+        const f32x4* p = (const f32x4*)((const char*)a.src[s] + v * 32);
+        const f32x4 lo = __builtin_nontemporal_load(p), hi = __builtin_nontemporal_load(p + 1);
+        if (s == 0) {
+          for (int i = 0; i < 4; ++i) { acc[i] = lo[i]; acc[4 + i] = hi[i]; }
+        } else {
+          for (int i = 0; i < 4; ++i) { acc[i] += lo[i]; acc[4 + i] += hi[i]; }
+        }
+      }
+    }
+    u32x4 o;
+    V::store(&o, acc);
+    __builtin_nontemporal_store(o, (u32x4*)((char*)a.dst + v * 16));
+  }
+  const int ns = NS > 0 ? NS : a.nsrc;
+  for (int64_t i = nvec * 8 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.count;
+       i += stride) {
+    float acc = load1<0>(a.src[0], i);
+    for (int s = 1; s < ns; ++s) acc += load1<0>(a.src[s], i);
+    store1<DDT>(a.dst, i, acc);
+  }
+}
+
 // Blocks are dealt round-robin to the segments (one segment = one peer = one xGMI link in the
 // IPC all-gathers), so every link carries traffic at once; the blocks of a segment grid-stride
 // over it with U x 16 B in flight per lane (8 by default: a peer read over xGMI has several times
@@ -227,11 +277,26 @@ int grid_for(int64_t work_items) {
 
 }  // namespace
 
-hipError_t reduce_sum_launch(const ReduceArgs& a, int dtype, hipStream_t s) {
+hipError_t reduce_sum_launch(const ReduceArgs& a, int dtype, hipStream_t s, int src_dtype) {
   if (a.nsrc < 1 || a.nsrc > kMaxReduceSrc || a.count <= 0) return hipErrorInvalidValue;
   for (int i = 0; i < a.nsrc; ++i)
     if ((uintptr_t)a.src[i] & 15) return hipErrorInvalidValue;
   if ((uintptr_t)a.dst & 15) return hipErrorInvalidValue;
+  if (src_dtype >= 0 && src_dtype != dtype) {  // f32 partials -> f16 / bf16, one rounding
+    if (src_dtype != 0 || (dtype != 1 && dtype != 2)) return hipErrorInvalidValue;
+    const int g = grid_for(a.count / 8 + 1);
+#define DDLB_RF_CASE(NS)                                                                    \
+  case NS:                                                                                  \
+    if (dtype == 1) hipLaunchKernelGGL((reduce_f32_to_kernel<1, NS>), dim3(g), dim3(256), 0, s, a); \
+    else hipLaunchKernelGGL((reduce_f32_to_kernel<2, NS>), dim3(g), dim3(256), 0, s, a);    \
+    break;
+    switch (a.nsrc >= 2 && a.nsrc <= 8 ? a.nsrc : 0) {
+      DDLB_RF_CASE(0) DDLB_RF_CASE(2) DDLB_RF_CASE(3) DDLB_RF_CASE(4) DDLB_RF_CASE(5)
+      DDLB_RF_CASE(6) DDLB_RF_CASE(7) DDLB_RF_CASE(8)
+    }
+#undef DDLB_RF_CASE
+    return hipGetLastError();
+  }
   const int per = dtype == 0 ? 4 : 8;
   const int g = grid_for(a.count / per + 1);
   static const bool generic = getenv("DDLB_REDUCE_GENERIC") != nullptr;  // A/B knob (benches)

@@ -97,7 +97,7 @@ def device_cus() -> int:
 def split_k_factor(M: int, N: int, K: int, esz: int, ncu: int = 0) -> int:
     """K-slices for a GEMM whose 256x256 grid covers at most half the CUs and whose K is long
     (e.g. 8192 x 1024 x 8192: 128 tiles): ``S`` slices run as (slice, tile) pairs of ONE pt4
-    launch (``GemmArgs::ksplit``) that also reduces them (``GemmArgs::ks_ws``). Each slice
+    launch (``GemmArgs::ksplit``), their partials summed by the reduce kernel. Each slice
     keeps >= 16 K-tiles (the fixed per-tile cost stays small, profiles/r04/r4_15_*); measured
     on the config #2 shape: 0.1009 ms vs 0.1338 unsplit (profiles/r04/r4_22_*). 1 = no split."""
     if M % 256 or N % 256 or M <= 0 or N <= 0:
@@ -115,11 +115,15 @@ def split_k_factor(M: int, N: int, K: int, esz: int, ncu: int = 0) -> int:
 
 def gemm(a, w, out=None, *, out_dtype=None, tile: str = "auto", mode: str = "auto",
          M: Optional[int] = None, a_grp: int = 0, a_gstride: int = 0, c_grp: int = 0,
-         c_gstride: int = 0, stream=None, act: str = "none", ksplit: int = 0):
+         c_gstride: int = 0, stream=None, act: str = "none", ksplit: int = 0,
+         ks_form: str = "reduce"):
     """``out[:M] = act(a[:M] @ w.T)`` on the current HIP stream (grouped-row addressing and a
     fused epilogue activation — none / gelu (tanh) / relu / silu — optional). ``ksplit``: 0 =
     auto (:func:`split_k_factor` for plain-row auto-tile GEMMs with no activation and a dense
-    output), 1 = never, S > 1 = S slices."""
+    output), 1 = never, S > 1 = S slices. A pt4 split rounds once either way: ``ks_form``
+    "reduce" = one launch over (slice, tile) pairs into f32 partials + the reduce kernel
+    (0.1122 ms on 8192 x 1024 x 8192 bf16, ``profiles/r05/r5_14_*``), "inlaunch" = the same
+    launch reduces them (``GemmArgs::ks_ws``, slower on every shape measured)."""
     import torch
 
     C = load()
@@ -162,18 +166,35 @@ def gemm(a, w, out=None, *, out_dtype=None, tile: str = "auto", mode: str = "aut
             if stream is not None:
                 part.record_stream(torch.cuda.ExternalStream(s))
             return out
-        # pt4: one launch; the slices' f32 partials meet in a workspace and the last slice of
-        # each tile writes out (csrc/gemm/gemm.h ks_ws); fresh zeroed tile counters per call,
-        # so concurrent calls on different streams never share them
         ws = torch.empty((S, M, N), dtype=torch.float32, device=a.device)
-        cnt = torch.zeros((2 * (M // 256) * (N // 256),), dtype=torch.int32, device=a.device)
-        C.gemm(a.data_ptr(), w.data_ptr(), out.data_ptr(), a.stride(0), w.stride(0), N, M, N,
-               K // S, dtype_code(a.dtype), dtype_code(out.dtype),
-               TILES["pt4" if tile == "auto" else tile], MODES[mode], 0, 0, 0, 0, s, 0, S,
-               ws.data_ptr(), cnt.data_ptr())
+        keep = [ws]
+        if ks_form == "inlaunch":
+            # the slices' f32 partials meet in the workspace and the last slice of each tile
+            # writes out (csrc/gemm/gemm.h ks_ws); fresh zeroed tile counters per call, so
+            # concurrent calls on different streams never share them
+            cnt = torch.zeros((2 * (M // 256) * (N // 256),), dtype=torch.int32,
+                              device=a.device)
+            keep.append(cnt)
+            C.gemm(a.data_ptr(), w.data_ptr(), out.data_ptr(), a.stride(0), w.stride(0), N, M,
+                   N, K // S, dtype_code(a.dtype), dtype_code(out.dtype), TILES["pt4"],
+                   MODES[mode], 0, 0, 0, 0, s, 0, S, ws.data_ptr(), cnt.data_ptr())
+        elif ks_form == "reduce":
+            # every (slice, tile) pair in one launch into f32 partials, summed in slice order
+            # and rounded once by the reduce kernel (an unsplit GEMM's rounding)
+            C.gemm(a.data_ptr(), w.data_ptr(), ws.data_ptr(), a.stride(0), w.stride(0), N, M, N,
+                   K // S, dtype_code(a.dtype), DT_F32, TILES["pt4"], MODES[mode], 0, 0, 0, 0,
+                   s, 0, S)
+            if out.dtype == torch.float32:
+                C.reduce_sum(out.data_ptr(), [ws[j].data_ptr() for j in range(S)], M * N,
+                             DT_F32, s)
+            else:
+                C.reduce_sum(out.data_ptr(), [ws[j].data_ptr() for j in range(S)], M * N,
+                             dtype_code(out.dtype), s, DT_F32)
+        else:
+            raise ValueError(f"ks_form must be 'reduce' or 'inlaunch', not {ks_form!r}")
         if stream is not None:  # the workspace stays allocated until that stream reaches it
-            ws.record_stream(torch.cuda.ExternalStream(s))
-            cnt.record_stream(torch.cuda.ExternalStream(s))
+            for t in keep:
+                t.record_stream(torch.cuda.ExternalStream(s))
         return out
     C.gemm(a.data_ptr(), w.data_ptr(), out.data_ptr(), a.stride(0), w.stride(0), out.stride(0),
            M, N, K, dtype_code(a.dtype), dtype_code(out.dtype), TILES[tile], MODES[mode],

@@ -928,7 +928,7 @@ def test_ksplit_reduced_in_launch(comm, S, shape, dt, mode, dout):
     (the last slice of a tile to arrive sums the others' f32 partials with its own, in slice
     order, and writes C once). Against the fp32 full-K product with the tight bound (one
     rounding, as an unsplit GEMM); repeat launches on the SAME never-reset counters (epochs
-    2..11) bit-identical; every partial-slab byte of the workspace is overwritten by a run."""
+    2..11, the workspace NaN-filled before each) bit-identical."""
     from ddlb_amd.parallel.context import NativeContext
     from ddlb_amd.parallel.plan import DT_BF16, DT_F32, DT_FP8, Plan
 
@@ -965,11 +965,13 @@ def test_ksplit_reduced_in_launch(comm, S, shape, dt, mode, dout):
     ref = A.float() @ W.float().T
     err = float((first.float() - ref).abs().max())
     assert err <= _tight(ref, K), err
-    for _ in range(10):
+    for _ in range(10):  # a partial read before its producer's stores landed would be NaN
+        bound.buffer("ws").view(torch.float32).fill_(float("nan"))
+        torch.cuda.synchronize()
         bound.run()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        assert torch.equal(out, first)
     bound.check_health()
-    assert torch.equal(out, first)
     counts = bound.buffer("cnt").view(torch.int32)[:2 * tiles].view(tiles, 2).cpu()
     assert torch.equal(counts[:, 0], torch.full((tiles,), 11 * S, dtype=torch.int32))
     assert torch.equal(counts[:, 1], torch.full((tiles,), 11 * (S - 1), dtype=torch.int32))
@@ -977,19 +979,31 @@ def test_ksplit_reduced_in_launch(comm, S, shape, dt, mode, dout):
     ctx.close()
 
 
-def test_ksplit_reduced_ops_gemm(comm):
-    """The public op takes the in-launch reduction for auto-split shapes (config #2's GEMM)."""
+@pytest.mark.parametrize("dtype,mode", [("bfloat16", "auto"), ("float8_e4m3fn", "mx"),
+                                        ("float32", "auto")])
+def test_ksplit_reduced_ops_gemm(comm, dtype, mode):
+    """The public op's auto split (config #2's GEMM) rounds once: f32 partials summed by the
+    reduce kernel ("reduce", the default) or inside the launch ("inlaunch"); the two forms sum
+    the same f32 partials in the same slice order, so they agree bit for bit."""
     from ddlb_amd.ops.gemm import gemm, split_k_factor
 
+    tdt = getattr(torch, dtype)
     M, N, K = 8192, 1024, 8192
-    assert split_k_factor(M, N, K, 2) == 2
-    A = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
-    W = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
-    out = gemm(A, W)
+    if tdt != torch.float32:
+        assert split_k_factor(M, N, K, tdt.itemsize) == 2
+    A = (torch.rand(M, K, device="cuda") * 2 - 1).to(tdt)
+    W = (torch.rand(N, K, device="cuda") * 2 - 1).to(tdt)
+    S = 2
+    out = gemm(A, W, mode=mode, ksplit=S)
     torch.cuda.synchronize()
     ref = A.float() @ W.float().T
     assert float((out.float() - ref).abs().max()) <= _tight(ref, K)
-    assert torch.equal(gemm(A, W), out)
+    assert torch.equal(gemm(A, W, mode=mode, ksplit=S), out)
+    assert torch.equal(gemm(A, W, mode=mode, ksplit=S, ks_form="inlaunch"), out)
+    with pytest.raises(ValueError):
+        gemm(A, W, mode=mode, ksplit=S, ks_form="bogus")
+    if tdt != torch.bfloat16:
+        return
     t4 = gemm(A, W, tile="t4", ksplit=2)  # the slice-by-slice partial form stays available
     torch.cuda.synchronize()
     assert float((t4.float() - ref).abs().max()) <= _tight(ref, K)

@@ -32,3 +32,30 @@ def test_reduce_sum(dtype, nsrc, count):
     torch.testing.assert_close(out[:count].float(), ref.to(dtype).float(), rtol=0, atol=tol)
     if pad > count:
         assert torch.isnan(out[count:].float()).all()  # nothing written past count
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("nsrc", [1, 2, 4, 8, 9])
+@pytest.mark.parametrize("count", [8, 1003, (1 << 20) + 5])
+def test_reduce_sum_f32_sources(dtype, nsrc, count):
+    """f32 sources into a 16-bit destination (the K-split GEMM's partials, rounded once): equal
+    to the fp32 sum in source order, rounded to the destination dtype."""
+    from ddlb_amd.ops import load
+
+    C = load()
+    gen = torch.Generator(device="cuda").manual_seed(nsrc * 7 + count)
+    pad = (count + 7) // 8 * 8
+    slab = 2 * torch.rand((nsrc, pad), generator=gen, device="cuda", dtype=torch.float32) - 1
+    out = torch.full((pad,), float("nan"), device="cuda", dtype=dtype)
+    s = torch.cuda.current_stream().cuda_stream
+    C.reduce_sum(out.data_ptr(), [slab[i].data_ptr() for i in range(nsrc)], count, DT[dtype], s,
+                 DT[torch.float32])
+    torch.cuda.synchronize()
+    ref = slab[0, :count].clone()
+    for i in range(1, nsrc):
+        ref = ref + slab[i, :count]
+    assert torch.equal(out[:count], ref.to(dtype))
+    if pad > count:
+        assert torch.isnan(out[count:].float()).all()
+    with pytest.raises(RuntimeError):  # f32 sources only, 16-bit destinations only
+        C.reduce_sum(out.data_ptr(), [slab[0].data_ptr()], count, DT[dtype], s, DT[dtype] ^ 3)
