@@ -1423,10 +1423,13 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     // the last one waits for S - 1 done counts of this launch -- those workgroups have arrived,
     // i.e. are resident and storing, so the wait needs no co-residency assumption -- then sums
     // the partials in slice order (bit-exact run to run) and writes C.
-    // Hand-off: every partial byte stored sc1 (write-through) and drained by every storing wave
-    // (vmcnt(0)), a workgroup barrier, ONE lane's agent release + agent-scope add; the consumer
-    // polls the counter, joins a barrier, and reads every partial byte with sc1 buffer loads
-    // (L1 bypassed, so no acquire invalidate is needed on that side).
+    // Hand-off, the cdna guide's canonical counter form (§5 split-K item 2, Guideline 16): plain
+    // partial stores drained by every storing wave (vmcnt(0)), a workgroup barrier, ONE lane's
+    // agent release + agent-scope add; the consumer's lane polls relaxed, takes ONE agent
+    // acquire, the workgroup joins a barrier and reads the partials with plain loads. The
+    // fence-free variant (sc1 stores / sc1 loads, the guide's measured row) read stale partials
+    // in 3 of 30 launches with the counters in uncached memory and 1 of 11 in cached memory
+    // (r5_17, r5_18: scripts/diag_ksr_memtype.py, test_ksplit_reduced_in_launch).
     __shared__ unsigned ks_sh[1];  // the tile's arrival ticket, broadcast to every wave
     const int S = p.ksplit;
     const __amdgpu_buffer_rsrc_t wrc =
@@ -1452,15 +1455,16 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
           for (int nq = 0; nq < 2; ++nq)
 #pragma unroll
             for (int f = 0; f < 4; ++f)
-              store8_wt<DT_F32, 16>(wrc, w_lane, acc[mq * 4 + f][nq * 2],
-                                    acc[mq * 4 + f][nq * 2 + 1], w_off(mq, f, nq) + mine);
+              store8_wt<DT_F32, 0>(wrc, w_lane, acc[mq * 4 + f][nq * 2],
+                                   acc[mq * 4 + f][nq * 2 + 1], w_off(mq, f, nq) + mine);
         wait_vm<0>();
         __syncthreads();  // every storing wave has drained its stores
         if (tid == 0) {
-          // agent release (buffer_wbl2 sc1 + vmcnt(0)) before the count: the drained sc1 stores
-          // alone were not enough once they wrote whole 64-B runs (r5_14: 2 of 10 first-launch
-          // checks read a stale partial); one lane per tile, the L2 holds no dirty partial lines
+          // agent release: buffer_wbl2 sc1 writes the dirty partial lines back, its vmcnt(0)
+          // (repeated in asm: the builtin's own wait can be dropped, cdna guide G16 pitfall 12)
+          // completes that before the count
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           __hip_atomic_fetch_add(cnt + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         return;
@@ -1475,11 +1479,14 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
             break;
           }
         }
+        // agent acquire, completed before the barrier releases the loading waves
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       __syncthreads();
       auto ld = [&](unsigned o, unsigned extra) __attribute__((always_inline)) {
-        return __builtin_bit_cast(  // sc1 loads: the hand-off's consumer side
-            f32x4, __builtin_amdgcn_raw_buffer_load_b128(wrc, w_lane + extra, o, 16));
+        return __builtin_bit_cast(  // plain loads behind the acquire
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(wrc, w_lane + extra, o, 0));
       };
       auto store_c = [&](int mq, int f, int nq, f32x4 v0, f32x4 v1) __attribute__((always_inline)) {
         const int64_t prow = cm0 + mq * 64 + f * 16;

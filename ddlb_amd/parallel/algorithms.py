@@ -201,7 +201,12 @@ def _full_gemm(plan: Plan, a_ref: Ref, Bt: Ref, c_ref: Ref, M: int, N: int, K: i
         return
     if cfg.ks_fused:
         ws = plan.buffer(tag, S * M * N * 4)
-        cnt = plan.buffer(tag + "_cnt", max(256, 8 * (M // 256) * (N // 256)), zero=True)
+        # the tile counters live in ordinary (cached) device memory like the workspace, zeroed
+        # once at bind (local buffers are torch.zeros; counts are epoch-relative, never reset):
+        # NOT a zero=True flag buffer, which the binder puts in uncached memory -- there the
+        # count's atomic overtook the drained partial stores (r5_17: 50 of 8.4 M outputs read a
+        # stale partial), and the budget emulator would pre-set it like a flag
+        cnt = plan.buffer(tag + "_cnt", max(256, 8 * (M // 256) * (N // 256)))
         plan.gemm(S_MAIN, a_ref, Bt, c_ref, M=M, N=N, K=K // S, lda=K, ldb=K, ldc=N, ksplit=S,
                   ks_ws=ws, ks_cnt=cnt, **dict(gdt, tile=TILE_PT4))
         return

@@ -946,7 +946,7 @@ def test_ksplit_reduced_in_launch(comm, S, shape, dt, mode, dout):
     b = plan.buffer("b", N * K * es)
     c = plan.buffer("c", M * N * odt.itemsize)
     ws = plan.buffer("ws", S * M * N * 4)
-    cnt = plan.buffer("cnt", max(256, 8 * tiles), zero=True)
+    cnt = plan.buffer("cnt", max(256, 8 * tiles))  # cached memory, zeroed at bind (_full_gemm)
     plan.gemm(0, a, b, c, M=M, N=N, K=ks, lda=K, ldb=K, ldc=N, din=din, dout=dcode, tile=19,
               mode=mode, ksplit=S, ks_ws=ws, ks_cnt=cnt)
     ctx = NativeContext(comm)

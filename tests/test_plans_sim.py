@@ -415,7 +415,8 @@ def test_split_k_full_gemm(d, be, fused):
     assert g[0].args["K"] == k // 4 and g[0].args["lda"] == k and g[0].args["tile"] == 19
     if fused:
         assert g[0].args["ks_ws"] is not None and g[0].args["ks_cnt"] is not None
-        assert plan.buffers[g[0].args["ks_cnt"].buf].zero  # counters zeroed once, never reset
+        # counters zeroed once at bind, never reset, in cached memory: not a (uncached) flag
+        assert not plan.buffers[g[0].args["ks_cnt"].buf].zero
         assert plan.buffers[g[0].args["ks_ws"].buf].nbytes == 4 * m * n * 4
     assert sum(op.kind == OP_REDUCE for op in plan.ops) == (0 if fused else 1)
     _run_col(d, m, n, k, cfg, epochs=2)
