@@ -191,10 +191,10 @@ def _full_gemm(plan: Plan, a_ref: Ref, Bt: Ref, c_ref: Ref, M: int, N: int, K: i
     them in f32 into C (BASELINE config #2 shape: 0.1009 ms, r4_22). ``cfg.ks_fused``: the launch
     reduces them itself (per tile, the last slice to arrive sums the others' f32 partials from a
     workspace with its own and writes C once: one kernel, one rounding; csrc/gemm/gemm.h
-    ``ks_ws``), measured slower on that shape (0.1249 ms bench, r5_3): every workgroup finishes
-    its single tile together, so the partial stores, the arrival poll and the partial loads
-    form one serial chain at the end of the kernel where the two-kernel form overlaps its
-    stores with the last K-tile and reads back at full bandwidth."""
+    ``ks_ws``), measured slower on that shape (GEMM 0.1128 vs 0.1022 ms, profiles/r05/r5_19):
+    every workgroup finishes its single tile together, so the partial stores, the arrival poll
+    and the partial loads form one serial chain at the end of the kernel where the two-kernel
+    form overlaps its stores with the last K-tile and reads back at full bandwidth."""
     S = _split_k(plan, M, N, K, ein, cfg)
     if S == 1:
         plan.gemm(S_MAIN, a_ref, Bt, c_ref, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, **gdt)
