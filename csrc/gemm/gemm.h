@@ -55,6 +55,7 @@ struct GemmArgs {
   int nsub = 1;
   int reserve_cus = 0;              // flag-gated persistent GEMMs: CUs left free (see launch_pt4)
   int raster_g = 4;                 // m-blocks per raster group of tile_mn (tile_map.h)
+  int c_nt = 0;                     // pt4 whole-line 16-bit C stores: 1 = nt only (A/B knob)
   // In-kernel all-gather (flag-gated pt4 only): workgroups [0, ag_ctas) of the launch pull the
   // peers' row blocks of A over xGMI into A (the same rows), count each (producer, block)
   // segment's ag_parts pieces and set its flag when the last lands, and ACK each producer once

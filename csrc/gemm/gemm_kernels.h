@@ -558,6 +558,23 @@ template <> struct Store8<DT_F32> {
 // fixed and move only scalars per store (pt4).
 // (AUX 18 = sc1 | nt; 16 = sc1 alone, the K-split hand-off. For the C tiles, r5_6 measured nt
 // alone equal to sc1 | nt and sc1 alone 2.5-12 % slower: flagship 0.1118 / 0.1111 / 0.1249 ms)
+// 8 outputs (two f32x4) rounded to the 16-bit C type, as the 16 bytes one lane stores
+template <int OUT>
+__device__ __forceinline__ __attribute__((ext_vector_type(4))) unsigned pack8(const f32x4 a,
+                                                                             const f32x4 b) {
+  typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
+  static_assert(OUT == DT_BF16 || OUT == DT_F16, "16-bit outputs only");
+  if constexpr (OUT == DT_BF16) {
+    const bf16x8 o = {(__bf16)a.x, (__bf16)a.y, (__bf16)a.z, (__bf16)a.w,
+                      (__bf16)b.x, (__bf16)b.y, (__bf16)b.z, (__bf16)b.w};
+    return __builtin_bit_cast(u32x4_t, o);
+  } else {
+    const f16x8 o = {(_Float16)a.x, (_Float16)a.y, (_Float16)a.z, (_Float16)a.w,
+                     (_Float16)b.x, (_Float16)b.y, (_Float16)b.z, (_Float16)b.w};
+    return __builtin_bit_cast(u32x4_t, o);
+  }
+}
+
 // f32 (SWZ, the pt4 fragment layout: lane group g = lane >> 4 holds columns 8g .. 8g+7 of a
 // 32-column quadrant, `off` = its own 8 columns): storing a | b as they are makes each
 // instruction write 16 of every 32 bytes of the quadrant's rows, and write-through stores then
@@ -1028,7 +1045,7 @@ __global__ __launch_bounds__(512) void gemm_tn_t4_kernel(const GemmArgs p) {
 // KSR: the K-split reduced inside the launch (GemmArgs::ks_ws / ks_cnt; see ks_reduce below): C
 // itself is written, once, by the last slice of each tile to arrive
 template <class Mma, int OUT, bool GATED, int CMODE = 0, bool APAN = false, bool KS = false,
-          bool KSR = false>
+          bool KSR = false, bool WL = true>
 __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   static_assert(!KSR || (KS && !GATED && CMODE == 2), "KSR: the ungated K-split kernel only");
   constexpr int ROWB = 128, UNIT = 128 * ROWB;
@@ -1251,6 +1268,46 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     }
     __builtin_amdgcn_sched_barrier(0);
   };
+  // PAIRST (DEFER, 16-bit C): a tile's C leaves in whole 128-byte lines. A lane holds 16 B of row
+  // frow in each 32-column quadrant (nq 0 / 1: bytes 16 fq and 64 + 16 fq of the wave's 128-byte
+  // row slice); one DPP row_ror:8 per dword, masked to half the lanes, gives lanes 8-15 of every
+  // 16-lane row the quadrant-1 chunk of row frow - 8 (X) and lanes 0-7 the quadrant-0 chunk of
+  // row frow + 8 (Y), so X covers rows 0-7 and Y rows 8-15 of the fragment, 128 contiguous bytes
+  // per row each (lab: a 128 MB write-through stream 23.1-24.5 us vs 25.1-25.8 us in half lines,
+  // nt only 20.8-22.0 vs 38.1-40.1 us, profiles/r05/r5_21_store_pattern.txt).
+  constexpr bool PAIRST = DEFER && OUT != DT_F32 && WL;  // (WL = false: the A/B knob's form)
+  const unsigned c_pair =
+      (unsigned)(((wr * 128 + (frow & 7)) * p.ldc + wc * 64) * OSZ + ((frow & 8) ? 64 : 0) +
+                 fq * 16);
+  auto store_pair = [&](int mq) __attribute__((always_inline)) {
+    typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
+    if constexpr (PAIRST) {
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const int i = mq * 4 + f;
+      u32x4_t x = pack8<OUT>(acc[i][0], acc[i][1]), y = pack8<OUT>(acc[i][2], acc[i][3]);
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const int t = (int)x[d];
+        x[d] = (unsigned)__builtin_amdgcn_update_dpp(t, (int)y[d], 0x128, 0xF, 0xC, false);
+        y[d] = (unsigned)__builtin_amdgcn_update_dpp((int)y[d], t, 0x128, 0xF, 0x3, false);
+      }
+      const int64_t prow = cm0 + mq * 64 + f * 16;
+      const unsigned so = (unsigned)((prow * p.ldc + cn0) * OSZ) + (KS ? ccs : 0u);
+      const unsigned so8 = so + (unsigned)(8 * p.ldc * OSZ);
+      if (p.c_nt) {
+        __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, 2);
+        __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, 2);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, 18);
+        __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, 18);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    }
+  };
 #define T4_BAR()                         \
   do {                                   \
     __builtin_amdgcn_sched_barrier(0);   \
@@ -1318,25 +1375,34 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
       if constexpr (DEF) mm(1, 1, false);
       mm(0, 0, Z);
       __builtin_amdgcn_s_setprio(0);
-      if constexpr (KIND == 1) store_q(0, 0);
-      if (!g1) wait_vm<KIND == 2 ? 8 + 3 * NS : (KIND == 1 ? 8 + NS : 8)>();
+      // (PAIRST: every store after phase B, the first pair needs quadrant (0, 1); the counts of
+      // the two waits below then drop the NS stores issued here before)
+      if constexpr (KIND == 1 && !PAIRST) store_q(0, 0);
+      if (!g1) wait_vm<KIND == 2 ? 8 + 3 * NS : (KIND == 1 && !PAIRST ? 8 + NS : 8)>();
       T4_BAR();
       loadB(bufc, 1);  // phase B: halves 1
       loadA(bufc, 1);
       stage(0, 0, BUF, qb);
       stage(1, 0, BUF, qb);
       T4_LGKM0();
-      if (g1) wait_vm<KIND == 1 ? 8 + NS : 8>();
+      if (g1) wait_vm<KIND == 1 && !PAIRST ? 8 + NS : 8>();
       T4_BAR();
       __builtin_amdgcn_s_setprio(1);
       mm(0, 1, Z);
+      // PAIRST: rows mq = 0 are final here; storing them now frees their accumulators before
+      // the rest of the phase (held to the end of the phase they spilled 52 bytes)
+      if constexpr (KIND == 1 && PAIRST) store_pair(0);
       mm(1, 0, Z);
       if constexpr (KIND == 1 || KIND == 3) mm(1, 1, false);
       __builtin_amdgcn_s_setprio(0);
-      if constexpr (KIND == 1) {
+      if constexpr (KIND == 1 && PAIRST) {
+        store_pair(1);  // 4 NS stores in all, as the quadrant form's
+      } else if constexpr (KIND == 1) {
         store_q(0, 1);
         store_q(1, 0);
         store_q(1, 1);
+      }
+      if constexpr (KIND == 1) {
 #pragma unroll
         for (int f = 0; f < 4; ++f) {  // the next tile's first A1 x B1 is a deferred product
           acc[4 + f][2] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -2016,6 +2082,13 @@ bool pt4_ok(const GemmArgs& p, int esz) {
          nk % 2 == 0 && p.lda * esz <= (1 << 22) && p.ldb * esz <= (1 << 22);
 }
 
+// DDLB_PT4_HALF_LINES=1: the ungated 16-bit write-through pt4 stores C in half lines per
+// instruction as before round 5 (A/B knob against the whole-line stores)
+inline bool half_lines() {
+  static const bool h = getenv("DDLB_PT4_HALF_LINES") != nullptr;
+  return h;
+}
+
 template <class Mma, int OUT>
 hipError_t launch_pt4(const GemmArgs& p, hipStream_t s) {
   const int tiles = (p.M / 256) * (p.N / 256);
@@ -2087,7 +2160,11 @@ hipError_t launch_pt4(const GemmArgs& p, hipStream_t s) {
                        s, q);
   else if (p.c_table != nullptr)
     hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false, 1>), dim3(grid), dim3(512), 0, s, p);
-  else if (wt)
+  else if (wt && OUT != DT_F32 && half_lines()) {  // A/B knob: the round-4 half-line C stores
+    if constexpr (OUT != DT_F32)
+      hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false, 2, false, false, false, false>),
+                         dim3(grid), dim3(512), 0, s, p);
+  } else if (wt)
     hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false, 2>), dim3(grid), dim3(512), 0, s, p);
   else
     hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false>), dim3(grid), dim3(512), 0, s, p);

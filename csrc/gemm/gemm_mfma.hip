@@ -85,6 +85,8 @@ hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mo
   GemmArgs p = p_in;
   static const int raster_env = getenv("DDLB_RASTER_G") ? atoi(getenv("DDLB_RASTER_G")) : 0;
   if (raster_env > 0) p.raster_g = raster_env;  // A/B knob of the tile raster (tile_map.h)
+  static const int cnt_env = getenv("DDLB_PT4_C_NT") ? atoi(getenv("DDLB_PT4_C_NT")) : 0;
+  if (cnt_env > 0) p.c_nt = 1;  // A/B knob: pt4's whole-line C stores nt instead of sc1 | nt
   if (p.a_grp <= 0) { p.a_grp = p.M > 0 ? p.M : 1; p.a_gstride = p.a_grp; }
   if (p.c_grp <= 0) { p.c_grp = p.M > 0 ? p.M : 1; p.c_gstride = p.c_grp; }
   switch (tile) {  // known codes only (the retired families' codes are refused, not rerouted)

@@ -1,6 +1,7 @@
 """A/B of an environment knob of the native GEMM (read once per process by the launcher): each
 variant runs ``scripts/bench_gemm.py`` in its own process, variants interleaved over rounds, the
-native ``auto`` row's median per variant and shape reported (one box, one call).
+native ``auto`` row's median per variant and shape reported (one box, one call). The value
+``unset`` runs with the knob absent.
 
     python scripts/ab_env_gemm.py --knob DDLB_PT4_CAUX --values 18,16,19,2 --shapes 0,6 --rounds 3
 """
@@ -32,7 +33,11 @@ def main():
     for rnd in range(a.rounds):
         for v in vals:
             out = os.path.join("/tmp", f"ab_{os.getpid()}_{rnd}_{v}.json")
-            env = dict(os.environ, **{a.knob: v})
+            env = dict(os.environ)
+            if v == "unset":  # the knob absent (knobs read as "set or not")
+                env.pop(a.knob, None)
+            else:
+                env[a.knob] = v
             cmd = [sys.executable, os.path.join(ROOT, "scripts", "bench_gemm.py"), "--shapes",
                    a.shapes, "--tiles", "auto", "--modes", a.modes, "--dtype", a.dtype,
                    "--rounds", "3", "--json", out]
