@@ -1045,9 +1045,10 @@ __global__ __launch_bounds__(512) void gemm_tn_t4_kernel(const GemmArgs p) {
 // KSR: the K-split reduced inside the launch (GemmArgs::ks_ws / ks_cnt; see ks_reduce below): C
 // itself is written, once, by the last slice of each tile to arrive
 template <class Mma, int OUT, bool GATED, int CMODE = 0, bool APAN = false, bool KS = false,
-          bool KSR = false, bool WL = true>
+          bool KSR = false, bool WL = true, bool ONE = false>
 __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   static_assert(!KSR || (KS && !GATED && CMODE == 2), "KSR: the ungated K-split kernel only");
+  static_assert(!ONE || (!GATED && CMODE == 2 && !APAN && !KS), "ONE: the plain ungated kernel");
   constexpr int ROWB = 128, UNIT = 128 * ROWB;
   constexpr int NS = 4 * Store8<OUT>::kStores;
   constexpr int OSZ = out_size<OUT>();
@@ -1091,9 +1092,13 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
 
   const int drow = lane >> 3, dpc = lane & 7;
   unsigned offA[2][2], offB[2][2];
+  // ONE: the wave group g1 stages every unit alone, each of its waves the rows of two waves'
+  // shares (virtual waves 2 (wave & 3) and 2 (wave & 3) + 1; the second's source offsets are the
+  // first's plus a wave-uniform row delta, see stage1)
+  const int swave = ONE ? 2 * (wave & 3) : wave;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const int ur = wave * 16 + i * 8 + drow;
+    const int ur = swave * 16 + i * 8 + drow;
     const int ch = (dpc ^ ((ur >> 1) & 7)) * 16;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -1172,6 +1177,37 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
                                              soff, 0, 0);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(X == 0 ? rsA : rsB, (LDS_AS void*)(dst + 8 * ROWB),
                                              16, off[1], soff, 0, 0);
+  };
+  // ONE: a g1 wave's share of unit (X, q) of K-tile c: the 32 rows of virtual waves swave and
+  // swave + 1 (the second 16 rows are 16 A rows / 4 B rows further in the source: t8_perm(t + 16)
+  // = t8_perm(t) + 4 for t < 16; same LDS swizzle, since (ur >> 1) & 7 repeats every 16 rows)
+  auto stage1 = [&](int X, int q, int buf, Cur c) __attribute__((always_inline)) {
+    if (c.ti != src_tile) {
+      rsA = __builtin_amdgcn_make_buffer_rsrc((void*)(a_panel(nm0) + (KS ? nko : 0)), 0,
+                                              0x7FFFFFF0, 0x00020000);
+      rsB = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)((const char*)p.b + nn0 * p.ldb * esz + (KS ? nko : 0)), 0, 0x7FFFFFF0,
+          0x00020000);
+      src_tile = c.ti;
+    }
+    const unsigned* off = X == 0 ? offA[q] : offB[q];
+    char* dst = smem + uoff(X, buf, q) + swave * 16 * ROWB;
+    const unsigned soff = (unsigned)(c.kt * ROWB);
+    const unsigned soff2 = soff + (unsigned)((X == 0 ? 16 * p.lda : 4 * p.ldb) * esz);
+    const __amdgpu_buffer_rsrc_t rs = X == 0 ? rsA : rsB;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)dst, 16, off[0], soff, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)(dst + 8 * ROWB), 16, off[1], soff,
+                                             0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)(dst + 16 * ROWB), 16, off[0],
+                                             soff2, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)(dst + 24 * ROWB), 16, off[1],
+                                             soff2, 0, 0);
+  };
+  auto stage1_all = [&](int buf, Cur c) __attribute__((always_inline)) {
+    stage1(0, 0, buf, c);
+    stage1(0, 1, buf, c);
+    stage1(1, 0, buf, c);
+    stage1(1, 1, buf, c);
   };
   const int frow = lane & 15, fq = lane >> 4, sw = (frow >> 1) & 7;
   const int c0 = ((0 + fq) ^ sw) * 16, c1 = ((4 + fq) ^ sw) * 16;
@@ -1330,7 +1366,12 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   }
   Cur q0{0, 0}, q1{0, 0};
   adv(q1);
-  if constexpr (DEFER) {
+  if constexpr (ONE) {
+    if (g1) {  // K-tiles 0 and 1 into buffers 0 and 1, all by g1 (see stage1)
+      stage1_all(0, q0);
+      stage1_all(1, q1);
+    }
+  } else if constexpr (DEFER) {
     stage(0, 0, 0, q0);  // halves 0 of K-tile 0 ("phase B of K-tile -2")
     stage(1, 0, 0, q0);
     stage(0, 1, 0, q0);  // halves 1 of K-tile 0 ("phase A of K-tile -1")
@@ -1349,7 +1390,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   // (A units, phase A), qb = t+2 (B units, phase B)
   Cur qa = q1, qb = q1;
   adv(qb);
-  wait_vm<DEFER ? 8 : 6>();
+  wait_vm<ONE ? 0 : (DEFER ? 8 : 6)>();
   T4_BAR();
   if (g1) T4_BAR();
   // KIND: 0 normal, 1 last K-tile of a tile, 2 first K-tile after a tile's last, 4 the kernel's
@@ -1360,7 +1401,33 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     constexpr int KIND = decltype(kind_tag)::value;
     constexpr int BUF = decltype(bufc)::value;
     constexpr bool Z = KIND == 2 || KIND == 4;
-    if constexpr (DEFER) {
+    if constexpr (ONE) {
+      // ONE (one load phase and one 64-MFMA section per K-tile and wave group: two wave-group
+      // hand-offs per K-tile instead of DEFER's four, measured worth 2.4-3.3 % by a timing-only
+      // ablation, profiles/r05/r5_23): g0 only reads; g1 reads K-tile t, then -- t is now read
+      // by both groups -- restages its buffer with K-tile t + 2 (every unit, see stage1) and
+      // waits for its t + 1 DMA (issued one load phase ago) before the barrier after which g0
+      // reads t + 1. DMA lead: 2.5 phases from issue to first read.
+      loadB(bufc, 0);
+      loadA(bufc, 0);
+      loadB(bufc, 1);
+      loadA(bufc, 1);
+      T4_LGKM0();
+      if (g1) {
+        stage1_all(BUF, qb);  // 16 ops; the window also holds the previous tile's 4 NS stores
+        wait_vm<KIND == 2 ? 16 + 4 * NS : 16>();
+      }
+      T4_BAR();
+      __builtin_amdgcn_s_setprio(1);
+      mm(0, 0, Z);
+      mm(0, 1, Z);
+      if constexpr (KIND == 1 && PAIRST) store_pair(0);
+      mm(1, 0, Z);
+      mm(1, 1, Z);
+      __builtin_amdgcn_s_setprio(0);
+      if constexpr (KIND == 1 && PAIRST) store_pair(1);
+      T4_BAR();
+    } else if constexpr (DEFER) {
       // KIND 3 (KSR): a tile's last K-tile computed like KIND 1 but with no C stores (the
       // in-launch reduction stores after the loop), so every wait keeps its KIND 0 count
       constexpr bool DEF = KIND == 0 || KIND == 1 || KIND == 3;  // previous K-tile's A1 x B1
@@ -2088,6 +2155,12 @@ inline bool half_lines() {
   static const bool h = getenv("DDLB_PT4_HALF_LINES") != nullptr;
   return h;
 }
+// DDLB_PT4_ONE=1: the ungated 16-bit write-through pt4 runs the ONE schedule (one section per
+// K-tile and wave group, see the kernel)
+inline bool one_section() {
+  static const bool h = getenv("DDLB_PT4_ONE") != nullptr;
+  return h;
+}
 
 template <class Mma, int OUT>
 hipError_t launch_pt4(const GemmArgs& p, hipStream_t s) {
@@ -2163,6 +2236,10 @@ hipError_t launch_pt4(const GemmArgs& p, hipStream_t s) {
   else if (wt && OUT != DT_F32 && half_lines()) {  // A/B knob: the round-4 half-line C stores
     if constexpr (OUT != DT_F32)
       hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false, 2, false, false, false, false>),
+                         dim3(grid), dim3(512), 0, s, p);
+  } else if (wt && OUT != DT_F32 && one_section()) {
+    if constexpr (OUT != DT_F32)
+      hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false, 2, false, false, false, true, true>),
                          dim3(grid), dim3(512), 0, s, p);
   } else if (wt)
     hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false, 2>), dim3(grid), dim3(512), 0, s, p);
