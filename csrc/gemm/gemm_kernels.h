@@ -1065,7 +1065,8 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   // tile_order 3 (own rows first, never gated) exists only for the RCCL-fed gated GEMM, whose A
   // is a row table (APAN): every other pt4 kernel compiles it out (SGPR pressure)
   constexpr bool OWN = GATED && APAN;
-  __shared__ __attribute__((aligned(1024))) char smem[8 * UNIT];
+  // ONE: A in a 3-deep ring (3 x 32 KB) + B in 2 buffers (2 x 32 KB) = the whole 160 KB
+  __shared__ __attribute__((aligned(1024))) char smem[(ONE ? 10 : 8) * UNIT];
   // CMODE 2: C through one wave-uniform descriptor (launch_pt4 checks the extent fits)
   const __amdgpu_buffer_rsrc_t crc =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.c, 0, 0x7FFFFFF0, 0x00020000);
@@ -1180,19 +1181,23 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   };
   // ONE: a g1 wave's share of unit (X, q) of K-tile c: the 32 rows of virtual waves swave and
   // swave + 1 (the second 16 rows are 16 A rows / 4 B rows further in the source: t8_perm(t + 16)
-  // = t8_perm(t) + 4 for t < 16; same LDS swizzle, since (ur >> 1) & 7 repeats every 16 rows)
-  auto stage1 = [&](int X, int q, int buf, Cur c) __attribute__((always_inline)) {
-    if (c.ti != src_tile) {
-      rsA = __builtin_amdgcn_make_buffer_rsrc((void*)(a_panel(nm0) + (KS ? nko : 0)), 0,
+  // = t8_perm(t) + 4 for t < 16; same LDS swizzle, since (ur >> 1) & 7 repeats every 16 rows).
+  // LDS: A slot s (0..2, run time) at s * 32 KB, B buffer b at 96 KB + b * 32 KB. The A and B
+  // cursors run 3 and 2 K-tiles ahead, so each operand switches to the next tile's panel on its
+  // own (nk >= 4 keeps both within the next tile, whose origin is nm0 / nn0).
+  // (a cursor enters a tile at its K-tile 0: the descriptor is rebuilt there, no tile tracking --
+  // SGPRs are at the limit)
+  auto stage1 = [&](int X, int q, unsigned lds_off, Cur c) __attribute__((always_inline)) {
+    if (X == 0 && c.kt == 0 && q == 0)
+      rsA = __builtin_amdgcn_make_buffer_rsrc((void*)a_panel(nm0), 0, 0x7FFFFFF0, 0x00020000);
+    if (X == 1 && c.kt == 0 && q == 0)
+      rsB = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.b + nn0 * p.ldb * esz), 0,
                                               0x7FFFFFF0, 0x00020000);
-      rsB = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)((const char*)p.b + nn0 * p.ldb * esz + (KS ? nko : 0)), 0, 0x7FFFFFF0,
-          0x00020000);
-      src_tile = c.ti;
-    }
-    const unsigned* off = X == 0 ? offA[q] : offB[q];
-    char* dst = smem + uoff(X, buf, q) + swave * 16 * ROWB;
-    const unsigned soff = (unsigned)(c.kt * ROWB);
+    // half q is 64 A rows / 32 B rows further: a uniform delta in soffset, so only the q = 0
+    // per-lane offsets stay live (4 VGPRs fewer: at 256 the kernel spilled)
+    const unsigned* off = X == 0 ? offA[0] : offB[0];
+    char* dst = smem + lds_off + q * 16384 + swave * 16 * ROWB;
+    const unsigned soff = (unsigned)(c.kt * ROWB + q * (X == 0 ? 64 * p.lda : 32 * p.ldb) * esz);
     const unsigned soff2 = soff + (unsigned)((X == 0 ? 16 * p.lda : 4 * p.ldb) * esz);
     const __amdgpu_buffer_rsrc_t rs = X == 0 ? rsA : rsB;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)dst, 16, off[0], soff, 0, 0);
@@ -1203,16 +1208,19 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)(dst + 24 * ROWB), 16, off[1],
                                              soff2, 0, 0);
   };
-  auto stage1_all = [&](int buf, Cur c) __attribute__((always_inline)) {
-    stage1(0, 0, buf, c);
-    stage1(0, 1, buf, c);
-    stage1(1, 0, buf, c);
-    stage1(1, 1, buf, c);
+  auto stage1_a = [&](unsigned slot, Cur c) __attribute__((always_inline)) {  // 8 ops
+    stage1(0, 0, slot * 32768u, c);
+    stage1(0, 1, slot * 32768u, c);
+  };
+  auto stage1_b = [&](int buf, Cur c) __attribute__((always_inline)) {  // 8 ops
+    stage1(1, 0, 98304u + (unsigned)buf * 32768u, c);
+    stage1(1, 1, 98304u + (unsigned)buf * 32768u, c);
   };
   const int frow = lane & 15, fq = lane >> 4, sw = (frow >> 1) & 7;
   const int c0 = ((0 + fq) ^ sw) * 16, c1 = ((4 + fq) ^ sw) * 16;
   unsigned rA0 = (wr * 64 + frow) * ROWB + c0, rA1 = (wr * 64 + frow) * ROWB + c1;
-  unsigned rB0 = 65536 + (wc * 32 + frow) * ROWB + c0, rB1 = 65536 + (wc * 32 + frow) * ROWB + c1;
+  constexpr unsigned BBASE = ONE ? 98304 : 65536;  // start of the B units
+  unsigned rB0 = BBASE + (wc * 32 + frow) * ROWB + c0, rB1 = BBASE + (wc * 32 + frow) * ROWB + c1;
   // opaque bases: otherwise the B base's 64K can be re-associated into a read's constant, which
   // then no longer fits the ds_read offset field (a VGPR per read)
   asm volatile("" : "+v"(rA0), "+v"(rA1), "+v"(rB0), "+v"(rB1));
@@ -1228,7 +1236,8 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     const int h = DEFER ? mq : 0;
 #pragma unroll
     for (int f = 0; f < 4; ++f) {
-      const int o = uoff(0, BUF, mq) + f * 16 * ROWB;
+      // (ONE: rA0 / rA1 carry the current A slot)
+      const int o = uoff(0, ONE ? 0 : BUF, mq) + f * 16 * ROWB;
       if constexpr (PAIR) {
         aP[h][f].lo = *(const i32x4*)(smem + rA0 + o);
         aP[h][f].hi = *(const i32x4*)(smem + rA1 + o);
@@ -1366,10 +1375,14 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   }
   Cur q0{0, 0}, q1{0, 0};
   adv(q1);
-  if constexpr (ONE) {
-    if (g1) {  // K-tiles 0 and 1 into buffers 0 and 1, all by g1 (see stage1)
-      stage1_all(0, q0);
-      stage1_all(1, q1);
+  unsigned aslot = 0;  // ONE: the A slot of the current K-tile
+  if constexpr (ONE) {  // A of K-tiles 0-1 into slots 0-1 by g1, B of K-tile 0 by g0 (B of
+                        // K-tile 1 goes out in g0's first load phase)
+    if (g1) {
+      stage1_a(0, q0);
+      stage1_a(1, q1);
+    } else {
+      stage1_b(0, q0);
     }
   } else if constexpr (DEFER) {
     stage(0, 0, 0, q0);  // halves 0 of K-tile 0 ("phase B of K-tile -2")
@@ -1404,19 +1417,21 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     if constexpr (ONE) {
       // ONE (one load phase and one 64-MFMA section per K-tile and wave group: two wave-group
       // hand-offs per K-tile instead of DEFER's four, measured worth 2.4-3.3 % by a timing-only
-      // ablation, profiles/r05/r5_23): g0 only reads; g1 reads K-tile t, then -- t is now read
-      // by both groups -- restages its buffer with K-tile t + 2 (every unit, see stage1) and
-      // waits for its t + 1 DMA (issued one load phase ago) before the barrier after which g0
-      // reads t + 1. DMA lead: 2.5 phases from issue to first read.
+      // ablation, profiles/r05/r5_23). Both groups read K-tile t in their load phase (g0 one
+      // phase ahead of g1). Each first issues DMA into a unit both groups are done with: g0 B of
+      // t + 1 into the B buffer of t - 1, g1 A of t + 2 into the A slot of t - 1 (3-deep ring).
+      // Before the barrier after which g0 reads t + 1, g1 (end of its load phase) has its A of
+      // t + 1 and g0 (end of its MFMA phase) its B of t + 1. DMA lead: A ~3 phases, B ~1.5.
+      if (g1)
+        stage1_a(aslot == 0 ? 2u : aslot - 1, qb);  // A of t + 2 (8 ops)
+      else
+        stage1_b(BUF ^ 1, qa);  // B of t + 1 (8 ops)
       loadB(bufc, 0);
       loadA(bufc, 0);
       loadB(bufc, 1);
       loadA(bufc, 1);
       T4_LGKM0();
-      if (g1) {
-        stage1_all(BUF, qb);  // 16 ops; the window also holds the previous tile's 4 NS stores
-        wait_vm<KIND == 2 ? 16 + 4 * NS : 16>();
-      }
+      if (g1) wait_vm<KIND == 2 ? 8 + 4 * NS : 8>();  // A of t + 1 (window: A of t + 2, stores)
       T4_BAR();
       __builtin_amdgcn_s_setprio(1);
       mm(0, 0, Z);
@@ -1426,6 +1441,15 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
       mm(1, 1, Z);
       __builtin_amdgcn_s_setprio(0);
       if constexpr (KIND == 1 && PAIRST) store_pair(1);
+      {  // the next K-tile's A slot (the read bases move with it)
+        const unsigned d = aslot == 2 ? (unsigned)-65536 : 32768u;
+        rA0 += d;
+        rA1 += d;
+        aslot = aslot == 2 ? 0 : aslot + 1;
+      }
+      qa = qb;
+      adv(qb);
+      if (!g1) wait_vm<KIND == 1 ? 4 * NS : 0>();  // g0's B of t + 1 (window: this K-tile's stores)
       T4_BAR();
     } else if constexpr (DEFER) {
       // KIND 3 (KSR): a tile's last K-tile computed like KIND 1 but with no C stores (the
@@ -1524,8 +1548,10 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
       if (!g1) wait_vm<KIND == 1 ? 6 + 4 * NS : 6>();
       T4_BAR();
     }
-    qa = qb;
-    adv(qb);
+    if constexpr (!ONE) {  // (ONE advances its own cursors)
+      qa = qb;
+      adv(qb);
+    }
   };
   using B0 = std::integral_constant<int, 0>;
   using B1 = std::integral_constant<int, 1>;
@@ -2237,7 +2263,8 @@ hipError_t launch_pt4(const GemmArgs& p, hipStream_t s) {
     if constexpr (OUT != DT_F32)
       hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false, 2, false, false, false, false>),
                          dim3(grid), dim3(512), 0, s, p);
-  } else if (wt && OUT != DT_F32 && one_section()) {
+  } else if (wt && OUT != DT_F32 && one_section() &&
+             (int64_t)p.K * Mma::kElem / 128 >= 4) {  // (ONE: both cursors within the next tile)
     if constexpr (OUT != DT_F32)
       hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false, 2, false, false, false, true, true>),
                          dim3(grid), dim3(512), 0, s, p);
