@@ -1131,3 +1131,22 @@ def test_side_stream_cycle_is_not_captured():
         r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "scripts", "diag_graph_edges.py"),
                             "--child", variant], capture_output=True, text=True, timeout=120)
         assert r.returncode == 0 and "bytes ok" in r.stdout, (variant, r.returncode, r.stderr[-800:])
+
+
+@pytest.mark.parametrize("knob", ["", "DDLB_PT4_ONE", "DDLB_PT4_HALF_LINES", "DDLB_PT4_C_NT"])
+def test_pt4_schedule_knobs(knob):
+    """The ungated write-through pt4 under each of its A/B knobs (read once per process, hence a
+    child process each): the default DEFER schedule with whole-line C stores, the ONE schedule
+    (3-deep A ring), the half-line stores, nt-only stores -- bf16 / f16 / fp8 / MX-fp8 against
+    the fp32 product with the tight bound, repeat bit-identical."""
+    env = dict(os.environ, DDLB_TEST_KNOB=knob)
+    for k in ("DDLB_PT4_ONE", "DDLB_PT4_HALF_LINES", "DDLB_PT4_C_NT"):
+        env.pop(k, None)
+    if knob:
+        env[knob] = "1"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "_pt4_knob_worker.py")],
+                       capture_output=True, text=True, timeout=100, env=env)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert r.returncode == 0 and lines, (knob, r.stdout[-2000:], r.stderr[-3000:])
+    res = json.loads(lines[-1])
+    assert res["cases"] == 5 and res["worst"] <= 1.0, res
