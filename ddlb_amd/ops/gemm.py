@@ -126,6 +126,8 @@ def gemm(a, w, out=None, *, out_dtype=None, tile: str = "auto", mode: str = "aut
     launch reduces them (``GemmArgs::ks_ws``, slower on every shape measured)."""
     import torch
 
+    if ks_form not in ("reduce", "inlaunch"):
+        raise ValueError(f"ks_form must be 'reduce' or 'inlaunch', not {ks_form!r}")
     C = load()
     if out is None:
         rows = M if M is not None else a.shape[0]
@@ -178,7 +180,7 @@ def gemm(a, w, out=None, *, out_dtype=None, tile: str = "auto", mode: str = "aut
             C.gemm(a.data_ptr(), w.data_ptr(), out.data_ptr(), a.stride(0), w.stride(0), N, M,
                    N, K // S, dtype_code(a.dtype), dtype_code(out.dtype), TILES["pt4"],
                    MODES[mode], 0, 0, 0, 0, s, 0, S, ws.data_ptr(), cnt.data_ptr())
-        elif ks_form == "reduce":
+        else:
             # every (slice, tile) pair in one launch into f32 partials, summed in slice order
             # and rounded once by the reduce kernel (an unsplit GEMM's rounding)
             C.gemm(a.data_ptr(), w.data_ptr(), ws.data_ptr(), a.stride(0), w.stride(0), N, M, N,
@@ -190,8 +192,6 @@ def gemm(a, w, out=None, *, out_dtype=None, tile: str = "auto", mode: str = "aut
             else:
                 C.reduce_sum(out.data_ptr(), [ws[j].data_ptr() for j in range(S)], M * N,
                              dtype_code(out.dtype), s, DT_F32)
-        else:
-            raise ValueError(f"ks_form must be 'reduce' or 'inlaunch', not {ks_form!r}")
         if stream is not None:  # the workspace stays allocated until that stream reaches it
             for t in keep:
                 t.record_stream(torch.cuda.ExternalStream(s))

@@ -550,3 +550,14 @@ def test_gemm_first_only_on_separate_queues(monkeypatch):
     off = AlgoConfig(algorithm="p2p_pipeline", backend="rccl", fused=True, gemm_first=False)
     plan, _ = build_tp_columnwise(0, 2, 2048, 256, 256, DT_F32, DT_F32, off)
     assert not plan.meta["gemm_first"] and plan.ops[-1].kind == OP_GEMM
+
+
+def test_ops_gemm_ks_form_checked_first():
+    """ops.gemm rejects an unknown K-split form before touching the device (CPU tensors here)."""
+    import torch
+
+    from ddlb_amd.ops.gemm import gemm
+
+    a = torch.zeros(256, 256, dtype=torch.bfloat16)
+    with pytest.raises(ValueError, match="ks_form"):
+        gemm(a, a, ks_form="fused")
