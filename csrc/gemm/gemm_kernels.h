@@ -1093,9 +1093,9 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
 
   const int drow = lane >> 3, dpc = lane & 7;
   unsigned offA[2][2], offB[2][2];
-  // ONE: the wave group g1 stages every unit alone, each of its waves the rows of two waves'
-  // shares (virtual waves 2 (wave & 3) and 2 (wave & 3) + 1; the second's source offsets are the
-  // first's plus a wave-uniform row delta, see stage1)
+  // ONE: a wave group stages a unit alone, each of its waves the rows of two waves' shares
+  // (virtual waves 2 (wave & 3) and 2 (wave & 3) + 1; the second's source offsets are the first's
+  // plus a wave-uniform row delta, see stage1)
   const int swave = ONE ? 2 * (wave & 3) : wave;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -1179,9 +1179,10 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(X == 0 ? rsA : rsB, (LDS_AS void*)(dst + 8 * ROWB),
                                              16, off[1], soff, 0, 0);
   };
-  // ONE: a g1 wave's share of unit (X, q) of K-tile c: the 32 rows of virtual waves swave and
-  // swave + 1 (the second 16 rows are 16 A rows / 4 B rows further in the source: t8_perm(t + 16)
-  // = t8_perm(t) + 4 for t < 16; same LDS swizzle, since (ur >> 1) & 7 repeats every 16 rows).
+  // ONE: one wave group stages each unit alone (g0 the B units, g1 the A units); a wave's share
+  // of unit (X, q) of K-tile c is the 32 rows of virtual waves swave and swave + 1 (the second
+  // 16 rows are 16 A rows / 4 B rows further in the source: t8_perm(t + 16) = t8_perm(t) + 4 for
+  // t < 16; same LDS swizzle, since (ur >> 1) & 7 repeats every 16 rows).
   // LDS: A slot s (0..2, run time) at s * 32 KB, B buffer b at 96 KB + b * 32 KB. The A and B
   // cursors run 3 and 2 K-tiles ahead, so each operand switches to the next tile's panel on its
   // own (nk >= 4 keeps both within the next tile, whose origin is nm0 / nn0).
@@ -1327,30 +1328,30 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   auto store_pair = [&](int mq) __attribute__((always_inline)) {
     typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
     if constexpr (PAIRST) {
-    __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      const int i = mq * 4 + f;
-      u32x4_t x = pack8<OUT>(acc[i][0], acc[i][1]), y = pack8<OUT>(acc[i][2], acc[i][3]);
+      for (int f = 0; f < 4; ++f) {
+        const int i = mq * 4 + f;
+        u32x4_t x = pack8<OUT>(acc[i][0], acc[i][1]), y = pack8<OUT>(acc[i][2], acc[i][3]);
 #pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        const int t = (int)x[d];
-        x[d] = (unsigned)__builtin_amdgcn_update_dpp(t, (int)y[d], 0x128, 0xF, 0xC, false);
-        y[d] = (unsigned)__builtin_amdgcn_update_dpp((int)y[d], t, 0x128, 0xF, 0x3, false);
-      }
-      const int64_t prow = cm0 + mq * 64 + f * 16;
-      const unsigned so = (unsigned)((prow * p.ldc + cn0) * OSZ) + (KS ? ccs : 0u);
-      const unsigned so8 = so + (unsigned)(8 * p.ldc * OSZ);
-      if (p.c_nt) {
-        __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, 2);
-        __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, 2);
-      } else {
-        __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, 18);
-        __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, 18);
+        for (int d = 0; d < 4; ++d) {
+          const int t = (int)x[d];
+          x[d] = (unsigned)__builtin_amdgcn_update_dpp(t, (int)y[d], 0x128, 0xF, 0xC, false);
+          y[d] = (unsigned)__builtin_amdgcn_update_dpp((int)y[d], t, 0x128, 0xF, 0x3, false);
+        }
+        const int64_t prow = cm0 + mq * 64 + f * 16;
+        const unsigned so = (unsigned)((prow * p.ldc + cn0) * OSZ) + (KS ? ccs : 0u);
+        const unsigned so8 = so + (unsigned)(8 * p.ldc * OSZ);
+        if (p.c_nt) {
+          __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, 2);
+          __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, 2);
+        } else {
+          __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, 18);
+          __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, 18);
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
       __builtin_amdgcn_sched_barrier(0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
     }
   };
 #define T4_BAR()                         \
