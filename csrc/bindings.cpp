@@ -66,6 +66,52 @@ py::object buffer_dlpack(std::shared_ptr<SymmetricBuffer> buf, int device) {
   return raw_dlpack(buf, buf->local(), buf->bytes(), device);
 }
 
+// CU holder of the rccl_cap preflight phase (ddlb_amd/parallel/preflight.py): holds n CUs with
+// hold_cus_kernel while a capped RCCL collective must finish beside them. The counters live in
+// host-coherent pinned memory, so the host sees residency and releases the holders without any
+// stream ordering (the collective is queued on another stream).
+class CuHolder {
+ public:
+  explicit CuHolder(int device) : device_(device) {
+    check(hipSetDevice(device), "hipSetDevice");
+    check(hipHostMalloc((void**)&host_, 512, hipHostMallocCoherent | hipHostMallocMapped),
+          "hipHostMalloc");
+    check(hipHostGetDevicePointer((void**)&dev_, host_, 0), "hipHostGetDevicePointer");
+    reset();
+  }
+  ~CuHolder() {
+    if (host_) {
+      release();
+      hipSetDevice(device_);
+      hipDeviceSynchronize();
+      hipHostFree(host_);
+    }
+  }
+  void start(int nwg, uintptr_t stream, unsigned spin_limit) {
+    reset();
+    HoldArgs a;
+    a.arrived = dev_;
+    a.go = dev_ + 32;
+    a.timeout_word = dev_ + 64;
+    a.spin_limit = spin_limit;
+    check(hipSetDevice(device_), "hipSetDevice");
+    check(hold_cus_launch(a, nwg, (hipStream_t)stream), "hold_cus_launch");
+  }
+  unsigned arrived() const { return __atomic_load_n(host_, __ATOMIC_ACQUIRE); }
+  unsigned timeout_bits() const { return __atomic_load_n(host_ + 64, __ATOMIC_ACQUIRE); }
+  void release() { __atomic_store_n(host_ + 32, 1u, __ATOMIC_RELEASE); }
+
+ private:
+  void reset() {
+    __atomic_store_n(host_, 0u, __ATOMIC_RELEASE);
+    __atomic_store_n(host_ + 32, 0u, __ATOMIC_RELEASE);
+    __atomic_store_n(host_ + 64, 0u, __ATOMIC_RELEASE);
+  }
+  int device_;
+  unsigned* host_ = nullptr;  // [0] arrived, [32] go, [64] timeout bits (separate 128-B lines)
+  unsigned* dev_ = nullptr;
+};
+
 GemmArgs make_args(uintptr_t a, uintptr_t b, uintptr_t c, int64_t lda, int64_t ldb, int64_t ldc,
                    int M, int N, int K, int64_t a_grp, int64_t a_gstride, int64_t c_grp,
                    int64_t c_gstride) {
@@ -89,21 +135,18 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm",
         [](uintptr_t a, uintptr_t b, uintptr_t c, int64_t lda, int64_t ldb, int64_t ldc, int M,
            int N, int K, int din, int dout, int tile, int mode, int64_t a_grp, int64_t a_gstride,
-           int64_t c_grp, int64_t c_gstride, uintptr_t stream, int act, int ksplit,
-           uintptr_t ks_ws, uintptr_t ks_cnt) {
+           int64_t c_grp, int64_t c_gstride, uintptr_t stream, int act, int ksplit) {
           GemmArgs g = make_args(a, b, c, lda, ldb, ldc, M, N, K, a_grp, a_gstride, c_grp,
                                  c_gstride);
           g.act = act;
           g.ksplit = ksplit > 1 ? ksplit : 1;
-          g.ks_ws = (float*)ks_ws;
-          g.ks_cnt = (unsigned*)ks_cnt;
           check(gemm_launch(g, din, dout, tile, mode, (hipStream_t)stream), "gemm_launch");
         },
         py::arg("a"), py::arg("b"), py::arg("c"), py::arg("lda"), py::arg("ldb"), py::arg("ldc"),
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("din"), py::arg("dout"),
         py::arg("tile") = 0, py::arg("mode") = 0, py::arg("a_grp") = 0, py::arg("a_gstride") = 0,
         py::arg("c_grp") = 0, py::arg("c_gstride") = 0, py::arg("stream") = 0,
-        py::arg("act") = 0, py::arg("ksplit") = 1, py::arg("ks_ws") = 0, py::arg("ks_cnt") = 0);
+        py::arg("act") = 0, py::arg("ksplit") = 1);
   m.def("gemm_fast_path_ok",
         [](uintptr_t a, uintptr_t b, uintptr_t c, int64_t lda, int64_t ldb, int64_t ldc, int M,
            int N, int K, int din, int dout) {
@@ -176,10 +219,29 @@ PYBIND11_MODULE(_C, m) {
            py::arg("uid"), py::arg("nranks"), py::arg("rank"), py::arg("device"),
            py::arg("max_ctas") = 0, py::call_guard<py::gil_scoped_release>())
       .def("destroy", &RcclComm::destroy)
+      // collectives on the caller's stream (preflight / diagnostics: the plans go through the
+      // executor); count in elements of dtype (DT_* codes)
+      .def("all_gather",
+           [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, uintptr_t s) {
+             DDLB_NCCL(ncclAllGather((const void*)send, (void*)recv, count, nccl_dtype(dtype),
+                                     c.get(), (hipStream_t)s));
+           })
+      .def("reduce_scatter",
+           [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, uintptr_t s) {
+             DDLB_NCCL(ncclReduceScatter((const void*)send, (void*)recv, count, nccl_dtype(dtype),
+                                         ncclSum, c.get(), (hipStream_t)s));
+           })
       .def("async_error", &RcclComm::async_error)
       .def_property_readonly("rank", &RcclComm::rank)
       .def_property_readonly("nranks", &RcclComm::nranks)
       .def_property_readonly("max_ctas", &RcclComm::max_ctas);
+  py::class_<CuHolder>(m, "CuHolder")
+      .def(py::init<int>(), py::arg("device"))
+      .def("start", &CuHolder::start, py::arg("nwg"), py::arg("stream"),
+           py::arg("spin_limit") = 1u << 24)
+      .def("arrived", &CuHolder::arrived)
+      .def("timeout_bits", &CuHolder::timeout_bits)
+      .def("release", &CuHolder::release);
 
   py::class_<RcclMem, std::shared_ptr<RcclMem>>(m, "RcclMem")
       .def(py::init<std::shared_ptr<RcclComm>, size_t, int>(), py::arg("comm"), py::arg("bytes"),

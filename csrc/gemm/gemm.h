@@ -55,7 +55,6 @@ struct GemmArgs {
   int nsub = 1;
   int reserve_cus = 0;              // flag-gated persistent GEMMs: CUs left free (see launch_pt4)
   int raster_g = 4;                 // m-blocks per raster group of tile_mn (tile_map.h)
-  int c_nt = 0;                     // pt4 whole-line 16-bit C stores: 1 = nt only (A/B knob)
   // In-kernel all-gather (flag-gated pt4 only): workgroups [0, ag_ctas) of the launch pull the
   // peers' row blocks of A over xGMI into A (the same rows), count each (producer, block)
   // segment's ag_parts pieces and set its flag when the last lands, and ACK each producer once
@@ -82,15 +81,6 @@ struct GemmArgs {
   // c + s * M * ldc elements (the caller sums the partials). pt4 runs every (slice, tile) in one
   // launch; other kernels run the slices one after another.
   int ksplit = 1;
-  // In-launch K-split reduction (optional, with ksplit > 1 on pt4): the S slices of a tile write no
-  // partial to c; each (slice, tile) workgroup counts its arrival in ks_cnt[2 tile] (monotonic
-  // across launches), every slice but the last to arrive stores its f32 partial at
-  // ks_ws + slice * M * N floats (row pitch N) and counts it done in ks_cnt[2 tile + 1]; the last
-  // arrival waits for those (already running, so deadlock-free), sums all S partials in slice
-  // order in f32 (its own from registers) and writes C once, rounded once. ks_cnt: 2 * tiles
-  // words, zeroed once and never reset.
-  float* ks_ws = nullptr;
-  unsigned* ks_cnt = nullptr;
 };
 enum Act : int { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_SILU = 3 };
 // In-kernel all-gather variants (GemmArgs::ag_mode bits; 0 = write-through publication, 8 loads

@@ -821,7 +821,7 @@ __global__ __launch_bounds__(512) void gemm_tn_t8_kernel(const GemmArgs p) {
 // interval after its last read (UB0/UB1 of t are read only in phase A and held in registers).
 // RAW: vmcnt(8) after phase A retires A1 of t (younger: B0/B1(t+1), A0/A1(t+1)); vmcnt(6) after
 // phase B retires A0 of t+1, the youngest unit phase A of t+1 reads. Clamped restaging past the
-// last K-tile as in t8. Measured (scripts/lab, profiles/r01/s2/lab/t8_vs_ring2.txt): 9 % faster
+// last K-tile as in t8. Measured (research/lab, profiles/r01/s2/lab/t8_vs_ring2.txt): 9 % faster
 // than t8 with one short-K tile per CU (16384x1024x1024), 3 % at 65536x1024x8192, 3 % slower at
 // 8192^3.
 template <class Mma, int OUT, int CMODE = 0>  // CMODE 2: write-through nt C stores (as pt4)
@@ -1041,14 +1041,13 @@ __global__ __launch_bounds__(512) void gemm_tn_t4_kernel(const GemmArgs p) {
 // KS: K-split (GemmArgs::ksplit slices, ungated, plain rows, CMODE 2): the virtual tiles are
 // (slice, tile) pairs, slice-major; slice s reads A / B columns [s K, (s + 1) K) (K = the slice's
 // length, lda / ldb the full rows) and stores its partial C at c + s * M * ldc (summed by the
-// caller): a few-tile long-K GEMM fills the chip in ONE launch
-// KSR: the K-split reduced inside the launch (GemmArgs::ks_ws / ks_cnt; see ks_reduce below): C
-// itself is written, once, by the last slice of each tile to arrive
-template <class Mma, int OUT, bool GATED, int CMODE = 0, bool APAN = false, bool KS = false,
-          bool KSR = false, bool WL = true, bool ONE = false>
+// caller's reduce op): a few-tile long-K GEMM fills the chip in ONE launch
+// (Retired in round 6, each measured slower than what stays, docs/RESULTS.md: the ONE schedule
+// -- one section per K-tile and wave group, 0.6-2 % behind DEFER, r5_28 / r5_32; the K-split
+// reduced inside the launch, ~10 % behind split + reduce op, r5_19; half-line C stores and the
+// nt-only store policy, within noise, r5_22.)
+template <class Mma, int OUT, bool GATED, int CMODE = 0, bool APAN = false, bool KS = false>
 __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
-  static_assert(!KSR || (KS && !GATED && CMODE == 2), "KSR: the ungated K-split kernel only");
-  static_assert(!ONE || (!GATED && CMODE == 2 && !APAN && !KS), "ONE: the plain ungated kernel");
   constexpr int ROWB = 128, UNIT = 128 * ROWB;
   constexpr int NS = 4 * Store8<OUT>::kStores;
   constexpr int OSZ = out_size<OUT>();
@@ -1065,8 +1064,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   // tile_order 3 (own rows first, never gated) exists only for the RCCL-fed gated GEMM, whose A
   // is a row table (APAN): every other pt4 kernel compiles it out (SGPR pressure)
   constexpr bool OWN = GATED && APAN;
-  // ONE: A in a 3-deep ring (3 x 32 KB) + B in 2 buffers (2 x 32 KB) = the whole 160 KB
-  __shared__ __attribute__((aligned(1024))) char smem[(ONE ? 10 : 8) * UNIT];
+  __shared__ __attribute__((aligned(1024))) char smem[8 * UNIT];
   // CMODE 2: C through one wave-uniform descriptor (launch_pt4 checks the extent fits)
   const __amdgpu_buffer_rsrc_t crc =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.c, 0, 0x7FFFFFF0, 0x00020000);
@@ -1093,13 +1091,9 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
 
   const int drow = lane >> 3, dpc = lane & 7;
   unsigned offA[2][2], offB[2][2];
-  // ONE: a wave group stages a unit alone, each of its waves the rows of two waves' shares
-  // (virtual waves 2 (wave & 3) and 2 (wave & 3) + 1; the second's source offsets are the first's
-  // plus a wave-uniform row delta, see stage1)
-  const int swave = ONE ? 2 * (wave & 3) : wave;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const int ur = swave * 16 + i * 8 + drow;
+    const int ur = wave * 16 + i * 8 + drow;
     const int ch = (dpc ^ ((ur >> 1) & 7)) * 16;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -1130,19 +1124,13 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   const char* na = nullptr;  // APAN: the next tile's A panel
   int64_t nko = 0;           // KS: the next tile's K-slice byte offset into the A / B rows
   unsigned ncs = 0, ccs = 0;  // KS: the next / current tile's partial-C byte offset
-  int nks = 0, cks = 0, ntid = 0, ctid = 0;  // KSR: the next / current tile's slice and tile id
   auto origin = [&](int ti, int64_t& m0, int64_t& n0) __attribute__((always_inline)) {
     int wg = tile_index_virtual<OWN>(p, bid + ti * nblk, nvt);
     if constexpr (KS) {
       const int ks = wg / ntiles;
       wg -= ks * ntiles;
       nko = (int64_t)ks * p.K * esz;
-      if constexpr (KSR) {
-        nks = ks;
-        ntid = wg;
-      } else {
-        ncs = (unsigned)((int64_t)ks * p.M * p.ldc * OSZ);
-      }
+      ncs = (unsigned)((int64_t)ks * p.M * p.ldc * OSZ);
     }
     int tm_, tn_;
     tile_mn(p, wg, p.M / 256, tiles_n, tm_, tn_);
@@ -1179,48 +1167,10 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(X == 0 ? rsA : rsB, (LDS_AS void*)(dst + 8 * ROWB),
                                              16, off[1], soff, 0, 0);
   };
-  // ONE: one wave group stages each unit alone (g0 the B units, g1 the A units); a wave's share
-  // of unit (X, q) of K-tile c is the 32 rows of virtual waves swave and swave + 1 (the second
-  // 16 rows are 16 A rows / 4 B rows further in the source: t8_perm(t + 16) = t8_perm(t) + 4 for
-  // t < 16; same LDS swizzle, since (ur >> 1) & 7 repeats every 16 rows).
-  // LDS: A slot s (0..2, run time) at s * 32 KB, B buffer b at 96 KB + b * 32 KB. The A and B
-  // cursors run 3 and 2 K-tiles ahead, so each operand switches to the next tile's panel on its
-  // own (nk >= 4 keeps both within the next tile, whose origin is nm0 / nn0).
-  // (a cursor enters a tile at its K-tile 0: the descriptor is rebuilt there, no tile tracking --
-  // SGPRs are at the limit)
-  auto stage1 = [&](int X, int q, unsigned lds_off, Cur c) __attribute__((always_inline)) {
-    if (X == 0 && c.kt == 0 && q == 0)
-      rsA = __builtin_amdgcn_make_buffer_rsrc((void*)a_panel(nm0), 0, 0x7FFFFFF0, 0x00020000);
-    if (X == 1 && c.kt == 0 && q == 0)
-      rsB = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.b + nn0 * p.ldb * esz), 0,
-                                              0x7FFFFFF0, 0x00020000);
-    // half q is 64 A rows / 32 B rows further: a uniform delta in soffset, so only the q = 0
-    // per-lane offsets stay live (4 VGPRs fewer: at 256 the kernel spilled)
-    const unsigned* off = X == 0 ? offA[0] : offB[0];
-    char* dst = smem + lds_off + q * 16384 + swave * 16 * ROWB;
-    const unsigned soff = (unsigned)(c.kt * ROWB + q * (X == 0 ? 64 * p.lda : 32 * p.ldb) * esz);
-    const unsigned soff2 = soff + (unsigned)((X == 0 ? 16 * p.lda : 4 * p.ldb) * esz);
-    const __amdgpu_buffer_rsrc_t rs = X == 0 ? rsA : rsB;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)dst, 16, off[0], soff, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)(dst + 8 * ROWB), 16, off[1], soff,
-                                             0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)(dst + 16 * ROWB), 16, off[0],
-                                             soff2, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)(dst + 24 * ROWB), 16, off[1],
-                                             soff2, 0, 0);
-  };
-  auto stage1_a = [&](unsigned slot, Cur c) __attribute__((always_inline)) {  // 8 ops
-    stage1(0, 0, slot * 32768u, c);
-    stage1(0, 1, slot * 32768u, c);
-  };
-  auto stage1_b = [&](int buf, Cur c) __attribute__((always_inline)) {  // 8 ops
-    stage1(1, 0, 98304u + (unsigned)buf * 32768u, c);
-    stage1(1, 1, 98304u + (unsigned)buf * 32768u, c);
-  };
   const int frow = lane & 15, fq = lane >> 4, sw = (frow >> 1) & 7;
   const int c0 = ((0 + fq) ^ sw) * 16, c1 = ((4 + fq) ^ sw) * 16;
   unsigned rA0 = (wr * 64 + frow) * ROWB + c0, rA1 = (wr * 64 + frow) * ROWB + c1;
-  constexpr unsigned BBASE = ONE ? 98304 : 65536;  // start of the B units
+  constexpr unsigned BBASE = 65536;  // start of the B units
   unsigned rB0 = BBASE + (wc * 32 + frow) * ROWB + c0, rB1 = BBASE + (wc * 32 + frow) * ROWB + c1;
   // opaque bases: otherwise the B base's 64K can be re-associated into a read's constant, which
   // then no longer fits the ds_read offset field (a VGPR per read)
@@ -1237,8 +1187,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     const int h = DEFER ? mq : 0;
 #pragma unroll
     for (int f = 0; f < 4; ++f) {
-      // (ONE: rA0 / rA1 carry the current A slot)
-      const int o = uoff(0, ONE ? 0 : BUF, mq) + f * 16 * ROWB;
+      const int o = uoff(0, BUF, mq) + f * 16 * ROWB;
       if constexpr (PAIR) {
         aP[h][f].lo = *(const i32x4*)(smem + rA0 + o);
         aP[h][f].hi = *(const i32x4*)(smem + rA1 + o);
@@ -1321,7 +1270,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   // row frow + 8 (Y), so X covers rows 0-7 and Y rows 8-15 of the fragment, 128 contiguous bytes
   // per row each (lab: a 128 MB write-through stream 23.1-24.5 us vs 25.1-25.8 us in half lines,
   // nt only 20.8-22.0 vs 38.1-40.1 us, profiles/r05/r5_21_store_pattern.txt).
-  constexpr bool PAIRST = DEFER && OUT != DT_F32 && WL;  // (WL = false: the A/B knob's form)
+  constexpr bool PAIRST = DEFER && OUT != DT_F32;
   const unsigned c_pair =
       (unsigned)(((wr * 128 + (frow & 7)) * p.ldc + wc * 64) * OSZ + ((frow & 8) ? 64 : 0) +
                  fq * 16);
@@ -1342,13 +1291,8 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
         const int64_t prow = cm0 + mq * 64 + f * 16;
         const unsigned so = (unsigned)((prow * p.ldc + cn0) * OSZ) + (KS ? ccs : 0u);
         const unsigned so8 = so + (unsigned)(8 * p.ldc * OSZ);
-        if (p.c_nt) {
-          __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, 2);
-          __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, 2);
-        } else {
-          __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, 18);
-          __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, 18);
-        }
+        __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, 18);  // sc1 | nt
+        __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, 18);
         __builtin_amdgcn_sched_barrier(0);
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -1376,16 +1320,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   }
   Cur q0{0, 0}, q1{0, 0};
   adv(q1);
-  unsigned aslot = 0;  // ONE: the A slot of the current K-tile
-  if constexpr (ONE) {  // A of K-tiles 0-1 into slots 0-1 by g1, B of K-tile 0 by g0 (B of
-                        // K-tile 1 goes out in g0's first load phase)
-    if (g1) {
-      stage1_a(0, q0);
-      stage1_a(1, q1);
-    } else {
-      stage1_b(0, q0);
-    }
-  } else if constexpr (DEFER) {
+  if constexpr (DEFER) {
     stage(0, 0, 0, q0);  // halves 0 of K-tile 0 ("phase B of K-tile -2")
     stage(1, 0, 0, q0);
     stage(0, 1, 0, q0);  // halves 1 of K-tile 0 ("phase A of K-tile -1")
@@ -1404,7 +1339,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   // (A units, phase A), qb = t+2 (B units, phase B)
   Cur qa = q1, qb = q1;
   adv(qb);
-  wait_vm<ONE ? 0 : (DEFER ? 8 : 6)>();
+  wait_vm<DEFER ? 8 : 6>();
   T4_BAR();
   if (g1) T4_BAR();
   // KIND: 0 normal, 1 last K-tile of a tile, 2 first K-tile after a tile's last, 4 the kernel's
@@ -1415,47 +1350,8 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     constexpr int KIND = decltype(kind_tag)::value;
     constexpr int BUF = decltype(bufc)::value;
     constexpr bool Z = KIND == 2 || KIND == 4;
-    if constexpr (ONE) {
-      // ONE (one load phase and one 64-MFMA section per K-tile and wave group: two wave-group
-      // hand-offs per K-tile instead of DEFER's four, measured worth 2.4-3.3 % by a timing-only
-      // ablation, profiles/r05/r5_23). Both groups read K-tile t in their load phase (g0 one
-      // phase ahead of g1). Each first issues DMA into a unit both groups are done with: g0 B of
-      // t + 1 into the B buffer of t - 1, g1 A of t + 2 into the A slot of t - 1 (3-deep ring).
-      // Before the barrier after which g0 reads t + 1, g1 (end of its load phase) has its A of
-      // t + 1 and g0 (end of its MFMA phase) its B of t + 1. DMA lead: A ~3 phases, B ~1.5.
-      if (g1)
-        stage1_a(aslot == 0 ? 2u : aslot - 1, qb);  // A of t + 2 (8 ops)
-      else
-        stage1_b(BUF ^ 1, qa);  // B of t + 1 (8 ops)
-      loadB(bufc, 0);
-      loadA(bufc, 0);
-      loadB(bufc, 1);
-      loadA(bufc, 1);
-      T4_LGKM0();
-      if (g1) wait_vm<KIND == 2 ? 8 + 4 * NS : 8>();  // A of t + 1 (window: A of t + 2, stores)
-      T4_BAR();
-      __builtin_amdgcn_s_setprio(1);
-      mm(0, 0, Z);
-      mm(0, 1, Z);
-      if constexpr (KIND == 1 && PAIRST) store_pair(0);
-      mm(1, 0, Z);
-      mm(1, 1, Z);
-      __builtin_amdgcn_s_setprio(0);
-      if constexpr (KIND == 1 && PAIRST) store_pair(1);
-      {  // the next K-tile's A slot (the read bases move with it)
-        const unsigned d = aslot == 2 ? (unsigned)-65536 : 32768u;
-        rA0 += d;
-        rA1 += d;
-        aslot = aslot == 2 ? 0 : aslot + 1;
-      }
-      qa = qb;
-      adv(qb);
-      if (!g1) wait_vm<KIND == 1 ? 4 * NS : 0>();  // g0's B of t + 1 (window: this K-tile's stores)
-      T4_BAR();
-    } else if constexpr (DEFER) {
-      // KIND 3 (KSR): a tile's last K-tile computed like KIND 1 but with no C stores (the
-      // in-launch reduction stores after the loop), so every wait keeps its KIND 0 count
-      constexpr bool DEF = KIND == 0 || KIND == 1 || KIND == 3;  // previous K-tile's A1 x B1
+    if constexpr (DEFER) {
+      constexpr bool DEF = KIND == 0 || KIND == 1;  // previous K-tile's A1 x B1
       loadB(bufc, 0);  // phase A: halves 0
       loadA(bufc, 0);
       stage(0, 1, BUF ^ 1, qa);
@@ -1485,7 +1381,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
       // the rest of the phase (held to the end of the phase they spilled 52 bytes)
       if constexpr (KIND == 1 && PAIRST) store_pair(0);
       mm(1, 0, Z);
-      if constexpr (KIND == 1 || KIND == 3) mm(1, 1, false);
+      if constexpr (KIND == 1) mm(1, 1, false);
       __builtin_amdgcn_s_setprio(0);
       if constexpr (KIND == 1 && PAIRST) {
         store_pair(1);  // 4 NS stores in all, as the quadrant form's
@@ -1549,10 +1445,8 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
       if (!g1) wait_vm<KIND == 1 ? 6 + 4 * NS : 6>();
       T4_BAR();
     }
-    if constexpr (!ONE) {  // (ONE advances its own cursors)
-      qa = qb;
-      adv(qb);
-    }
+    qa = qb;
+    adv(qb);
   };
   using B0 = std::integral_constant<int, 0>;
   using B1 = std::integral_constant<int, 1>;
@@ -1562,10 +1456,6 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     cm0 = nm0;  // this tile (C rows: physical, grouped C rows keep a tile contiguous)
     cn0 = nn0;
     if constexpr (KS) ccs = ncs;
-    if constexpr (KSR) {
-      cks = nks;
-      ctid = ntid;
-    }
     if constexpr (CMODE == 2) cm0 = map_row(cm0, p.c_grp, p.c_gstride);
     if (ti + 1 < my_tiles) origin(ti + 1, nm0, nn0);
     iter(B0{}, first_kind);  // K-tile 0
@@ -1575,133 +1465,10 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     }
     iter(B1{}, last_kind);  // K-tile nk - 1 (nk even)
   };
-  if constexpr (KSR) {
-    // In-launch K-split reduction, per tile after its K loop (both wave groups aligned, every
-    // DMA drained: the next tile's staging restarts from the prologue's state). Ticket = the
-    // tile's arrival count before this one; launch e (1-based) hands out [(e-1) S, e S), so the
-    // holder of e S - 1 is the last slice of this launch. The others publish their f32 partial;
-    // the last one waits for S - 1 done counts of this launch -- those workgroups have arrived,
-    // i.e. are resident and storing, so the wait needs no co-residency assumption -- then sums
-    // the partials in slice order (bit-exact run to run) and writes C.
-    // Hand-off, the cdna guide's canonical counter form (§5 split-K item 2, Guideline 16): plain
-    // partial stores drained by every storing wave (vmcnt(0)), a workgroup barrier, ONE lane's
-    // agent release + agent-scope add; the consumer's lane polls relaxed, takes ONE agent
-    // acquire, the workgroup joins a barrier and reads the partials with plain loads. The
-    // fence-free variant (sc1 stores / sc1 loads, the guide's measured row) read stale partials
-    // in 3 of 30 launches with the counters in uncached memory and 1 of 11 in cached memory
-    // (r5_17, r5_18: scripts/diag_ksr_memtype.py, test_ksplit_reduced_in_launch).
-    __shared__ unsigned ks_sh[1];  // the tile's arrival ticket, broadcast to every wave
-    const int S = p.ksplit;
-    const __amdgpu_buffer_rsrc_t wrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)p.ks_ws, 0, 0x7FFFFFF0, 0x00020000);
-    const unsigned w_lane = (unsigned)(((wr * 128 + frow) * p.N + wc * 64 + fq * 8) * 4);
-    const unsigned slab = (unsigned)((int64_t)p.M * p.N * 4);
-    auto ks_reduce = [&]() __attribute__((always_inline)) {
-      unsigned* cnt = p.ks_cnt + 2 * ctid;
-      if (tid == 0)
-        ks_sh[0] = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __syncthreads();
-      const unsigned ticket = ks_sh[0];
-      const bool last = ticket % (unsigned)S == (unsigned)(S - 1);
-      const unsigned epoch = ticket / (unsigned)S + 1;
-      auto w_off = [&](int mq, int f, int nq) __attribute__((always_inline)) {
-        return (unsigned)(((cm0 + mq * 64 + f * 16) * p.N + cn0 + nq * 32) * 4);
-      };
-      if (!last) {
-        const unsigned mine = (unsigned)cks * slab;
-#pragma unroll
-        for (int mq = 0; mq < 2; ++mq)
-#pragma unroll
-          for (int nq = 0; nq < 2; ++nq)
-#pragma unroll
-            for (int f = 0; f < 4; ++f)
-              store8_wt<DT_F32, 0>(wrc, w_lane, acc[mq * 4 + f][nq * 2],
-                                   acc[mq * 4 + f][nq * 2 + 1], w_off(mq, f, nq) + mine);
-        wait_vm<0>();
-        __syncthreads();  // every storing wave has drained its stores
-        if (tid == 0) {
-          // agent release: buffer_wbl2 sc1 writes the dirty partial lines back, its vmcnt(0)
-          // (repeated in asm: the builtin's own wait can be dropped, cdna guide G16 pitfall 12)
-          // completes that before the count
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __hip_atomic_fetch_add(cnt + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        return;
-      }
-      if (tid == 0) {
-        const unsigned want = epoch * (unsigned)(S - 1);
-        unsigned spins = 0;
-        while (__hip_atomic_load(cnt + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-          __builtin_amdgcn_s_sleep(1);
-          if (++spins > p.spin_limit) {  // (cannot happen: the others are resident) report
-            if (p.timeout_word) atomicOr(p.timeout_word, 32u);
-            break;
-          }
-        }
-        // agent acquire, completed before the barrier releases the loading waves
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __syncthreads();
-      auto ld = [&](unsigned o, unsigned extra) __attribute__((always_inline)) {
-        return __builtin_bit_cast(  // plain loads behind the acquire
-            f32x4, __builtin_amdgcn_raw_buffer_load_b128(wrc, w_lane + extra, o, 0));
-      };
-      auto store_c = [&](int mq, int f, int nq, f32x4 v0, f32x4 v1) __attribute__((always_inline)) {
-        const int64_t prow = cm0 + mq * 64 + f * 16;
-        store8_wt<OUT>(crc, c_lane, v0, v1, (unsigned)((prow * p.ldc + cn0 + nq * 32) * OSZ));
-      };
-      // the partials summed in slice order (bit-exact whichever slice arrived last), one quadrant
-      // (8 loads) at a time: a 16-load batch for S = 2 spilled (16 B of scratch) and wrote wrong
-      // rows (r5_6 diag_ksr); this form keeps every value in registers and is exact
-#pragma unroll
-      for (int mq = 0; mq < 2; ++mq)
-#pragma unroll
-        for (int nq = 0; nq < 2; ++nq) {
-          f32x4 s0[4], s1[4];
-          for (int sl = 0; sl < S; ++sl) {
-            f32x4 v0[4], v1[4];
-            if (sl == cks) {
-#pragma unroll
-              for (int f = 0; f < 4; ++f) {
-                v0[f] = acc[mq * 4 + f][nq * 2];
-                v1[f] = acc[mq * 4 + f][nq * 2 + 1];
-              }
-            } else {
-#pragma unroll
-              for (int f = 0; f < 4; ++f) {
-                v0[f] = ld(w_off(mq, f, nq) + (unsigned)sl * slab, 0);
-                v1[f] = ld(w_off(mq, f, nq) + (unsigned)sl * slab, 16);
-              }
-            }
-#pragma unroll
-            for (int f = 0; f < 4; ++f) {
-              s0[f] = sl == 0 ? v0[f] : s0[f] + v0[f];
-              s1[f] = sl == 0 ? v1[f] : s1[f] + v1[f];
-            }
-          }
-#pragma unroll
-          for (int f = 0; f < 4; ++f) store_c(mq, f, nq, s0[f], s1[f]);
-        }
-    };
-    for (ti = 0; ti < my_tiles; ++ti) {
-      if (ti > 0 && g1) T4_BAR();  // re-stagger the wave groups (the prologue's, for tile 0)
-      tile_body(std::integral_constant<int, 4>{}, std::integral_constant<int, 3>{});
-      if (!g1) T4_BAR();  // align the groups
-      wait_vm<0>();
-      ks_reduce();
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  } else {
-    ti = 0;
-    tile_body(std::integral_constant<int, DEFER ? 4 : 0>{}, K1{});
-    for (ti = 1; ti < my_tiles; ++ti) tile_body(std::integral_constant<int, 2>{}, K1{});
-    if (!g1) T4_BAR();
-  }
+  ti = 0;
+  tile_body(std::integral_constant<int, DEFER ? 4 : 0>{}, K1{});
+  for (ti = 1; ti < my_tiles; ++ti) tile_body(std::integral_constant<int, 2>{}, K1{});
+  if (!g1) T4_BAR();
 #undef T4_BAR
 #undef T4_LGKM0
   wait_vm<0>();  // never leave an LDS-DMA in flight past the end of the workgroup
@@ -1716,7 +1483,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
 // its vmcnt (vmcnt counts loads, LDS-DMA and stores together, in issue order). The stage cursors
 // advance incrementally (no integer division in the loop) and the tile's last K-tile is a
 // separate instantiation of the body, so the steady-state loop carries no store code.
-// Measured (scripts/lab, profiles/r01/s2/lab/): 65536x1024x1024 bf16 0.1116 ms vs t8 0.1163.
+// Measured (research/lab, profiles/r01/s2/lab/): 65536x1024x1024 bf16 0.1116 ms vs t8 0.1163.
 template <class Mma, int OUT>
 __global__ __launch_bounds__(512) void gemm_tn_pt8_kernel(const GemmArgs p) {
   constexpr int ROWB = 128, UNIT = 128 * ROWB, STAGE = 4 * UNIT;
@@ -2144,10 +1911,8 @@ hipError_t launch_t8(const GemmArgs& p, hipStream_t s) {
 
 // Write-through C stores (CMODE 2 of pt4 / t4) whenever every C byte is within 2 GiB of p.c
 // (32-bit buffer offsets); C row tables (direct store) and larger outputs keep plain nt stores.
-// DDLB_PT4_NT_STORES=1 forces nt stores (A/B knob).
 inline bool c_fits_wt(const GemmArgs& p, int osz) {
-  static const bool nt = getenv("DDLB_PT4_NT_STORES") != nullptr;
-  if (nt || p.c_table != nullptr || p.M <= 0) return false;
+  if (p.c_table != nullptr || p.M <= 0) return false;
   const int64_t cg = p.c_grp > 0 ? p.c_grp : p.M, cgs = p.c_gstride > 0 ? p.c_gstride : cg;
   const int64_t last_row = (int64_t)(p.M - 1) / cg * cgs + (int64_t)(p.M - 1) % cg;
   return (last_row * p.ldc + p.N) * (int64_t)osz < 0x7FFFFFF0LL;
@@ -2174,19 +1939,6 @@ bool pt4_ok(const GemmArgs& p, int esz) {
                                          : (p.a_grp == p.M || p.a_grp % 256 == 0);
   return p.M % 256 == 0 && p.N % 256 == 0 && a_ok && p.act == ACT_NONE && nk >= 2 &&
          nk % 2 == 0 && p.lda * esz <= (1 << 22) && p.ldb * esz <= (1 << 22);
-}
-
-// DDLB_PT4_HALF_LINES=1: the ungated 16-bit write-through pt4 stores C in half lines per
-// instruction as before round 5 (A/B knob against the whole-line stores)
-inline bool half_lines() {
-  static const bool h = getenv("DDLB_PT4_HALF_LINES") != nullptr;
-  return h;
-}
-// DDLB_PT4_ONE=1: the ungated 16-bit write-through pt4 runs the ONE schedule (one section per
-// K-tile and wave group, see the kernel)
-inline bool one_section() {
-  static const bool h = getenv("DDLB_PT4_ONE") != nullptr;
-  return h;
 }
 
 template <class Mma, int OUT>
@@ -2222,13 +1974,6 @@ hipError_t launch_pt4(const GemmArgs& p, hipStream_t s) {
   if (p.ksplit > 1) {  // (gemm_launch routes only eligible K-splits here: plain rows, ungated)
     if (p.flags != nullptr || apan || p.c_table != nullptr || p.c_grp != p.M || !wt)
       return hipErrorNotSupported;
-    if (p.ks_ws != nullptr) {  // in-launch reduction: C written once; f32 slabs within 2 GiB
-      if (p.ks_cnt == nullptr || (int64_t)p.ksplit * p.M * p.N * 4 >= 0x7FFFFFF0LL)
-        return hipErrorNotSupported;
-      hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false, 2, false, true, true>), dim3(grid),
-                         dim3(512), 0, s, q);
-      return hipGetLastError();
-    }
     if ((int64_t)p.ksplit * p.M * p.ldc * out_size<OUT>() >= 0x7FFFFFF0LL)
       return hipErrorNotSupported;
     hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false, 2, false, true>), dim3(grid),
@@ -2260,16 +2005,7 @@ hipError_t launch_pt4(const GemmArgs& p, hipStream_t s) {
                        s, q);
   else if (p.c_table != nullptr)
     hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false, 1>), dim3(grid), dim3(512), 0, s, p);
-  else if (wt && OUT != DT_F32 && half_lines()) {  // A/B knob: the round-4 half-line C stores
-    if constexpr (OUT != DT_F32)
-      hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false, 2, false, false, false, false>),
-                         dim3(grid), dim3(512), 0, s, p);
-  } else if (wt && OUT != DT_F32 && one_section() &&
-             (int64_t)p.K * Mma::kElem / 128 >= 4) {  // (ONE: both cursors within the next tile)
-    if constexpr (OUT != DT_F32)
-      hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false, 2, false, false, false, true, true>),
-                         dim3(grid), dim3(512), 0, s, p);
-  } else if (wt)
+  else if (wt)
     hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false, 2>), dim3(grid), dim3(512), 0, s, p);
   else
     hipLaunchKernelGGL((gemm_tn_pt4_kernel<Mma, OUT, false>), dim3(grid), dim3(512), 0, s, p);

@@ -30,7 +30,6 @@
 #include <hip/hip_fp16.h>
 #include <stdint.h>
 
-#include <cstdlib>
 
 #include "gemm.h"
 #include "gemm_entry.h"
@@ -83,10 +82,6 @@ int choose_tile(int64_t M, int64_t N, int64_t K, int din) {
 hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mode,
                        hipStream_t s) {
   GemmArgs p = p_in;
-  static const int raster_env = getenv("DDLB_RASTER_G") ? atoi(getenv("DDLB_RASTER_G")) : 0;
-  if (raster_env > 0) p.raster_g = raster_env;  // A/B knob of the tile raster (tile_map.h)
-  static const int cnt_env = getenv("DDLB_PT4_C_NT") ? atoi(getenv("DDLB_PT4_C_NT")) : 0;
-  if (cnt_env > 0) p.c_nt = 1;  // A/B knob: pt4's whole-line C stores nt instead of sc1 | nt
   if (p.a_grp <= 0) { p.a_grp = p.M > 0 ? p.M : 1; p.a_gstride = p.a_grp; }
   if (p.c_grp <= 0) { p.c_grp = p.M > 0 ? p.M : 1; p.c_gstride = p.c_grp; }
   switch (tile) {  // known codes only (the retired families' codes are refused, not rerouted)
@@ -96,7 +91,6 @@ hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mo
     default: return hipErrorInvalidValue;
   }
   if (p.M == 0 || p.N == 0) return hipSuccess;
-  if (p.ks_ws != nullptr && (p.ksplit < 2 || p.ks_cnt == nullptr)) return hipErrorInvalidValue;
   if (p.ksplit > 1) {
     // K-split: slice j of K columns -> partial j at c + j * M * ldc (the caller sums them). pt4
     // runs every (slice, tile) pair in one launch; any other kernel runs the slices one by one.
@@ -112,8 +106,6 @@ hipError_t gemm_launch(const GemmArgs& p_in, int din, int dout, int tile, int mo
       else if (fast) e = launch_fast(q, din, dout, TILE_PT4, s);
       if (e != hipErrorNotSupported && e != hipErrorInvalidValue) return e;
     }
-    // the in-launch reduction (ks_ws) exists only in pt4: never fall back to partial slabs in C
-    if (p.ks_ws != nullptr) return hipErrorNotSupported;
     const int esz = dtype_size(din), osz = dtype_size(dout);
     for (int j = 0; j < p.ksplit; ++j) {
       GemmArgs q = p;

@@ -57,5 +57,15 @@ struct BumpSignalArgs {
   int n = 0;
 };
 hipError_t bump_signal_launch(const BumpSignalArgs& a, hipStream_t s);
+// CU holder (preflight ``rccl_cap``): ``nwg`` workgroups that each occupy a whole CU as the
+// flag-gated persistent GEMM does (full register file + LDS), count themselves in *arrived and
+// spin until *go != 0 (bounded by spin_limit polls; timeout bit 4 in *timeout_word).
+struct HoldArgs {
+  unsigned* arrived = nullptr;
+  const unsigned* go = nullptr;
+  unsigned* timeout_word = nullptr;
+  unsigned spin_limit = 1u << 24;
+};
+hipError_t hold_cus_launch(const HoldArgs& a, int nwg, hipStream_t s);
 
 }  // namespace ddlb

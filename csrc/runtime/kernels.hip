@@ -268,6 +268,28 @@ __global__ void epoch_bump_kernel(unsigned* epoch) {
   if (threadIdx.x == 0) *epoch += 1;
 }
 
+// CU holder: each workgroup takes a whole CU the way the flag-gated persistent pt4 GEMM does (512
+// threads at 256 VGPRs = the full register file, plus all 160 KB of LDS), counts itself resident
+// in *arrived (host-coherent memory) and spins, bounded, until the host sets *go.
+__global__ __launch_bounds__(512, 1) void hold_cus_kernel(HoldArgs a) {
+  __shared__ char pad[160 * 1024];
+  asm volatile("" ::: "v255");  // a 256-VGPR allocation, as the gated GEMM's
+  pad[threadIdx.x * 320] = 1;   // touched across all 160 KB, so all of it is allocated
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(a.arrived, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    unsigned spins = 0;
+    while (__hip_atomic_load(a.go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
+      __builtin_amdgcn_s_sleep(8);
+      if (++spins > a.spin_limit) {  // bounded: never outlives a lost host
+        atomicOr(a.timeout_word, 4u);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  if (pad[threadIdx.x * 320] != 1) atomicOr(a.timeout_word, 8u);  // (keeps the LDS array)
+}
+
 int grid_for(int64_t work_items) {
   int64_t g = (work_items + 255) / 256;
   if (g > 2048) g = 2048;
@@ -361,6 +383,13 @@ hipError_t wait_launch(const WaitArgs& a, hipStream_t s) {
 hipError_t bump_signal_launch(const BumpSignalArgs& a, hipStream_t s) {
   if (a.epoch == nullptr || a.n < 0 || a.n > kMaxPrologue) return hipErrorInvalidValue;
   hipLaunchKernelGGL(bump_signal_kernel, dim3(1), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t hold_cus_launch(const HoldArgs& a, int nwg, hipStream_t s) {
+  if (nwg < 1 || a.arrived == nullptr || a.go == nullptr || a.timeout_word == nullptr)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(hold_cus_kernel, dim3(nwg), dim3(512), 0, s, a);
   return hipGetLastError();
 }
 

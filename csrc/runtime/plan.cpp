@@ -205,23 +205,8 @@ PlanExecutor::~PlanExecutor() {
 }
 
 void PlanExecutor::load(const std::vector<int64_t>& ops) {
-  if (ops.size() % kOpWords != 0) throw std::runtime_error("plan: bad op array length");
-  std::fill(used_.begin(), used_.end(), false);
-  for (size_t i = 0; i < ops.size(); i += kOpWords) {
-    const int64_t s = ops[i + 1];
-    if (s < 0 || (size_t)s >= streams_.size()) throw std::runtime_error("plan: bad stream index");
-    used_[(size_t)s] = true;
-    const int64_t kind = ops[i];
-    if (kind == OP_RECORD || kind == OP_WAIT) {
-      const int64_t e = ops[i + 2];
-      if (e < 0 || (size_t)e >= events_.size()) throw std::runtime_error("plan: bad event index");
-    }
-    if (kind == OP_GEMM) {
-      if (ops[i + 12] < 0 || ops[i + 13] < 0 || ops[i + 14] <= 0)
-        throw std::runtime_error("plan: bad GEMM shape");
-      if (!ops[i + 2] || !ops[i + 3] || !ops[i + 4]) throw std::runtime_error("plan: null GEMM ptr");
-    }
-  }
+  validate_ops(ops, streams_.size(), events_.size());  // plan_ir.h: every bound exec relies on
+  used_ = used_streams(ops, streams_.size());
   ops_ = ops;
   clear_batch_graphs();
   if (timeline_on_) set_timeline(true);  // one timing event per (new) op
@@ -249,49 +234,8 @@ bool PlanExecutor::graph_capturable() const {
   //    hipStreamEndCapture of this HIP runtime segfaults on it (scripts/diag_graph_edges.py
   //    `cycle`, profiles/r03/r3_15_*). Cycles through the capture's origin stream (the fork /
   //    join every plan has) are fine.
-  if (comm_cus_ > 0) return false;
-  for (size_t i = 0; i < ops_.size(); i += kOpWords) {
-    const int64_t k = ops_[i];
-    if (k == OP_ALLGATHER || k == OP_REDUCE_SCATTER || k == OP_SEND || k == OP_RECV ||
-        k == OP_GROUP_START || k == OP_GROUP_END)
-      return false;
-    if (k == OP_GEMM && ops_[i + 19] != 0 && ops_[i + 29] == 0) return false;
-  }
-  return !side_stream_cycle();
-}
-
-bool PlanExecutor::side_stream_cycle() const {
-  // the stream relations a capture of this plan creates, as enqueue() issues them in graph mode
-  const size_t ns = streams_.size();
-  std::vector<std::vector<char>> adj(ns, std::vector<char>(ns, 0));
-  std::vector<int64_t> rec_on(events_.size(), -1);
-  std::vector<char> effect(ns, 0);
-  auto edge = [&](int64_t a, int64_t b) {
-    if (a >= 1 && b >= 1 && a != b && (size_t)a < ns && (size_t)b < ns) adj[a][b] = 1;
-  };
-  for (size_t i = 0; i < ops_.size(); i += kOpWords) {
-    const int64_t k = ops_[i], st = ops_[i + 1];
-    if (k == OP_RECORD && (size_t)ops_[i + 2] < rec_on.size()) rec_on[(size_t)ops_[i + 2]] = st;
-    if (k == OP_WAIT && (size_t)ops_[i + 2] < rec_on.size()) edge(rec_on[(size_t)ops_[i + 2]], st);
-    if (k == OP_WAIT_SIGNAL)
-      for (size_t j = 0; j < ns; ++j)
-        if (effect[j]) edge((int64_t)j, st);
-    if (k != OP_WAIT_SIGNAL && k != OP_WAIT && k != OP_RECORD && (size_t)st < ns) effect[st] = 1;
-  }
-  // cycle check (colour DFS over at most a few dozen streams)
-  std::vector<int> colour(ns, 0);
-  std::function<bool(size_t)> dfs = [&](size_t u) {
-    colour[u] = 1;
-    for (size_t v = 0; v < ns; ++v) {
-      if (!adj[u][v]) continue;
-      if (colour[v] == 1 || (colour[v] == 0 && dfs(v))) return true;
-    }
-    colour[u] = 2;
-    return false;
-  };
-  for (size_t u = 1; u < ns; ++u)
-    if (colour[u] == 0 && dfs(u)) return true;
-  return false;
+  if (comm_cus_ > 0 || has_uncapturable_op(ops_)) return false;
+  return !side_stream_cycle(ops_, streams_.size(), events_.size());
 }
 
 void PlanExecutor::enable_graph(bool on) {
@@ -419,20 +363,8 @@ void PlanExecutor::enqueue(hipStream_t main) {
     // (each small kernel after a GEMM costs a few us of boundary + L2 write-back)
     BumpSignalArgs b;
     b.epoch = d_epoch_;
-    static const bool fuse = getenv("DDLB_GRAPH_PROLOGUE") == nullptr ||
-                             atoi(getenv("DDLB_GRAPH_PROLOGUE")) != 0;  // A/B knob
-    for (; fuse && first < ops_.size(); first += kOpWords) {
-      const int64_t* o = &ops_[first];
-      if (o[0] != OP_SIGNAL || o[1] != 0 || o[2] < 1 || o[2] > kMaxSignal ||
-          b.n + o[2] > kMaxPrologue)
-        break;
-      for (int i = 0; i < (int)o[2]; ++i) {
-        b.ptr[b.n] = (unsigned*)o[5 + i];
-        b.delta[b.n] = (int)o[4];
-        ++b.n;
-      }
-      touched_[0] = true;
-    }
+    first = fused_prologue(ops_, b);
+    if (first > 0) touched_[0] = true;
     DDLB_HIP(bump_signal_launch(b, main));
   }
   if (any_side_ || compute_) {
@@ -538,38 +470,11 @@ unsigned PlanExecutor::run(uintptr_t main_stream) {
 }
 
 GemmArgs PlanExecutor::gemm_args(const int64_t* o) const {
-  GemmArgs g;
-  g.a = (const void*)o[2];
-  g.b = (const void*)o[3];
-  g.c = (void*)o[4];
-  g.lda = o[5]; g.ldb = o[6]; g.ldc = o[7];
-  g.a_grp = o[8]; g.a_gstride = o[9];
-  g.c_grp = o[10]; g.c_gstride = o[11];
-  g.M = (int)o[12]; g.N = (int)o[13]; g.K = (int)o[14];
-  g.flags = (const unsigned*)o[19];
+  GemmArgs g = decode_gemm(o);  // plan_ir.h
   g.epoch = epoch_;
-  g.flag_rows = o[20] > 0 ? o[20] : 1;
-  g.nshards = o[21] > 0 ? (int)o[21] : 1;
-  g.first_shard = (int)o[22];
-  g.tile_order = (int)o[23];
-  g.nsub = o[27] > 0 ? (int)o[27] : 1;
-  g.reserve_cus = (int)o[28];
-  g.ag_ctas = (int)(o[29] & 0xfffff);
-  g.ag_parts = (int)((o[29] >> 20) & 0xfffff);
-  g.ag_rank = (int)((o[29] >> 40) & 0xffff);
-  g.ag_mode = (int)((o[29] >> 56) & 0x7f);
-  g.ag_tab = (const uint64_t*)o[30];
-  g.act = (int)o[24];
-  g.a_table = (const uint64_t*)o[25];
-  g.shard_rows = o[26];
-  g.c_table = (const uint64_t*)o[32];
-  g.c_shard_rows = o[33];
-  g.ksplit = o[31] > 1 ? (int)o[31] : 1;
-  g.ks_ws = (float*)o[34];
-  g.ks_cnt = (unsigned*)o[35];
   g.timeout_word = d_timeout_;
   // DDLB_SPIN_LIMIT: polls before a gated GEMM's bounded spin gives up (diagnostics that provoke
-  // a blocked producer on purpose, scripts/diag_gate_placement.py); default ~30 s
+  // a blocked producer on purpose, research/diag/diag_gate_placement.py); default ~30 s
   static const unsigned spin_env = getenv("DDLB_SPIN_LIMIT") ? (unsigned)atol(getenv("DDLB_SPIN_LIMIT")) : 0u;
   if (spin_env > 0) g.spin_limit = spin_env;
   g.epoch_ptr = graph_on_ ? d_epoch_ : nullptr;

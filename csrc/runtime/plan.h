@@ -17,41 +17,11 @@
 
 #include "../comm/comm.h"
 #include "../gemm/gemm.h"
+#include "plan_ir.h"
 
 namespace ddlb {
 
-// Op layout: kOpWords int64 per op. word 0 = kind, word 1 = stream index.
-constexpr int kOpWords = 36;
-enum OpKind : int64_t {
-  OP_NOP = 0,
-  OP_GEMM = 1,        // 2 a, 3 b, 4 c, 5 lda, 6 ldb, 7 ldc, 8 a_grp, 9 a_gstride, 10 c_grp,
-                      // 11 c_gstride, 12 M, 13 N, 14 K, 15 din, 16 dout, 17 tile, 18 mode,
-                      // 19 flags ptr (0 = none), 20 flag_rows, 21 nshards, 22 first_shard,
-                      // 23 tile_order, 24 fused epilogue activation, 25 A shard table,
-                      // 26 A shard rows, 27 nsub, 28 reserve_cus, 29 in-kernel all-gather
-                      // (ctas | parts << 20 | rank << 40 | mode << 56), 30 its table,
-                      // 31 K-split slices, 32 C shard table (direct store), 33 C shard rows,
-                      // 34 K-split f32 workspace (in-launch reduction), 35 its tile counters
-  OP_RECORD = 2,      // 2 event
-  OP_WAIT = 3,        // 2 event
-  OP_ALLGATHER = 4,   // 2 send, 3 recv, 4 count per rank, 5 dtype
-  OP_REDUCE_SCATTER = 5,  // 2 send, 3 recv, 4 recv count, 5 dtype
-  OP_SEND = 6,        // 2 buf, 3 count, 4 dtype, 5 peer
-  OP_RECV = 7,        // 2 buf, 3 count, 4 dtype, 5 peer
-  OP_GROUP_START = 8,
-  OP_GROUP_END = 9,
-  OP_COPY = 10,       // 2 dst, 3 src, 4 bytes, 5 method (0 copy engine, 1 CU kernel),
-                      // 6 max CU blocks (kernel method)
-  OP_SIGNAL = 11,     // 2 n, 3 method (0 kernel, 1 stream write), 4 delta, 5.. flag ptrs;
-                      //   stores value = epoch + delta
-  OP_WAIT_SIGNAL = 12,  // 2 n, 3 method (0 kernel, 1 stream wait), 4 delta, 5.. flag ptrs;
-                        //   waits until every flag >= epoch + delta
-  OP_REDUCE = 13,     // 2 dst, 3 count, 4 dtype, 5 nsrc, 6.. src ptrs
-  OP_MEMSET = 14,     // 2 dst, 3 bytes, 4 byte value
-  OP_COPY_MULTI = 15, // 2 nseg, 3 max blocks, then (dst, src, bytes) triples from word 4
-  OP_COPY_BATCH = 16, // 2 nseg, then (dst, src, bytes) triples from word 4: copy-engine copies
-                      //   submitted as ONE hipMemcpyBatchAsync (multicast_protocol=batch_memcpy)
-};
+// Op layout and kinds: plan_ir.h (the host-only decoder / validator this executor runs on).
 // hipMemcpyBatchAsync, resolved at run time (dlsym): the HIP runtime torch ships (7.0) predates
 // it, so a batch falls back to one hipMemcpyAsync per segment on the same stream there.
 bool copy_batch_api_available();
@@ -146,7 +116,6 @@ class PlanExecutor {
   std::vector<hipEvent_t> sync_ev_;
   std::vector<bool> touched_;  // graph capture: stream has an effectful op (not a wait / record)
   void join_others(int64_t stream, hipStream_t main);
-  bool side_stream_cycle() const;  // see graph_capturable
   RcclComm* comm_ = nullptr;
   bool timeline_on_ = false;
   hipEvent_t tl_start_ = nullptr;

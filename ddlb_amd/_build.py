@@ -47,7 +47,7 @@ SOURCES = [  # heaviest translation units first (the parallel build's critical p
 ]
 HEADERS = ["gemm/gemm.h", "gemm/gemm_kernels.h", "gemm/gemm_entry.h", "gemm/tile_map.h",
            "runtime/kernels.h",
-           "comm/comm.h", "runtime/plan.h"]
+           "comm/comm.h", "runtime/plan.h", "runtime/plan_ir.h"]
 
 
 def ext_path() -> str:

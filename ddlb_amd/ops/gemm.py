@@ -115,19 +115,15 @@ def split_k_factor(M: int, N: int, K: int, esz: int, ncu: int = 0) -> int:
 
 def gemm(a, w, out=None, *, out_dtype=None, tile: str = "auto", mode: str = "auto",
          M: Optional[int] = None, a_grp: int = 0, a_gstride: int = 0, c_grp: int = 0,
-         c_gstride: int = 0, stream=None, act: str = "none", ksplit: int = 0,
-         ks_form: str = "reduce"):
+         c_gstride: int = 0, stream=None, act: str = "none", ksplit: int = 0):
     """``out[:M] = act(a[:M] @ w.T)`` on the current HIP stream (grouped-row addressing and a
     fused epilogue activation — none / gelu (tanh) / relu / silu — optional). ``ksplit``: 0 =
     auto (:func:`split_k_factor` for plain-row auto-tile GEMMs with no activation and a dense
-    output), 1 = never, S > 1 = S slices. A pt4 split rounds once either way: ``ks_form``
-    "reduce" = one launch over (slice, tile) pairs into f32 partials + the reduce kernel
-    (0.1122 ms on 8192 x 1024 x 8192 bf16, ``profiles/r05/r5_14_*``), "inlaunch" = the same
-    launch reduces them (``GemmArgs::ks_ws``, slower on every shape measured)."""
+    output), 1 = never, S > 1 = S slices. A pt4 split runs one launch over (slice, tile) pairs
+    into f32 partials, summed in slice order and rounded once by the reduce kernel (0.1122 ms on
+    8192 x 1024 x 8192 bf16, ``profiles/r05/r5_14_*``)."""
     import torch
 
-    if ks_form not in ("reduce", "inlaunch"):
-        raise ValueError(f"ks_form must be 'reduce' or 'inlaunch', not {ks_form!r}")
     C = load()
     if out is None:
         rows = M if M is not None else a.shape[0]
@@ -168,33 +164,18 @@ def gemm(a, w, out=None, *, out_dtype=None, tile: str = "auto", mode: str = "aut
             if stream is not None:
                 part.record_stream(torch.cuda.ExternalStream(s))
             return out
+        # every (slice, tile) pair in one launch into f32 partials, summed in slice order and
+        # rounded once by the reduce kernel (an unsplit GEMM's rounding)
         ws = torch.empty((S, M, N), dtype=torch.float32, device=a.device)
-        keep = [ws]
-        if ks_form == "inlaunch":
-            # the slices' f32 partials meet in the workspace and the last slice of each tile
-            # writes out (csrc/gemm/gemm.h ks_ws); fresh zeroed tile counters per call, so
-            # concurrent calls on different streams never share them
-            cnt = torch.zeros((2 * (M // 256) * (N // 256),), dtype=torch.int32,
-                              device=a.device)
-            keep.append(cnt)
-            C.gemm(a.data_ptr(), w.data_ptr(), out.data_ptr(), a.stride(0), w.stride(0), N, M,
-                   N, K // S, dtype_code(a.dtype), dtype_code(out.dtype), TILES["pt4"],
-                   MODES[mode], 0, 0, 0, 0, s, 0, S, ws.data_ptr(), cnt.data_ptr())
+        C.gemm(a.data_ptr(), w.data_ptr(), ws.data_ptr(), a.stride(0), w.stride(0), N, M, N,
+               K // S, dtype_code(a.dtype), DT_F32, TILES["pt4"], MODES[mode], 0, 0, 0, 0, s, 0, S)
+        if out.dtype == torch.float32:
+            C.reduce_sum(out.data_ptr(), [ws[j].data_ptr() for j in range(S)], M * N, DT_F32, s)
         else:
-            # every (slice, tile) pair in one launch into f32 partials, summed in slice order
-            # and rounded once by the reduce kernel (an unsplit GEMM's rounding)
-            C.gemm(a.data_ptr(), w.data_ptr(), ws.data_ptr(), a.stride(0), w.stride(0), N, M, N,
-                   K // S, dtype_code(a.dtype), DT_F32, TILES["pt4"], MODES[mode], 0, 0, 0, 0,
-                   s, 0, S)
-            if out.dtype == torch.float32:
-                C.reduce_sum(out.data_ptr(), [ws[j].data_ptr() for j in range(S)], M * N,
-                             DT_F32, s)
-            else:
-                C.reduce_sum(out.data_ptr(), [ws[j].data_ptr() for j in range(S)], M * N,
-                             dtype_code(out.dtype), s, DT_F32)
+            C.reduce_sum(out.data_ptr(), [ws[j].data_ptr() for j in range(S)], M * N,
+                         dtype_code(out.dtype), s, DT_F32)
         if stream is not None:  # the workspace stays allocated until that stream reaches it
-            for t in keep:
-                t.record_stream(torch.cuda.ExternalStream(s))
+            ws.record_stream(torch.cuda.ExternalStream(s))
         return out
     C.gemm(a.data_ptr(), w.data_ptr(), out.data_ptr(), a.stride(0), w.stride(0), out.stride(0),
            M, N, K, dtype_code(a.dtype), dtype_code(out.dtype), TILES[tile], MODES[mode],

@@ -94,9 +94,6 @@ class AlgoConfig:
     # kernel in the queue, 0.19 vs 0.23 ms (s4) emulated at d = 8 with fast and with link-like
     # slow collectives, profiles/r04/r4_12_ab_*)
     sig_side: bool = False
-    # K-split GEMMs (few tiles, long K): reduce the slices inside the launch (one kernel, f32
-    # partials, one rounding) instead of a reduce op over output-dtype partials (see _full_gemm)
-    ks_fused: bool = False
 
 
 @dataclass
@@ -188,27 +185,14 @@ def _full_gemm(plan: Plan, a_ref: Ref, Bt: Ref, c_ref: Ref, M: int, N: int, K: i
     the S (slice, tile) pairs (slice s = K/S columns of A and Bt).
 
     Default: the launch writes S partials (output dtype) to a scratch buffer and a reduce op sums
-    them in f32 into C (BASELINE config #2 shape: 0.1009 ms, r4_22). ``cfg.ks_fused``: the launch
-    reduces them itself (per tile, the last slice to arrive sums the others' f32 partials from a
-    workspace with its own and writes C once: one kernel, one rounding; csrc/gemm/gemm.h
-    ``ks_ws``), measured slower on that shape (GEMM 0.1128 vs 0.1022 ms, profiles/r05/r5_19):
-    every workgroup finishes its single tile together, so the partial stores, the arrival poll
-    and the partial loads form one serial chain at the end of the kernel where the two-kernel
-    form overlaps its stores with the last K-tile and reads back at full bandwidth."""
+    them in f32 into C (BASELINE config #2 shape: 0.1009 ms, r4_22). (A form that reduced inside
+    the launch -- the last slice of each tile summing the others' f32 partials -- was measured
+    slower, GEMM 0.1128 vs 0.1022 ms, profiles/r05/r5_19, and retired in round 6: every
+    workgroup finishes its single tile together, so the partial stores, the arrival poll and the
+    partial loads form one serial chain at the end of the kernel.)"""
     S = _split_k(plan, M, N, K, ein, cfg)
     if S == 1:
         plan.gemm(S_MAIN, a_ref, Bt, c_ref, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, **gdt)
-        return
-    if cfg.ks_fused:
-        ws = plan.buffer(tag, S * M * N * 4)
-        # the tile counters live in ordinary (cached) device memory like the workspace, zeroed
-        # once at bind (local buffers are torch.zeros; counts are epoch-relative, never reset):
-        # NOT a zero=True flag buffer, which the binder puts in uncached memory -- there the
-        # count's atomic overtook the drained partial stores (r5_17: 50 of 8.4 M outputs read a
-        # stale partial), and the budget emulator would pre-set it like a flag
-        cnt = plan.buffer(tag + "_cnt", max(256, 8 * (M // 256) * (N // 256)))
-        plan.gemm(S_MAIN, a_ref, Bt, c_ref, M=M, N=N, K=K // S, lda=K, ldb=K, ldc=N, ksplit=S,
-                  ks_ws=ws, ks_cnt=cnt, **dict(gdt, tile=TILE_PT4))
         return
     part = plan.buffer(tag, S * M * N * eout)
     plan.gemm(S_MAIN, a_ref, Bt, part, M=M, N=N, K=K // S, lda=K, ldb=K, ldc=N, ksplit=S,
@@ -223,7 +207,7 @@ def _full_gemm(plan: Plan, a_ref: Ref, Bt: Ref, c_ref: Ref, M: int, N: int, K: i
 # whatever the other arrays have free. MI355X: 32 arrays (4 per XCD) of 8 active CUs (KFD topology:
 # array_count 32, cu_per_simd_array 9 of which 8 enabled); the gated grid is spread evenly (one
 # workgroup per CU, round-robin), so a reserve of one CU per array (256 / 8 = 32) leaves every array
-# a free CU. Measured (scripts/diag_gate_placement.py, profiles/r05/r5_6_gate_placement.txt): grid
+# a free CU. Measured (research/diag/diag_gate_placement.py, profiles/r05/r5_6_gate_placement.txt): grid
 # 224 (reserve 32) ran with feeders of 32, 64 and 256 workgroups; 232 (reserve 24) blocked with 32
 # or 256 and ran with 8; 240 (reserve 16) blocked with 64, ran with 16 -- exactly the hangs of
 # profiles/r04/r4_32..r4_36. Smaller requests are raised to this floor.

@@ -127,9 +127,12 @@ class NativeContext:
             if self.world > 1:
                 dist.broadcast_object_list(obj, src=0)
             comm = self.C.RcclComm(obj[0], self.world, self.rank, self.device_index, cap)
+            # (comm.max_ctas is the cap WE passed in ncclConfig_t, a binding consistency check
+            # only; what RCCL actually needs beside a gated GEMM is observed by the rccl_cap
+            # preflight phase, which holds num_cus - cap CUs while the capped collective runs)
             if int(comm.max_ctas) != cap:
-                raise RuntimeError(f"RCCL communicator: asked for a {cap}-CTA cap, got "
-                                   f"{comm.max_ctas}")
+                raise RuntimeError(f"RCCL communicator binding: asked for a {cap}-CTA cap, "
+                                   f"recorded {comm.max_ctas}")
             self._rccl[cap] = comm
         return self._rccl[cap]
 
@@ -162,8 +165,14 @@ class NativeContext:
             b.close()
         self._owned = []
         comms, self._rccl = list(self._rccl.values()), {}
-        for c in comms:
-            c.destroy()
+        first = None
+        for c in comms:  # every communicator is destroyed even if one destroy() raises
+            try:
+                c.destroy()
+            except Exception as e:  # noqa: BLE001 (re-raised below)
+                first = first or e
+        if first is not None:
+            raise first
 
 
 def rccl_buffers(plan: Plan) -> List[str]:

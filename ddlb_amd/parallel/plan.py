@@ -19,7 +19,7 @@ from __future__ import annotations
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
-OP_WORDS = 36
+OP_WORDS = 34
 (OP_NOP, OP_GEMM, OP_RECORD, OP_WAIT, OP_ALLGATHER, OP_REDUCE_SCATTER, OP_SEND, OP_RECV,
  OP_GROUP_START, OP_GROUP_END, OP_COPY, OP_SIGNAL, OP_WAIT_SIGNAL, OP_REDUCE, OP_MEMSET,
  OP_COPY_MULTI, OP_COPY_BATCH) = range(17)
@@ -127,7 +127,7 @@ class Plan:
              a_shards: Optional[Sequence[Ref]] = None, shard_rows: int = 0,
              nsub: int = 1, reserve_cus: int = 0, ag: Optional[dict] = None,
              c_shards: Optional[Sequence[Ref]] = None, c_shard_rows: int = 0,
-             ksplit: int = 1, ks_ws: Optional[Ref] = None, ks_cnt: Optional[Ref] = None) -> Op:
+             ksplit: int = 1) -> Op:
         """``a_shards``: A row block s (``shard_rows`` rows each) is read from ``a_shards[s]``
         (a peer's copy for a direct-access GEMM that pulls its operand over xGMI).
         ``flags`` (arrival-gated tiles): shard ``i`` = rows ``[i*flag_rows, (i+1)*flag_rows)`` may
@@ -145,19 +145,13 @@ class Plan:
         partials straight over xGMI; ``tile_order=2`` interleaves the blocks (every destination's
         tiles in flight at once). ``ksplit`` > 1: K-split, ``K`` is the slice length (``lda`` /
         ``ldb`` the full rows); slice s reads A / B columns ``[s K, (s + 1) K)`` and writes its
-        partial product at ``c + s * M * ldc`` elements (plain rows only; the caller sums them),
-        or, with ``ks_ws`` (f32 workspace of ``ksplit * M * N`` floats) and ``ks_cnt`` (2 words
-        per 256x256 tile, zero-initialised, never reset), C itself: the launch reduces the slices
-        (csrc/gemm/gemm.h ``ks_ws``)."""
+        partial product at ``c + s * M * ldc`` elements (plain rows only; the caller sums them
+        with a reduce op)."""
         if ksplit < 1 or (ksplit > 1 and (flags is not None or a_shards is not None or
                                           c_shards is not None or ag is not None or act or
                                           a_grp not in (0, M) or c_grp not in (0, M))):
             raise ValueError("ksplit > 1 takes plain rows only (no flags, tables, all-gather, "
                              "activation or grouped rows)")
-        if (ks_ws is None) != (ks_cnt is None) or (ks_ws is not None and (
-                ksplit < 2 or ldc != N or M % 256 or N % 256)):
-            raise ValueError("ks_ws / ks_cnt (in-launch K-split reduction) go together, with "
-                             "ksplit > 1, whole 256x256 tiles and a dense C (ldc == N)")
         if nsub < 1 or nshards % nsub:
             raise ValueError(f"nsub ({nsub}) must divide nshards ({nshards})")
         if ag is not None:
@@ -196,8 +190,7 @@ class Plan:
                          shard_rows=shard_rows, a_table=a_table, nsub=nsub,
                          reserve_cus=reserve_cus, ag=ag,
                          c_shards=list(c_shards) if c_shards is not None else None,
-                         c_shard_rows=c_shard_rows, c_table=c_table, ksplit=ksplit,
-                         ks_ws=ks_ws, ks_cnt=ks_cnt)
+                         c_shard_rows=c_shard_rows, c_table=c_table, ksplit=ksplit)
 
     def table(self, name: str, refs: Sequence[Ref]) -> Ref:
         """Device array of 64-bit addresses of ``refs`` (written once when the plan is bound)."""
@@ -301,8 +294,6 @@ class Plan:
                 if a.get("c_table") is not None:
                     w[32], w[33] = resolve(a["c_table"]), a["c_shard_rows"]
                 w[31] = a.get("ksplit", 1)
-                if a.get("ks_ws") is not None:
-                    w[34], w[35] = resolve(a["ks_ws"]), resolve(a["ks_cnt"])
             elif k in (OP_RECORD, OP_WAIT):
                 w[2] = a["event"]
             elif k in (OP_ALLGATHER, OP_REDUCE_SCATTER):

@@ -30,6 +30,15 @@ check           what it proves (every rank, every peer, two epochs)
                 gate acquire, ACK stores across the link), validated against fp32
 ``ipc_dstore``  the direct-store epilogue: a GEMM whose C row blocks are written straight into
                 every peer's receive slot (tp_rowwise p2p fused), then the d-way reduce, validated
+``rccl_cap``    the CTA cap the RCCL-fed gated GEMM relies on, OBSERVED: every CU but ``cap`` is
+                held the way the gated GEMM holds it (one 512-thread workgroup per CU, the full
+                register file and LDS, spinning), then an all-gather on the communicator capped
+                at ``cap`` workgroups must finish on the CUs left free within a bound; it is
+                timed against the same all-gather with nothing held. A collective that needs
+                more CUs than the cap, or cannot run where the held CUs leave room, fails this
+                phase (the holders are released by the host, so it never hangs) and drops the
+                RCCL-fed fused family -- the communicator's own ``max_ctas`` is only what we
+                asked RCCL for
 ``rccl_fused``  RCCL stage all-gathers feeding ONE flag-gated GEMM through signal kernels on the
                 comm stream (coll_pipeline backend=rccl fused=True), validated
 ==============  ==================================================================================
@@ -56,7 +65,7 @@ from ddlb_amd.parallel.plan import (COPY_ENGINE, DT_F32, DT_U8, SIG_KERNEL, SIG_
 
 IPC_PHASES = ("ipc", "ipc_ksig", "ipc_kernel", "ipc_sdma", "ipc_push", "ipc_batch", "ipc_agk",
               "ipc_dstore")
-RCCL_PHASES = ("torch_nccl", "rccl", "rccl_fused", "rccl_fused_cm")
+RCCL_PHASES = ("torch_nccl", "rccl", "rccl_cap", "rccl_fused", "rccl_fused_cm")
 # phases that run a whole primitive (the real plan builder) instead of a data-movement plan:
 # (primitive, options); the shape is PRIMITIVE_SHAPE(d)
 PRIMITIVE_PHASES = {
@@ -229,12 +238,13 @@ class _Progress:
 def _run_checked(name: str, progress: _Progress, fn: Callable[[], None]) -> bool:
     t0 = time.perf_counter()
     try:
-        fn()
+        detail = fn()
     except Exception as e:  # recorded, never raised: the other phases still run
-        progress.put(name, f"failed: {type(e).__name__}: {str(e).splitlines()[0][:160]}"
+        progress.put(name, f"failed: {type(e).__name__}: {str(e).splitlines()[0][:200]}"
                      if str(e) else f"failed: {type(e).__name__}")
         return False
-    progress.put(name, f"ok ({(time.perf_counter() - t0) * 1e3:.0f} ms)")
+    extra = f"; {detail}" if isinstance(detail, str) and detail else ""
+    progress.put(name, f"ok ({(time.perf_counter() - t0) * 1e3:.0f} ms{extra})")
     return True
 
 
@@ -297,6 +307,7 @@ def phase_checks(comm, family: str, nbytes: int = PATTERN_BYTES, count: int = RS
     if family == "rccl":
         fns["torch_nccl"] = lambda: _torch_nccl_check(comm)
         fns["rccl"] = lambda: _own_rccl_check(comm, nbytes, count)
+        fns["rccl_cap"] = lambda: _rccl_cap_check(comm)
     return fns
 
 
@@ -361,6 +372,123 @@ def _own_rccl_check(comm, nbytes: int, count: int) -> None:
         bound.close()
 
 
+def fused_rccl_cap(d: int) -> int:
+    """The CTA cap the RCCL-fed fused candidates bind their communicator with (the plan's
+    ``rccl_max_ctas``, ``NativeContext.rccl``), from the rccl_fused phase's own plan."""
+    from ddlb_amd.parallel.algorithms import build_tp_columnwise
+    from ddlb_amd.parallel.context import rccl_gate_cap
+    from ddlb_amd.parallel.plan import DT_BF16
+    from ddlb_amd.primitives.native_common import algo_config
+    from ddlb_amd.primitives.registry import resolve
+
+    prim, opts = PRIMITIVE_PHASES["rccl_fused"]
+    cls, o, _ = resolve(prim, "native", dict(opts))
+    merged = {**cls.DEFAULT_OPTIONS, **o}
+    for key, alias in cls.OPTION_ALIASES.items():
+        merged[key] = alias.get(merged[key], merged[key])
+    plan, _ = build_tp_columnwise(0, d, *PRIMITIVE_SHAPES["rccl_fused"](d), DT_BF16, DT_BF16,
+                                  algo_config(merged))
+    return rccl_gate_cap(plan)
+
+
+def cap_probe(holder, launch, done, barrier, ncu: int, cap: int, resident_s: float = 2.0,
+              finish_s: float = 5.0, sleep=time.sleep, clock=time.perf_counter) -> Dict:
+    """The rccl_cap observation, independent of the device layer (tests drive it with fakes):
+    hold ``ncu - cap`` CUs (``holder.start(n)``; wait until ``holder.arrived() == n``), barrier,
+    ``launch()`` the capped collective, poll ``done()`` for ``finish_s``, release the holders in
+    every case. Raises if the holders never became resident, if the collective did not finish
+    while they held their CUs, or if a holder's own bounded spin gave up."""
+    n = ncu - cap
+    if n < 1:
+        raise ValueError(f"cap {cap} leaves nothing to hold on {ncu} CUs")
+    holder.start(n)
+    try:
+        t0 = clock()
+        while holder.arrived() < n and clock() - t0 < resident_s:
+            sleep(0.001)
+        got = holder.arrived()
+        if got < n:
+            raise RuntimeError(f"only {got} of {n} holder workgroups became resident in "
+                               f"{resident_s:.0f} s (another process on the GPU?)")
+        barrier()  # every rank holds its CUs before any collective starts
+        t1 = clock()
+        launch()
+        while not done() and clock() - t1 < finish_s:
+            sleep(0.0002)
+        held_ms = (clock() - t1) * 1e3
+        finished = done()
+    finally:
+        holder.release()
+    if holder.timeout_bits():
+        raise RuntimeError("a holder's bounded spin gave up (host release lost?)")
+    if not finished:
+        raise RuntimeError(f"the all-gather capped at {cap} workgroups did not finish within "
+                           f"{finish_s:.0f} s beside {n} held CUs: RCCL needs more CUs than the "
+                           "cap (or other ones) -- the RCCL-fed gated GEMM could hang here")
+    return {"held_cus": n, "cap": cap, "held_ms": round(held_ms, 3)}
+
+
+def _rccl_cap_check(comm, nbytes: int = PATTERN_BYTES) -> str:
+    """rccl_cap on the device: the capped all-gather beside ``num_cus - cap`` held CUs, checked
+    bytewise, and timed against the same all-gather with nothing held."""
+    import torch
+
+    from ddlb_amd.parallel.plan import DT_U8
+
+    r, d, dev = comm.rank, comm.world_size, comm.device
+    ctx = comm.native()
+    cap = fused_rccl_cap(d)
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    rc = ctx.rccl(cap)
+    send = pattern(r, nbytes).to(dev)
+    recv = torch.full((d * nbytes // 4,), -1, dtype=torch.int32, device=dev)
+    s_comm = torch.cuda.Stream(dev, priority=-1)
+    s_hold = torch.cuda.Stream(dev)
+    ev = torch.cuda.Event()
+
+    def launch():
+        rc.all_gather(send.data_ptr(), recv.data_ptr(), nbytes, DT_U8, s_comm.cuda_stream)
+        ev.record(s_comm)
+
+    torch.cuda.synchronize(dev)
+    comm.barrier()
+    t0 = time.perf_counter()
+    launch()
+    ev.synchronize()
+    free_ms = (time.perf_counter() - t0) * 1e3
+    recv.fill_(-1)
+    torch.cuda.synchronize(dev)
+    holder = ctx.C.CuHolder(comm.device.index)
+    res = cap_probe(_Holder(holder, s_hold.cuda_stream), launch, ev.query, comm.barrier, ncu,
+                    cap)
+    torch.cuda.synchronize(dev)
+    for q in range(d):
+        _check_eq(recv[q * nbytes // 4:(q + 1) * nbytes // 4], pattern(q, nbytes),
+                  f"capped all-gather slot of rank {q}")
+    comm.barrier()
+    return (f"cap {cap}: all-gather finished in {res['held_ms']:.2f} ms beside {res['held_cus']} "
+            f"held CUs (free {free_ms:.2f} ms)")
+
+
+class _Holder:
+    """``cap_probe``'s holder interface over the native ``CuHolder``."""
+
+    def __init__(self, native, stream: int):
+        self.h, self.stream = native, stream
+
+    def start(self, n: int) -> None:
+        self.h.start(n, self.stream)
+
+    def arrived(self) -> int:
+        return int(self.h.arrived())
+
+    def release(self) -> None:
+        self.h.release()
+
+    def timeout_bits(self) -> int:
+        return int(self.h.timeout_bits())
+
+
 def run_rccl_checks(comm, phases=RCCL_PHASES, progress_path: Optional[str] = None,
                     nbytes: int = PATTERN_BYTES, count: int = RS_COUNT) -> Dict[str, str]:
     """Every RCCL phase, in ``RCCL_PHASES`` order: torch's group, our communicator, the RCCL-fed
@@ -386,7 +514,9 @@ def needs(impl: str, opts: Dict, primitive: str = "tp_columnwise") -> List[str]:
     if backend in ("rccl", "nccl"):
         if not fused:
             return ["rccl"]
-        return ["rccl", "rccl_fused_cm" if int(opts.get("comm_cus", 0)) > 0 else "rccl_fused"]
+        if int(opts.get("comm_cus", 0)) > 0:  # a CU split: RCCL has CUs of its own, no cap
+            return ["rccl", "rccl_fused_cm"]
+        return ["rccl", "rccl_cap", "rccl_fused"]
     out = ["ipc"]
     # a missing "graph" key is the option default "auto" (graph replay whenever capturable, and
     # graph mode always signals with the kernels); the rowwise IPC plans send READY with the

@@ -178,16 +178,6 @@ class Simulator:
         what = f"r{r}.s{op.stream}.{OP_NAMES[k]}"
         if k == OP_GEMM and a.get("ag") is not None:
             self._exec_ag(r, op, vc, what)
-        if k == OP_GEMM and a.get("ksplit", 1) > 1 and a.get("ks_ws") is not None:
-            # K-split reduced inside the launch: C = A @ Bt^T over the full K (the slices' f32
-            # partials go through the workspace; the counters only order the launch)
-            S = a["ksplit"]
-            self._touch(r, a["ks_ws"], S * a["M"] * a["N"] * 4, True, vc, what + ".ws")
-            self._touch(r, a["ks_cnt"], 8 * (a["M"] // 256) * (a["N"] // 256), True, vc,
-                        what + ".cnt")
-            sub = dict(a, ksplit=1, K=S * a["K"], ks_ws=None, ks_cnt=None)
-            self._exec_local(r, type(op)(k, op.stream, sub), vc)
-            return
         if k == OP_GEMM and a.get("ksplit", 1) > 1:
             # K-split: slice s = A / B columns [s K, (s + 1) K) -> partial s at c + s * M * ldc
             ein, eout = DT_SIZE[a["din"]], DT_SIZE[a["dout"]]

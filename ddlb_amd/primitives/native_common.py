@@ -38,9 +38,7 @@ unmasked), ``register`` (RCCL buffers allocated with ``ncclMemAlloc`` and regist
 all-gather's copy variant, csrc/gemm/gemm.h ``AgMode`` bits: 1 plain stores + release fence instead
 of write-through stores, 2 agent-scope acquire in the gated tiles, 4 16 loads in flight per lane,
 8 more copy workgroups while the GEMM's tile rounds stay the same, 16 the launch waits for the
-peers' ACKs itself; default 30), ``ks_fused`` (K-split GEMMs of few tiles and long K reduce
-their slices inside the launch: one kernel, f32 partials, one rounding; default off, the split +
-reduce-op form measured faster, docs/RESULTS.md round 5).
+peers' ACKs itself; default 30).
 """
 
 from __future__ import annotations
@@ -69,7 +67,6 @@ COMMON_DEFAULTS = {
     "comm_cus": 0,
     "register": False,
     "trace": False,
-    "ks_fused": False,
 }
 COMMON_ALLOWED = {
     "backend": ["rccl", "ipc", *UCC_BACKENDS],
@@ -92,7 +89,6 @@ COMMON_ALLOWED = {
     "comm_cus": (0, 1024),
     "register": [True, False],
     "trace": [True, False],
-    "ks_fused": [True, False],
 }
 COMMON_ALIASES = {
     "backend": {"nccl": "rccl", "cuda": "ipc"},
@@ -125,8 +121,7 @@ def algo_config(options, order: str = "AG_before") -> AlgoConfig:
         reserve_cus=int(options.get("reserve_cus", 32)),
         copy_streams=int(options.get("copy_streams", 1)),
         direction=options.get("direction", "pull"), ag_mode=int(options.get("ag_mode", 30)),
-        comm_cus=int(options.get("comm_cus", 0)), register=bool(options.get("register", False)),
-        ks_fused=bool(options.get("ks_fused", False)))
+        comm_cus=int(options.get("comm_cus", 0)), register=bool(options.get("register", False)))
 
 
 def share_cus(cfg: AlgoConfig, communicator) -> AlgoConfig:

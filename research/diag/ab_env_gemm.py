@@ -3,7 +3,7 @@ variant runs ``scripts/bench_gemm.py`` in its own process, variants interleaved 
 native ``auto`` row's median per variant and shape reported (one box, one call). The value
 ``unset`` runs with the knob absent.
 
-    python scripts/ab_env_gemm.py --knob DDLB_PT4_CAUX --values 18,16,19,2 --shapes 0,6 --rounds 3
+    python research/diag/ab_env_gemm.py --knob DDLB_PT4_CAUX --values 18,16,19,2 --shapes 0,6 --rounds 3
 """
 
 from __future__ import annotations
@@ -15,7 +15,7 @@ import statistics
 import subprocess
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():

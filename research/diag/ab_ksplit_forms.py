@@ -5,9 +5,8 @@ interleaved rounds, median (cdna guide §5.4 rule 24):
   ks<S>[pt4]/reduce    pt4 runs every (slice, tile) pair in one launch into output-dtype
                        partials, then the reduce kernel sums them (the plans' ``_full_gemm``)
   ks<S>[pt4]/reduce-f32  the same with f32 partials, rounded once by the reduce
-  ks<S>[pt4]/inlaunch  the same launch reduces the f32 partials itself (``GemmArgs::ks_ws``)
 
-    python scripts/ab_ksplit_forms.py --dtype bfloat16 --shapes 8192x1024x8192,4096x1024x8192
+    python research/diag/ab_ksplit_forms.py --dtype bfloat16 --shapes 8192x1024x8192,4096x1024x8192
 """
 
 from __future__ import annotations
@@ -18,7 +17,7 @@ import statistics
 import sys
 import os
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def main():
@@ -83,8 +82,6 @@ def main():
                     C.reduce_sum(out.data_ptr(), q32, M * N, dout, s, G.DT_F32)
 
                 variants[f"ks{S}[pt4]/reduce-f32"] = two32
-            variants[f"ks{S}[pt4]/inlaunch"] = (lambda S=S: G.gemm(A, W, out, tile="pt4",
-                                                                   mode=mode, ksplit=S))
         if a.only:
             variants = {k: v for k, v in variants.items() if re.search(a.only, k)}
         for k, fn in variants.items():

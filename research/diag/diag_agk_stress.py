@@ -4,7 +4,7 @@ NaN before every launch, the copy workgroups pull them, publish (AgMode variants
 tiles consume them; counts the launches whose C misses the fp32 reference. The in-launch K-split
 showed that a fence-free publication can pass 10 launches and fail 1 in 10-30 (r5_18).
 
-    python scripts/diag_agk_stress.py --runs 100 --modes 0,6,14,30
+    python research/diag/diag_agk_stress.py --runs 100 --modes 0,6,14,30
 """
 
 from __future__ import annotations
@@ -14,7 +14,7 @@ import json
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def main():

@@ -17,7 +17,7 @@ workgroups and then the signal kernel that raises the GEMM's flag follow on a hi
 (the RCCL-fed fused plans' order). Reports the wall time and the timeout code, plus the device
 topology from KFD's sysfs (shader engines / arrays per engine / CUs per array).
 
-    python scripts/diag_gate_placement.py --configs 32:32,32:64,32:256,24:8,24:32,16:16
+    python research/diag/diag_gate_placement.py --configs 32:32,32:64,32:256,24:8,24:32,16:16
 """
 
 from __future__ import annotations
@@ -30,7 +30,7 @@ import subprocess
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
 

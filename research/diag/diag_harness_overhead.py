@@ -13,7 +13,7 @@ One iteration of the reference's default mode (``ddlb/benchmark.py:161-172``) is
 under the HIP device scheduling flag given by ``--schedule`` (auto | spin | yield | blocking),
 set with ``hipSetDeviceFlags`` BEFORE torch creates the context (a fresh process per flag).
 
-    python scripts/diag_harness_overhead.py [--schedule auto,spin] [-n 200]
+    python research/diag/diag_harness_overhead.py [--schedule auto,spin] [-n 200]
 """
 
 from __future__ import annotations
@@ -27,7 +27,7 @@ import subprocess
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 FLAGS = {"auto": 0, "spin": 1, "yield": 2, "blocking": 4}
 

@@ -3,7 +3,7 @@ by default) with A's row pitch set to 0 (every A row is row 0: A comes from L2 /
 stream), with A's and B's pitches 0 (no operand traffic beyond one row each), and as is. C is
 written in full in every form. Timing-only: the pitch-0 forms compute a different product.
 
-    python scripts/diag_operand_traffic.py --shapes 65536x1024x1024,65536x1024x8192
+    python research/diag/diag_operand_traffic.py --shapes 65536x1024x1024,65536x1024x8192
 """
 
 from __future__ import annotations
@@ -13,7 +13,7 @@ import statistics
 import sys
 import os
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def main():

@@ -11,7 +11,7 @@ time per bind and the mean side-stream op duration:
 * ``private``    the caller's stream is a fresh non-blocking torch stream, not the null stream;
 * ``prio0+private``.
 
-    python scripts/diag_side_stream_stall.py [--candidate coll_pipeline/rccl/s8/fused] [--binds 4]
+    python research/diag/diag_side_stream_stall.py [--candidate coll_pipeline/rccl/s8/fused] [--binds 4]
 Run it again with GPU_MAX_HW_QUEUES=8 to vary the stream -> hardware-queue mapping.
 """
 
@@ -22,7 +22,7 @@ import os
 import statistics
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "scripts"))
 

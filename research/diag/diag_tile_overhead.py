@@ -9,7 +9,7 @@ by least squares: ``k`` = time per K-tile step, ``o`` = fixed cost per tile (C e
 switch, pipeline refill), ``L`` = launch / fill / drain. bf16 and MX-fp8 (128-byte K-tiles: 64
 bf16 or 128 fp8 elements).
 
-    python scripts/diag_tile_overhead.py [--rounds 5] [--iters 20]
+    python research/diag/diag_tile_overhead.py [--rounds 5] [--iters 20]
 """
 
 from __future__ import annotations
@@ -19,7 +19,7 @@ import os
 import statistics
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
 

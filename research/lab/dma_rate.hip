@@ -3,7 +3,7 @@
 // instructions each wave keeps in flight, from an L2-resident source and from an HBM-streamed one?
 // Tells whether the GEMM's LDS-DMA path is bounded by the per-CU vector-memory path or by latency
 // x bytes in flight.
-//   hipcc -O3 --offload-arch=gfx950 -std=c++17 scripts/lab/dma_rate.hip -o scripts/lab/bin/dma_rate
+//   hipcc -O3 --offload-arch=gfx950 -std=c++17 research/lab/dma_rate.hip -o research/lab/bin/dma_rate
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>

@@ -1,7 +1,7 @@
 // Standalone GEMM lab (not part of the extension): iterate on new CDNA4 GEMM schedules with a
 // plain executable, validate against an fp32 reference kernel, time with hipEvents.
 //
-//   hipcc -O3 --offload-arch=gfx950 -std=c++17 scripts/lab/gemm_lab.hip -o build/gemm_lab
+//   hipcc -O3 --offload-arch=gfx950 -std=c++17 research/lab/gemm_lab.hip -o build/gemm_lab
 //   build/gemm_lab 65536 1024 1024
 //
 // Kernel under test: "ring" — persistent 256x256 tiles, 8 waves (2x4, 128x64 per wave),

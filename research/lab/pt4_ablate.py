@@ -1,0 +1,271 @@
+"""pt4 ablation lab: build text-patched copies of the product GEMM header and time them against
+the unpatched kernel, interleaved in ONE process (cdna guide §5.4 rule 24).
+
+The product kernel stays free of ablation switches: every variant here is the product header
+(``csrc/gemm/gemm_kernels.h``) with a few textual substitutions, compiled into its own shared
+object (``research/lab/pt4_lab.hip`` is the entry point). Build on the CPU host (hipcc
+cross-compiles gfx950), then time on the GPU box::
+
+    python research/lab/pt4_ablate.py --build-only                 # here
+    python research/lab/pt4_ablate.py --variants base,nostore      # on the GPU
+
+Variants (TIMING-ONLY unless marked exact):
+  base      the product kernel, unchanged (exact; checked against the fp32 product)
+  nostore   no C stores at all: the store instructions are replaced by a keep-alive of their
+            operands and the vmcnt windows that counted them shrink to the DMA alone
+  l2store   C stores with the default (write-back) policy into one 128 KB region per XCD group
+            (blocks b and b + 8 share it): the same store instructions, no HBM write stream
+  stamps    the product kernel (exact) with an s_memtime stamp after every workgroup barrier by
+            waves 0 and 4, kept in 8 KB of LDS beside the staging buffers (no vmcnt traffic) and
+            written to the debug buffer at the end: [block][group][512] u64, entry 0 / 1 =
+            s_memrealtime at start / end, 2 = stamp count, 3.. = stamps
+"""
+
+from __future__ import annotations
+
+import argparse
+import ctypes
+import os
+import shutil
+import statistics
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+CSRC = os.path.join(ROOT, "csrc", "gemm")
+BIN = os.path.join(HERE, "bin")
+WORK = os.path.join(ROOT, "build", "lab")
+
+_STORE_PAIR = ("""        __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, 18);  // sc1 | nt
+        __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, 18);""")
+_SO = """        const unsigned so = (unsigned)((prow * p.ldc + cn0) * OSZ) + (KS ? ccs : 0u);"""
+
+_STAMP_DEF = """  const bool g1 = wr == 1;  // wave-uniform (wave came through readfirstlane)
+  // lab: stamps after every barrier, waves 0 and 4, in LDS past the staging buffers
+  int lab_i = 3;
+  const uint64_t lab_t0 = __builtin_amdgcn_s_memrealtime();
+  auto lab_stamp = [&]() __attribute__((always_inline)) {
+    if ((wave & 3) == 0 && lab_i < 512) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      *(uint64_t*)(smem + 8 * UNIT + (wave >> 2) * 4096 + lab_i * 8) = t;
+    }
+    ++lab_i;
+  };
+#undef T4_BAR
+#define T4_BAR()                         \\
+  do {                                   \\
+    __builtin_amdgcn_sched_barrier(0);   \\
+    __builtin_amdgcn_s_barrier();        \\
+    __builtin_amdgcn_sched_barrier(0);   \\
+    lab_stamp();                         \\
+    __builtin_amdgcn_sched_barrier(0);   \\
+  } while (0)"""
+_STAMP_END = """  wait_vm<0>();  // never leave an LDS-DMA in flight past the end of the workgroup
+  if ((wave & 3) == 0) {  // lab: stamps out
+    uint64_t* d = (uint64_t*)p.timeout_word + ((int64_t)blockIdx.x * 2 + (wave >> 2)) * 512;
+    const uint64_t* src = (const uint64_t*)(smem + 8 * UNIT + (wave >> 2) * 4096);
+    for (int e = 3 + lane; e < (lab_i < 512 ? lab_i : 512); e += 64) d[e] = src[e];
+    if (lane == 0) {
+      d[0] = lab_t0;
+      d[1] = __builtin_amdgcn_s_memrealtime();
+      d[2] = (uint64_t)lab_i;
+    }
+  }"""
+
+PATCHES = {
+    "base": [],
+    "nostore": [
+        ("constexpr int NS = 4 * Store8<OUT>::kStores;", "constexpr int NS = 0;"),
+        (_STORE_PAIR, """        asm volatile("" ::"v"(x), "v"(y), "s"(so), "s"(so8));"""),
+    ],
+    "l2store": [
+        (_SO, """        const unsigned so = (unsigned)((((int64_t)(blockIdx.x % 8) * 256 + mq * 64 + f * 16) *
+                                         p.ldc) * OSZ);  // lab: one region per XCD group"""),
+        (_STORE_PAIR, """        __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, 0);  // lab: write-back
+        __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, 0);"""),
+    ],
+    "stamps": [
+        ("char smem[8 * UNIT];", "char smem[8 * UNIT + 8192];"),
+        ("  const bool g1 = wr == 1;  // wave-uniform (wave came through readfirstlane)",
+         _STAMP_DEF),
+        ("  wait_vm<0>();  // never leave an LDS-DMA in flight past the end of the workgroup",
+         _STAMP_END),
+    ],
+}
+
+
+def patched_header(variant: str) -> str:
+    """The product header with the variant's substitutions applied inside the pt4 kernel's
+    source (from its signature to the next kernel's); each pattern must occur exactly once."""
+    src = open(os.path.join(CSRC, "gemm_kernels.h")).read()
+    i = src.index("void gemm_tn_pt4_kernel(")
+    j = src.index("void gemm_tn_pt8_kernel(", i)
+    body = src[i:j]
+    for old, new in PATCHES[variant]:
+        n = body.count(old)
+        if n != 1:
+            raise RuntimeError(f"variant {variant}: pattern found {n} times: {old[:60]!r}")
+        body = body.replace(old, new)
+    return src[:i] + body + src[j:]
+
+
+def build(variant: str, verbose: bool = False) -> str:
+    """Compile one variant into research/lab/bin/pt4_<variant>.so (cached on the header text)."""
+    import hashlib
+
+    d = os.path.join(WORK, variant)
+    os.makedirs(d, exist_ok=True)
+    os.makedirs(BIN, exist_ok=True)
+    for h in ("gemm.h", "tile_map.h"):
+        shutil.copy(os.path.join(CSRC, h), os.path.join(d, h))
+    text = patched_header(variant)
+    with open(os.path.join(d, "gemm_kernels.h"), "w") as f:
+        f.write(text)
+    entry = open(os.path.join(HERE, "pt4_lab.hip")).read()
+    dig = hashlib.sha256((text + entry + open(os.path.join(d, "gemm.h")).read() +
+                          open(os.path.join(d, "tile_map.h")).read()).encode()).hexdigest()
+    out = os.path.join(BIN, f"pt4_{variant}.so")
+    stamp = out + ".sha256"
+    if os.path.exists(out) and os.path.exists(stamp) and open(stamp).read().strip() == dig:
+        return out
+    cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "--offload-arch=gfx950", f"-I{d}", os.path.join(HERE, "pt4_lab.hip"), "-o", out]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {variant}:\n{r.stderr[-4000:]}")
+    with open(stamp, "w") as f:
+        f.write(dig + "\n")
+    return out
+
+
+def main() -> int:
+    p = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    p.add_argument("--variants", default=",".join(PATCHES))
+    p.add_argument("--build-only", action="store_true")
+    p.add_argument("--shapes", default="65536x1024x1024")
+    p.add_argument("--dtype", default="bfloat16", choices=["bfloat16", "mx"])
+    p.add_argument("--rounds", type=int, default=5)
+    p.add_argument("--iters", type=int, default=40)
+    p.add_argument("--vendor", action="store_true", help="also time F.linear (hipBLASLt)")
+    p.add_argument("--stamp-report", action="store_true",
+                   help="with the stamps variant: per-K-tile cycle profile of its last launch")
+    a = p.parse_args()
+    names = [v for v in a.variants.split(",") if v]
+    if a.build_only:
+        for v in names:
+            print(v, build(v, verbose=True), flush=True)
+        return 0
+    import torch
+
+    sys.path.insert(0, ROOT)
+    from ddlb_amd.ops import gemm as G  # noqa: F401  (loads torch's HIP runtime first)
+
+    libs = {}
+    for v in names:
+        lib = ctypes.CDLL(os.path.join(BIN, f"pt4_{v}.so"))
+        lib.lab_pt4.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] * 4 + [ctypes.c_void_p] * 2
+        lib.lab_pt4.restype = ctypes.c_int
+        libs[v] = lib
+    mx = a.dtype == "mx"
+    dt = torch.float8_e4m3fn if mx else torch.bfloat16
+    dbg = torch.zeros(1 << 22, dtype=torch.int32, device="cuda")
+    for shp in a.shapes.split(","):
+        M, N, K = (int(x) for x in shp.split("x"))
+        A = (torch.rand((M, K), device="cuda") * 2 - 1).to(dt)
+        W = (torch.rand((N, K), device="cuda") * 2 - 1).to(dt)
+        out = torch.empty((M, N), dtype=torch.bfloat16, device="cuda")
+        s = torch.cuda.current_stream().cuda_stream
+
+        def launcher(v):
+            lib = libs[v]
+
+            def go():
+                rc = lib.lab_pt4(A.data_ptr(), W.data_ptr(), out.data_ptr(), M, N, K, int(mx),
+                                 dbg.data_ptr(), s)
+                if rc != 0:
+                    raise RuntimeError(f"{v}: lab_pt4 returned {rc}")
+            return go
+
+        fns = {v: launcher(v) for v in names}
+        if a.vendor and not mx:
+            fns["F.linear"] = lambda: torch.nn.functional.linear(A, W)
+        if "base" in fns:
+            out.fill_(float("nan"))
+            fns["base"]()
+            torch.cuda.synchronize()
+            ref = A.float() @ W.float().t()
+            err = float(torch.nan_to_num((out.float() - ref).abs(), nan=float("inf")).max())
+            bound = 2.0 ** -7 * float(ref.abs().max()) + K * 2.0 ** -12
+            print(f"{shp} base check: max|err| {err:.4g} (bound {bound:.4g}) "
+                  f"{'ok' if err <= bound else 'FAIL'}", flush=True)
+            del ref
+        for _ in range(200):  # clock ramp
+            fns[names[0]]()
+        times = {k: [] for k in fns}
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for _ in range(a.rounds):
+            for k, fn in fns.items():
+                for _ in range(5):
+                    fn()
+                ev0.record()
+                for _ in range(a.iters):
+                    fn()
+                ev1.record()
+                torch.cuda.synchronize()
+                times[k].append(ev0.elapsed_time(ev1) / a.iters)
+        flop = 2.0 * M * N * K
+        print(f"{shp} {a.dtype}: ms per launch, median / min over {a.rounds} rounds x "
+              f"{a.iters}", flush=True)
+        for k, ts in times.items():
+            med = statistics.median(ts)
+            print(f"  {k:10s} {med:.4f} / {min(ts):.4f}  ({flop / med / 1e9:.0f} TF)", flush=True)
+        if a.stamp_report and "stamps" in fns:
+            dbg.zero_()
+            for _ in range(20):
+                fns["stamps"]()
+            torch.cuda.synchronize()
+            stamp_report(dbg.cpu(), M, N, K, mx)
+        del A, W, out
+        torch.cuda.empty_cache()
+    return 0
+
+
+def stamp_report(dbg, M: int, N: int, K: int, mx: bool) -> None:
+    """Cycle profile of one stamps launch: per wave group, the median over workgroups of each
+    barrier-to-barrier interval, summed per K-tile (4 barriers each), plus the clock."""
+    import torch
+
+    d = dbg.view(torch.int64).view(-1, 2, 512)
+    nblk = int((d[:, 0, 2] > 0).sum())
+    d = d[:nblk]
+    wall_ns = (d[:, 0, 1] - d[:, 0, 0]).double() * 10.0  # s_memrealtime: 100 MHz
+    n = int(d[:, :, 2].min())
+    st = d[:, :, 3:n].double()
+    cyc = st[:, :, -1] - st[:, :, 0]
+    print(f"stamps: {nblk} workgroups, {n - 3} stamps per wave group, first -> last stamp "
+          f"median {float(cyc.median()):.0f} cycles, workgroup wall median "
+          f"{float(wall_ns.median()) / 1e3:.2f} us -> clock ~{float(cyc[:, 0].median()) / float(wall_ns.median()):.3f} GHz",
+          flush=True)
+    iv = st[:, :, 1:] - st[:, :, :-1]
+    med = iv.median(dim=0).values  # [2, n-4]
+    nk = K * (1 if mx else 2) // 128
+    for g in range(2):
+        row = med[g]
+        print(f"group {g}: barrier intervals (median cycles over workgroups), {row.numel()} of "
+              f"them; per K-tile sums of 4 (nk = {nk}):", flush=True)
+        off = 1 if g == 0 else 2  # prologue barriers before the first K-tile's (g1 one more)
+        body = row[off:]
+        kt = [float(body[i:i + 4].sum()) for i in range(0, body.numel() - 3, 4)]
+        for t0 in range(0, len(kt), nk):
+            seg = kt[t0:t0 + nk]
+            print(f"  tile {t0 // nk}: " + " ".join(f"{x:.0f}" for x in seg), flush=True)
+        print("  first 12 intervals: " + " ".join(f"{float(x):.0f}" for x in row[:12]), flush=True)
+        last = row[-12:]
+        print("  last 12 intervals:  " + " ".join(f"{float(x):.0f}" for x in last), flush=True)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -3,8 +3,8 @@
 // (16 rows x 64 B, the pt4 bf16 epilogue's pattern)? A 65536 x 1024 bf16 matrix (128 MB, the flagship's C) written by
 // 256 x 512-thread workgroups, each wave a 16 x 64 block at a time.
 //
-//   hipcc --offload-arch=gfx950 -O3 -o scripts/lab/bin/store_pattern scripts/lab/store_pattern.hip
-//   scripts/lab/bin/store_pattern
+//   hipcc --offload-arch=gfx950 -O3 -o research/lab/bin/store_pattern research/lab/store_pattern.hip
+//   research/lab/bin/store_pattern
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>

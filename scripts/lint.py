@@ -5,7 +5,7 @@ Checks, per file:
   * Python: compiles; no trailing whitespace; no tabs; lines <= 110 columns; final newline;
     no unused top-level imports (``ast`` name scan, ``__init__`` re-exports and ``noqa`` excepted);
     no bare ``except:``.
-  * C++ / HIP (``csrc/``, ``scripts/lab``): no trailing whitespace; no tabs; final newline;
+  * C++ / HIP (``csrc/``, ``research/lab``): no trailing whitespace; no tabs; final newline;
     lines <= 150 columns (long MFMA intrinsics).
 
     python scripts/lint.py            # lint the tree, exit 1 on findings
@@ -19,8 +19,8 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PY_DIRS = ["ddlb_amd", "tests", "scripts", "."]
-CXX_DIRS = ["csrc", "scripts/lab"]
+PY_DIRS = ["ddlb_amd", "tests", "scripts", "research/diag", "."]
+CXX_DIRS = ["csrc", "research/lab"]
 CXX_EXT = (".hip", ".cpp", ".h", ".hpp")
 SKIP_DIRS = {".git", "build", "gpurun_out", "__pycache__", "results", "profiles"}
 PY_MAX = 110

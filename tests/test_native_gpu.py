@@ -919,72 +919,11 @@ def test_ksplit_gemm_partials(comm, S, tile, dt, mode):
     ctx.close()
 
 
-@pytest.mark.parametrize("S", [2, 4])
-@pytest.mark.parametrize("shape", [(1024, 512, 4096), (8192, 1024, 8192), (512, 256, 2048)])
-@pytest.mark.parametrize("dt,mode,dout", [("bf16", 0, "bf16"), ("bf16", 0, "f32"),
-                                          ("fp8", 2, "bf16"), ("fp8", 0, "bf16")])
-def test_ksplit_reduced_in_launch(comm, S, shape, dt, mode, dout):
-    """GemmArgs::ks_ws: ONE pt4 launch runs the S K-slices of every tile and reduces them itself
-    (the last slice of a tile to arrive sums the others' f32 partials with its own, in slice
-    order, and writes C once). Against the fp32 full-K product with the tight bound (one
-    rounding, as an unsplit GEMM); repeat launches on the SAME never-reset counters (epochs
-    2..11, the workspace NaN-filled before each) bit-identical."""
-    from ddlb_amd.parallel.context import NativeContext
-    from ddlb_amd.parallel.plan import DT_BF16, DT_F32, DT_FP8, Plan
-
-    din = DT_FP8 if dt == "fp8" else DT_BF16
-    tdt = torch.float8_e4m3fn if dt == "fp8" else torch.bfloat16
-    odt, dcode = (torch.float32, DT_F32) if dout == "f32" else (torch.bfloat16, DT_BF16)
-    es = 1 if dt == "fp8" else 2
-    M, N, K = shape
-    if (K * es // 128) % (2 * S):
-        pytest.skip("each slice needs an even number of 128-byte K-tiles")
-    ks = K // S
-    tiles = (M // 256) * (N // 256)
-    plan = Plan(0, 1, nstreams=1, stream_priority=[0])
-    a = plan.buffer("a", M * K * es)
-    b = plan.buffer("b", N * K * es)
-    c = plan.buffer("c", M * N * odt.itemsize)
-    ws = plan.buffer("ws", S * M * N * 4)
-    cnt = plan.buffer("cnt", max(256, 8 * tiles))  # cached memory, zeroed at bind (_full_gemm)
-    plan.gemm(0, a, b, c, M=M, N=N, K=ks, lda=K, ldb=K, ldc=N, din=din, dout=dcode, tile=19,
-              mode=mode, ksplit=S, ks_ws=ws, ks_cnt=cnt)
-    ctx = NativeContext(comm)
-    bound = ctx.bind(plan)
-    A = (torch.rand(M, K, device="cuda") * 2 - 1).to(tdt)
-    W = (torch.rand(N, K, device="cuda") * 2 - 1).to(tdt)
-    bound.buffer("a").view(tdt).view(M, K).copy_(A)
-    bound.buffer("b").view(tdt).view(N, K).copy_(W)
-    out = bound.buffer("c").view(odt).view(M, N)
-    out.fill_(float("nan"))
-    bound.buffer("ws").view(torch.float32).fill_(float("nan"))
-    bound.run()
-    torch.cuda.synchronize()
-    bound.check_health()
-    first = out.clone()
-    ref = A.float() @ W.float().T
-    err = float((first.float() - ref).abs().max())
-    assert err <= _tight(ref, K), err
-    for _ in range(10):  # a partial read before its producer's stores landed would be NaN
-        bound.buffer("ws").view(torch.float32).fill_(float("nan"))
-        torch.cuda.synchronize()
-        bound.run()
-        torch.cuda.synchronize()
-        assert torch.equal(out, first)
-    bound.check_health()
-    counts = bound.buffer("cnt").view(torch.int32)[:2 * tiles].view(tiles, 2).cpu()
-    assert torch.equal(counts[:, 0], torch.full((tiles,), 11 * S, dtype=torch.int32))
-    assert torch.equal(counts[:, 1], torch.full((tiles,), 11 * (S - 1), dtype=torch.int32))
-    bound.close()
-    ctx.close()
-
-
 @pytest.mark.parametrize("dtype,mode", [("bfloat16", "auto"), ("float8_e4m3fn", "mx"),
                                         ("float32", "auto")])
 def test_ksplit_reduced_ops_gemm(comm, dtype, mode):
-    """The public op's auto split (config #2's GEMM) rounds once: f32 partials summed by the
-    reduce kernel ("reduce", the default) or inside the launch ("inlaunch"); the two forms sum
-    the same f32 partials in the same slice order, so they agree bit for bit."""
+    """The public op's auto split (config #2's GEMM) rounds once: f32 partials summed in slice
+    order by the reduce kernel; repeat bit-identical."""
     from ddlb_amd.ops.gemm import gemm, split_k_factor
 
     tdt = getattr(torch, dtype)
@@ -999,9 +938,6 @@ def test_ksplit_reduced_ops_gemm(comm, dtype, mode):
     ref = A.float() @ W.float().T
     assert float((out.float() - ref).abs().max()) <= _tight(ref, K)
     assert torch.equal(gemm(A, W, mode=mode, ksplit=S), out)
-    assert torch.equal(gemm(A, W, mode=mode, ksplit=S, ks_form="inlaunch"), out)
-    with pytest.raises(ValueError):
-        gemm(A, W, mode=mode, ksplit=S, ks_form="bogus")
     if tdt != torch.bfloat16:
         return
     t4 = gemm(A, W, tile="t4", ksplit=2)  # the slice-by-slice partial form stays available
@@ -1009,23 +945,20 @@ def test_ksplit_reduced_ops_gemm(comm, dtype, mode):
     assert float((t4.float() - ref).abs().max()) <= _tight(ref, K)
 
 
-@pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("dtype,mode", [("bfloat16", "auto"), ("float8_e4m3fn", "auto"),
                                         ("float8_e4m3fn", "mx")])
-def test_split_k_world1_native(comm, dtype, mode, fused):
+def test_split_k_world1_native(comm, dtype, mode):
     """BASELINE config #2's full GEMM (8192 x 1024 x 8192: 128 tiles of 256²) runs K-split: ONE
-    pt4 launch over (slice, tile) pairs writing two partials summed by the reduce op, or
-    (``ks_fused``) reducing them itself; validated by the primitive (fp32 reference) and
-    repeat-identical."""
+    pt4 launch over (slice, tile) pairs writing two partials summed by the reduce op; validated
+    by the primitive (fp32 reference) and repeat-identical."""
     from ddlb_amd.parallel.plan import OP_GEMM, OP_REDUCE
     from ddlb_amd.primitives.tp_columnwise.native import NativeTPColumnwise
 
-    impl = NativeTPColumnwise(m=8192, n=1024, k=8192, dtype=dtype, gemm_mode=mode,
-                              ks_fused=fused)
+    impl = NativeTPColumnwise(m=8192, n=1024, k=8192, dtype=dtype, gemm_mode=mode)
     ops = impl.bound.plan.ops
     g = [op for op in ops if op.kind == OP_GEMM]
-    assert len(g) == 1 and g[0].args["ksplit"] == 2 and (g[0].args["ks_ws"] is not None) == fused
-    assert sum(op.kind == OP_REDUCE for op in ops) == (0 if fused else 1)
+    assert len(g) == 1 and g[0].args["ksplit"] == 2
+    assert sum(op.kind == OP_REDUCE for op in ops) == 1
     out = impl.run()
     torch.cuda.synchronize()
     impl.validate(out)
@@ -1133,20 +1066,78 @@ def test_side_stream_cycle_is_not_captured():
         assert r.returncode == 0 and "bytes ok" in r.stdout, (variant, r.returncode, r.stderr[-800:])
 
 
-@pytest.mark.parametrize("knob", ["", "DDLB_PT4_ONE", "DDLB_PT4_HALF_LINES", "DDLB_PT4_C_NT"])
-def test_pt4_schedule_knobs(knob):
-    """The ungated write-through pt4 under each of its A/B knobs (read once per process, hence a
-    child process each): the default DEFER schedule with whole-line C stores, the ONE schedule
-    (3-deep A ring), the half-line stores, nt-only stores -- bf16 / f16 / fp8 / MX-fp8 against
-    the fp32 product with the tight bound, repeat bit-identical."""
-    env = dict(os.environ, DDLB_TEST_KNOB=knob)
-    for k in ("DDLB_PT4_ONE", "DDLB_PT4_HALF_LINES", "DDLB_PT4_C_NT"):
-        env.pop(k, None)
-    if knob:
-        env[knob] = "1"
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "_pt4_knob_worker.py")],
-                       capture_output=True, text=True, timeout=100, env=env)
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert r.returncode == 0 and lines, (knob, r.stdout[-2000:], r.stderr[-3000:])
-    res = json.loads(lines[-1])
+@pytest.mark.parametrize("M,N,K,dt,odt,mode", [
+    (65536, 1024, 1024, "bfloat16", "bfloat16", "auto"),      # the flagship: 4 tiles per workgroup
+    (65536, 1024, 1024, "float8_e4m3fn", "bfloat16", "mx"),   # the MX flagship
+    (32768, 2048, 2048, "float16", "float16", "auto"),         # 4 tiles per workgroup, nk = 32
+    (8192, 1024, 1024, "bfloat16", "bfloat16", "auto"),        # fewer tiles than CUs
+    (4096, 512, 4096, "float8_e4m3fn", "bfloat16", "auto"),    # non-scaled fp8, long K
+])
+def test_pt4_multi_tile(comm, M, N, K, dt, odt, mode):
+    """The ungated write-through pt4 across tile boundaries: with more tiles than CUs every
+    workgroup runs several tiles back to back (the next tile's staging issued during the last
+    K-tiles of the current one, its C stores in flight across the switch). Against
+    the fp32 product with the tight bound, NaN-filled output, repeat bit-identical."""
+    from ddlb_amd.ops.gemm import gemm
+
+    tdt, todt = getattr(torch, dt), getattr(torch, odt)
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(7)
+    a = (torch.rand((M, K), generator=gen, device="cuda") * 2 - 1).to(tdt)
+    w = (torch.rand((N, K), generator=gen, device="cuda") * 2 - 1).to(tdt)
+    out = torch.full((M, N), float("nan"), dtype=todt, device="cuda")
+    gemm(a, w, out, tile="pt4", mode=mode, ksplit=1)
+    torch.cuda.synchronize()
+    ref = a.float() @ w.float().t()
+    err = float(torch.nan_to_num((out.float() - ref).abs(), nan=float("inf")).max())
+    assert err <= _tight(ref, K), err
+    again = torch.full_like(out, float("nan"))
+    gemm(a, w, again, tile="pt4", mode=mode, ksplit=1)
+    torch.cuda.synchronize()
+    assert torch.equal(again, out)
     assert res["cases"] == 5 and res["worst"] <= 1.0, res
+
+
+def test_cu_holder_occupies_whole_cus(comm):
+    """The rccl_cap holder takes a whole CU per workgroup (full register file + LDS, like the
+    gated pt4 GEMM): with every CU held, a second holder workgroup cannot become resident until
+    the host releases the first; both spins end by release (no timeout bits)."""
+    import time
+
+    from ddlb_amd.ops import load
+
+    C = load()
+    dev = comm.device
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    h1, h2 = C.CuHolder(dev.index), C.CuHolder(dev.index)
+
+    def wait_for(h, n, limit=3.0):
+        t0 = time.time()
+        while h.arrived() < n and time.time() - t0 < limit:
+            time.sleep(0.001)
+        return h.arrived()
+
+    h1.start(ncu, s1.cuda_stream)
+    try:
+        assert wait_for(h1, ncu) == ncu
+        h2.start(1, s2.cuda_stream)
+        time.sleep(0.2)
+        assert h2.arrived() == 0  # no CU left for it
+    finally:
+        h1.release()
+    try:
+        assert wait_for(h2, 1) == 1
+    finally:
+        h2.release()
+    torch.cuda.synchronize(dev)
+    assert h1.timeout_bits() == 0 and h2.timeout_bits() == 0
+
+
+def test_rccl_cap_phase_world1(comm):
+    """The rccl_cap preflight phase on the device (world 1): num_cus - 32 CUs held, the
+    all-gather on the 32-CTA-capped communicator must finish beside them, bytes checked."""
+    from ddlb_amd.parallel import preflight as pf
+
+    status = pf._rccl_cap_check(comm)
+    assert status.startswith("cap 32: all-gather finished"), status

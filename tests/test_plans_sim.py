@@ -400,25 +400,18 @@ def test_rccl_fused_signal_stream(alg, side):
     assert any(op.kind in (OP_RECORD, OP_WAIT) for op in plan.ops) == side
 
 
-@pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("d,be", [(1, "rccl"), (2, "rccl"), (2, "ipc"), (4, "rccl"), (4, "ipc")])
-def test_split_k_full_gemm(d, be, fused):
+def test_split_k_full_gemm(d, be):
     """A full GEMM whose 256x256 grid covers few CUs and whose K is long runs K-split: ONE
-    persistent launch over (slice, tile) pairs writing S partials, summed by one reduce op, or
-    (``ks_fused``) reducing them itself (f32 workspace + tile counters, no reduce op); exact
+    persistent launch over (slice, tile) pairs writing S partials, summed by one reduce op; exact
     result, race-free."""
     m, n, k = 256 * d, 256, 2048
-    cfg = AlgoConfig(algorithm="default", backend=be, ks_fused=fused)
+    cfg = AlgoConfig(algorithm="default", backend=be)
     plan, _ = build_tp_columnwise(0, d, m, n, k, DT_F32, DT_F32, cfg)
     g = [op for op in plan.ops if op.kind == OP_GEMM]
     assert len(g) == 1 and g[0].stream == 0 and g[0].args["ksplit"] == 4
     assert g[0].args["K"] == k // 4 and g[0].args["lda"] == k and g[0].args["tile"] == 19
-    if fused:
-        assert g[0].args["ks_ws"] is not None and g[0].args["ks_cnt"] is not None
-        # counters zeroed once at bind, never reset, in cached memory: not a (uncached) flag
-        assert not plan.buffers[g[0].args["ks_cnt"].buf].zero
-        assert plan.buffers[g[0].args["ks_ws"].buf].nbytes == 4 * m * n * 4
-    assert sum(op.kind == OP_REDUCE for op in plan.ops) == (0 if fused else 1)
+    assert sum(op.kind == OP_REDUCE for op in plan.ops) == 1
     _run_col(d, m, n, k, cfg, epochs=2)
 
 
@@ -550,14 +543,3 @@ def test_gemm_first_only_on_separate_queues(monkeypatch):
     off = AlgoConfig(algorithm="p2p_pipeline", backend="rccl", fused=True, gemm_first=False)
     plan, _ = build_tp_columnwise(0, 2, 2048, 256, 256, DT_F32, DT_F32, off)
     assert not plan.meta["gemm_first"] and plan.ops[-1].kind == OP_GEMM
-
-
-def test_ops_gemm_ks_form_checked_first():
-    """ops.gemm rejects an unknown K-split form before touching the device (CPU tensors here)."""
-    import torch
-
-    from ddlb_amd.ops.gemm import gemm
-
-    a = torch.zeros(256, 256, dtype=torch.bfloat16)
-    with pytest.raises(ValueError, match="ks_form"):
-        gemm(a, a, ks_form="fused")

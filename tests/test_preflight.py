@@ -59,7 +59,8 @@ def test_rccl_plan(d):
 def test_needs_maps_candidates_to_checks():
     assert pf.needs("pytorch", {}) == ["torch_nccl"]
     assert pf.needs("native", {"backend": "rccl"}) == ["rccl"]
-    assert pf.needs("native", {"backend": "rccl", "fused": True}) == ["rccl", "rccl_fused"]
+    assert pf.needs("native", {"backend": "rccl", "fused": True}) == ["rccl", "rccl_cap",
+                                                                     "rccl_fused"]
     assert pf.needs("native", {"backend": "rccl", "fused": True, "comm_cus": 32}) == \
         ["rccl", "rccl_fused_cm"]
     assert pf.needs("native", {"backend": "ipc", "multicast_protocol": "memcpy",
@@ -150,6 +151,7 @@ def test_run_checks_report_every_phase(monkeypatch):
     assert list(res) == list(pf.RCCL_PHASES)
     assert res["torch_nccl"].startswith("ok")
     assert res["rccl"].startswith("failed: RuntimeError: no native layer")
+    assert res["rccl_cap"].startswith("failed: RuntimeError: no native layer")
     assert res["rccl_fused"].startswith("failed: TimeoutError: stand-in")
     assert res["rccl_fused_cm"].startswith("ok")
     assert "rccl_fused_cm" in ran
@@ -161,3 +163,88 @@ def test_run_checks_report_every_phase(monkeypatch):
         assert res[ph] != "failed: timeout"
     merged = pf.merge([res, res], pf.IPC_PHASES)
     assert not any(v == "failed: timeout" for v in merged.values())
+
+
+class _FakeHolder:
+    """cap_probe's holder: ``resident`` workgroups become resident (of those started)."""
+
+    def __init__(self, resident=None, timeout_bits=0):
+        self.resident, self.bits = resident, timeout_bits
+        self.n, self.released, self.events = 0, False, []
+
+    def start(self, n):
+        self.n = n
+        self.events.append(("start", n))
+
+    def arrived(self):
+        return self.n if self.resident is None else min(self.resident, self.n)
+
+    def release(self):
+        self.released = True
+        self.events.append(("release",))
+
+    def timeout_bits(self):
+        return self.bits
+
+
+class _Clock:
+    def __init__(self):
+        self.t = 0.0
+
+    def __call__(self):
+        return self.t
+
+    def sleep(self, dt):
+        self.t += dt
+
+
+@pytest.mark.parametrize("finish_after", [0.0, 0.05])
+def test_cap_probe_observes_capped_collective(finish_after):
+    """rccl_cap: num_cus - cap CUs held, barrier, then the capped all-gather
+    must finish while they are held; the holders are released afterwards, in every case."""
+    clk, h, order = _Clock(), _FakeHolder(), []
+    t_launch = []
+
+    def launch():
+        order.append("launch")
+        t_launch.append(clk.t)
+
+    res = pf.cap_probe(h, launch, lambda: clk.t - t_launch[0] >= finish_after,
+                       lambda: order.append("barrier"), ncu=256, cap=32, sleep=clk.sleep,
+                       clock=clk)
+    assert h.events[0] == ("start", 224) and h.released
+    assert order == ["barrier", "launch"]
+    assert res["held_cus"] == 224 and res["cap"] == 32
+    assert res["held_ms"] >= finish_after * 1e3 - 1e-6
+
+
+def test_cap_probe_refuses_collective_that_cannot_finish():
+    """The refusal path: a collective that never completes beside the held CUs (RCCL launched
+    more workgroups than the cap, or needs CUs the holders took) fails the phase after the bound
+    -- not a hang: the holders are released, so the collective drains afterwards."""
+    clk, h = _Clock(), _FakeHolder()
+    with pytest.raises(RuntimeError, match="did not finish .* beside 224 held CUs"):
+        pf.cap_probe(h, lambda: None, lambda: False, lambda: None, ncu=256, cap=32,
+                     finish_s=5.0, sleep=clk.sleep, clock=clk)
+    assert h.released and 5.0 <= clk.t < 5.1
+
+
+def test_cap_probe_holders_not_resident_and_spin_bound():
+    clk = _Clock()
+    h = _FakeHolder(resident=200)
+    with pytest.raises(RuntimeError, match="only 200 of 224 holder workgroups"):
+        pf.cap_probe(h, lambda: None, lambda: True, lambda: None, ncu=256, cap=32,
+                     sleep=clk.sleep, clock=clk)
+    assert h.released
+    h = _FakeHolder(timeout_bits=4)
+    with pytest.raises(RuntimeError, match="bounded spin gave up"):
+        pf.cap_probe(h, lambda: None, lambda: True, lambda: None, ncu=256, cap=32,
+                     sleep=clk.sleep, clock=clk)
+    with pytest.raises(ValueError):
+        pf.cap_probe(_FakeHolder(), lambda: None, lambda: True, lambda: None, ncu=32, cap=32)
+
+
+def test_fused_rccl_cap_is_the_gate_reserve():
+    """The cap the probe checks is the one the fused candidates bind (one CU per shader array)."""
+    for d in (2, 4, 8):
+        assert pf.fused_rccl_cap(d) == 32
