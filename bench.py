@@ -349,6 +349,43 @@ def child_main(a) -> int:
     return 0
 
 
+def diagnose_child(a) -> int:
+    """First-contact diagnostics of the N>1 data plane on this rank (ddlb_amd.parallel.diagnose):
+    xGMI pull bandwidth per peer, RCCL bus bandwidth on the default and the capped communicator,
+    and a per-op timeline of the winner (built eagerly). Written to --child-out; never raises."""
+    res = {}
+    try:
+        from ddlb_amd.communicator import Communicator
+        from ddlb_amd.parallel import diagnose
+        from ddlb_amd.primitives.registry import resolve
+
+        comm = Communicator()
+        comm.ensure_process_group(timeout_s=min(a.child_timeout, 60.0))
+        spec = json.loads(a.child_opts)
+        esz = 1 if a.dtype == "float8_e4m3fn" else (4 if a.dtype == "float32" else 2)
+
+        def factory():
+            if spec.get("impl") != "native":
+                raise RuntimeError(f"winner is the {spec.get('impl')} slot (no native plan)")
+            opts = dict(spec.get("opts", {}))
+            opts.pop("_env", None)
+            opts["graph"] = False  # per-op events need the eager enqueue
+            cls, o, _ = resolve(a.primitive, "native", opts)
+            return cls(m=a.m, n=a.n, k=a.k, dtype=a.dtype, **o)
+
+        from ddlb_amd.parallel.preflight import fused_rccl_cap
+
+        res = diagnose.diagnose(comm, a.primitive, a.m, a.n, a.k, esz, factory,
+                                budget_s=a.diag_budget_s,
+                                caps=(0, fused_rccl_cap(max(comm.world_size, 2))))
+        comm.destroy()
+    except Exception as e:  # reported to the parent
+        res["error"] = f"{type(e).__name__}: {str(e)[:300]}"
+    with open(a.child_out, "w") as f:
+        json.dump(res, f)
+    return 0
+
+
 def preflight_child(a) -> int:
     """One preflight family on this rank's GPU (progress file rewritten after every phase)."""
     from ddlb_amd.communicator import Communicator
@@ -497,6 +534,25 @@ class Job:
             return res
         errs = [r.get("error") for r in results if not r.get("ok")]
         return {"ok": False, "error": errs[0] if errs else "unknown"}
+
+    def diagnose(self, chosen, timeout: float) -> dict:
+        """First-contact diagnostics (``diagnose_child``) in a child per rank: every rank's xGMI
+        probe, rank 0's RCCL bus bandwidth and winner timeline (``diagnose.merge_ranks``)."""
+        from ddlb_amd.parallel.diagnose import merge_ranks
+
+        spec = {"impl": chosen[1], "opts": chosen[2]}
+        out, status, rc, _ = self._spawn("diagnose", spec, timeout,
+                                         ["--diag-budget-s", str(self.a.diag_budget_s)])
+        local = None
+        if status == "timeout":
+            local = {"error": f"timeout after {timeout:.0f} s"}
+        elif os.path.exists(out):
+            local = json.load(open(out))
+        else:
+            local = {"error": f"child exit {rc}"}
+        if os.path.exists(out):
+            os.remove(out)
+        return merge_ranks(self.gather(local))
 
     def preflight(self, timeout: float) -> dict:
         """Run the preflight families (RCCL, then IPC), each in its own child per rank."""
@@ -721,6 +777,12 @@ def main(argv=None) -> int:
                    help="untimed GPU pre-warm before the warmup steps (clock ramp)")
     p.add_argument("--preflight-only", action="store_true",
                    help="run the N>1 data-plane preflight, print its JSON line and exit")
+    p.add_argument("--diagnose", choices=["auto", "on", "off"], default="auto",
+                   help="first-contact diagnostics after the final run (xGMI probe, RCCL busbw "
+                        "default vs capped, winner timeline) -> 'diag' in the JSON line; auto = "
+                        "at world > 1")
+    p.add_argument("--diag-budget-s", type=float, default=30.0,
+                   help="wall-clock budget of the diagnostics' measurements")
     p.add_argument("--harness-iters", type=int, default=-1,
                    help="iterations of the reference-default timing (barrier before each, "
                         "MAX over ranks) after the timed window -> harness_mean_ms "
@@ -738,6 +800,8 @@ def main(argv=None) -> int:
     if a.child:
         if a.child_impl.startswith("preflight_"):
             return preflight_child(a)
+        if a.child_impl == "diagnose":
+            return diagnose_child(a)
         return child_main(a)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -792,6 +856,17 @@ def main(argv=None) -> int:
     if final is None:
         sys.stderr.write(f"final measurement failed (autotune: {json.dumps(tune)})\n")
         return 1
+    diag = None
+    if a.diagnose == "on" or (a.diagnose == "auto" and world > 1):
+        # bounded: the measurements' own budget plus child start-up, and never past the deadline
+        room = job.left() - 5.0
+        if job.bcast(room < a.diag_budget_s + 15.0 if job.rank == 0 else None):
+            diag = {"skipped": f"deadline ({room:.0f} s left)"}
+        else:
+            t0 = time.time()
+            diag = job.diagnose(chosen, min(a.diag_budget_s + 45.0, room))
+            diag["job_s"] = round(time.time() - t0, 1)
+            job.log(f"diagnostics: {json.dumps(diag)[:600]} ({diag['job_s']} s)")
     ms = final["ms"]
     flop = 2.0 * a.m * a.n * a.k
     harness_tflops = flop / (ms * 1e-3) / 1e12  # the reference's formula (ddlb/benchmark.py:211)
@@ -833,6 +908,8 @@ def main(argv=None) -> int:
             "deadline_s": a.deadline_s, "job_wall_s": round(time.time() - job.t_start, 1),
             "autotune_ms": tune,
         }
+        if diag is not None:
+            line["diag"] = diag
         print(json.dumps(line), file=out, flush=True)
     if job.pg is not None:
         job.pg.destroy_process_group()

@@ -87,13 +87,13 @@ class CuHolder {
       hipHostFree(host_);
     }
   }
-  void start(int nwg, uintptr_t stream, unsigned spin_limit) {
+  void start(int nwg, uintptr_t stream, double max_s) {
     reset();
     HoldArgs a;
     a.arrived = dev_;
     a.go = dev_ + 32;
     a.timeout_word = dev_ + 64;
-    a.spin_limit = spin_limit;
+    a.max_ticks = (uint64_t)(max_s * 1e8);  // s_memrealtime: 100 MHz
     check(hipSetDevice(device_), "hipSetDevice");
     check(hold_cus_launch(a, nwg, (hipStream_t)stream), "hold_cus_launch");
   }
@@ -179,6 +179,12 @@ PYBIND11_MODULE(_C, m) {
           a.bytes[0] = bytes;
           check(copy_launch(a, max_blocks, (hipStream_t)s), "copy");
         });
+  m.def("memcpy_async",  // one copy-engine copy (diagnostics: the xGMI probe's SDMA pulls)
+        [](uintptr_t dst, uintptr_t src, int64_t bytes, uintptr_t s) {
+          check(hipMemcpyAsync((void*)dst, (const void*)src, (size_t)bytes,
+                               hipMemcpyDeviceToDevice, (hipStream_t)s),
+                "hipMemcpyAsync");
+        });
   m.def("copy_multi",  // segments (dst, src, bytes) copied concurrently by one CU kernel
         [](std::vector<std::tuple<uintptr_t, uintptr_t, int64_t>> segs, int max_blocks,
            uintptr_t s) {
@@ -238,7 +244,7 @@ PYBIND11_MODULE(_C, m) {
   py::class_<CuHolder>(m, "CuHolder")
       .def(py::init<int>(), py::arg("device"))
       .def("start", &CuHolder::start, py::arg("nwg"), py::arg("stream"),
-           py::arg("spin_limit") = 1u << 24)
+           py::arg("max_s") = 10.0)
       .def("arrived", &CuHolder::arrived)
       .def("timeout_bits", &CuHolder::timeout_bits)
       .def("release", &CuHolder::release);

@@ -59,12 +59,13 @@ struct BumpSignalArgs {
 hipError_t bump_signal_launch(const BumpSignalArgs& a, hipStream_t s);
 // CU holder (preflight ``rccl_cap``): ``nwg`` workgroups that each occupy a whole CU as the
 // flag-gated persistent GEMM does (full register file + LDS), count themselves in *arrived and
-// spin until *go != 0 (bounded by spin_limit polls; timeout bit 4 in *timeout_word).
+// spin until *go != 0 (bounded: max_ticks of the 100 MHz s_memrealtime clock; then timeout bit
+// 4 in *timeout_word).
 struct HoldArgs {
   unsigned* arrived = nullptr;
   const unsigned* go = nullptr;
   unsigned* timeout_word = nullptr;
-  unsigned spin_limit = 1u << 24;
+  uint64_t max_ticks = 1000000000ull;  // 10 s
 };
 hipError_t hold_cus_launch(const HoldArgs& a, int nwg, hipStream_t s);
 

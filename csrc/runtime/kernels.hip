@@ -277,10 +277,12 @@ __global__ __launch_bounds__(512, 1) void hold_cus_kernel(HoldArgs a) {
   pad[threadIdx.x * 320] = 1;   // touched across all 160 KB, so all of it is allocated
   if (threadIdx.x == 0) {
     __hip_atomic_fetch_add(a.arrived, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    unsigned spins = 0;
+    // bounded in wall time (s_memrealtime: 100 MHz), not in polls: a poll of host memory costs
+    // a PCIe round trip, so a poll count says little about how long a holder can stay
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(a.go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
-      __builtin_amdgcn_s_sleep(8);
-      if (++spins > a.spin_limit) {  // bounded: never outlives a lost host
+      __builtin_amdgcn_s_sleep(32);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > a.max_ticks) {  // never outlives a lost host
         atomicOr(a.timeout_word, 4u);
         break;
       }

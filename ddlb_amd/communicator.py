@@ -136,6 +136,26 @@ class Communicator:
             else:
                 dist.barrier()
 
+    def host_barrier(self, tag: str = "hb") -> None:
+        """A cross-rank barrier that touches no GPU queue (the process group's TCP store): for
+        points where a device sync or a collective kernel would wait on work that is waiting on
+        this barrier (the rccl_cap preflight's CU holders)."""
+        import torch.distributed as dist
+
+        if self.world_size <= 1 or not (dist.is_available() and dist.is_initialized()):
+            return
+        store = dist.distributed_c10d._get_default_store()
+        self._hb_round = getattr(self, "_hb_round", 0) + 1
+        key = f"ddlb_{tag}_{self._hb_round}"
+        store.add(key, 1)
+        import time
+
+        t0 = time.time()
+        while store.add(key, 0) < self.world_size:
+            if time.time() - t0 > 120.0:
+                raise TimeoutError(f"host barrier {key}: peers missing after 120 s")
+            time.sleep(0.0005)
+
     def all_reduce_max(self, tensor):
         import torch.distributed as dist
 

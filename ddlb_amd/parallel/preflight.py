@@ -459,8 +459,9 @@ def _rccl_cap_check(comm, nbytes: int = PATTERN_BYTES) -> str:
     recv.fill_(-1)
     torch.cuda.synchronize(dev)
     holder = ctx.C.CuHolder(comm.device.index)
-    res = cap_probe(_Holder(holder, s_hold.cuda_stream), launch, ev.query, comm.barrier, ncu,
-                    cap)
+    # (the barrier inside the hold must not sync the device: the holders spin until released)
+    res = cap_probe(_Holder(holder, s_hold.cuda_stream), launch, ev.query,
+                    lambda: comm.host_barrier("cap"), ncu, cap)
     torch.cuda.synchronize(dev)
     for q in range(d):
         _check_eq(recv[q * nbytes // 4:(q + 1) * nbytes // 4], pattern(q, nbytes),

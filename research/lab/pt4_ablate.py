@@ -11,10 +11,16 @@ cross-compiles gfx950), then time on the GPU box::
 
 Variants (TIMING-ONLY unless marked exact):
   base      the product kernel, unchanged (exact; checked against the fp32 product)
+  ref       the product kernel as committed at git revision $DDLB_LAB_REF (default HEAD): the
+            A/B partner of an edited kernel (exact; checked)
   nostore   no C stores at all: the store instructions are replaced by a keep-alive of their
             operands and the vmcnt windows that counted them shrink to the DMA alone
   l2store   C stores with the default (write-back) policy into one 128 KB region per XCD group
             (blocks b and b + 8 share it): the same store instructions, no HBM write stream
+  auxN      the product kernel with C store cache-policy bits N (exact)
+  behind    store-behind (exact; research/lab/pt4_store_behind.diff, round 6, measured slower:
+            profiles/r06/README.md): a tile's C packed into held registers and stored over three
+            intervals of the next tile instead of one
   stamps    the product kernel (exact) with an s_memtime stamp after every workgroup barrier by
             waves 0 and 4, kept in 8 KB of LDS beside the staging buffers (no vmcnt traffic) and
             written to the debug buffer at the end: [block][group][512] u64, entry 0 / 1 =
@@ -26,7 +32,6 @@ from __future__ import annotations
 import argparse
 import ctypes
 import os
-import shutil
 import statistics
 import subprocess
 import sys
@@ -75,6 +80,8 @@ _STAMP_END = """  wait_vm<0>();  // never leave an LDS-DMA in flight past the en
 
 PATCHES = {
     "base": [],
+    "ref": [],
+    "behind": [],
     "nostore": [
         ("constexpr int NS = 4 * Store8<OUT>::kStores;", "constexpr int NS = 0;"),
         (_STORE_PAIR, """        asm volatile("" ::"v"(x), "v"(y), "s"(so), "s"(so8));"""),
@@ -85,6 +92,10 @@ PATCHES = {
         (_STORE_PAIR, """        __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, 0);  // lab: write-back
         __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, 0);"""),
     ],
+    # C store cache policy (aux bits of buffer_store: 1 sc0, 2 nt, 16 sc1; the product uses 18)
+    **{f"aux{a}": [(_STORE_PAIR, f"""        __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, {a});  // lab
+        __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, {a});""")]
+       for a in (0, 1, 3, 17)},
     "stamps": [
         ("char smem[8 * UNIT];", "char smem[8 * UNIT + 8192];"),
         ("  const bool g1 = wr == 1;  // wave-uniform (wave came through readfirstlane)",
@@ -95,10 +106,44 @@ PATCHES = {
 }
 
 
+REF_REV = os.environ.get("DDLB_LAB_REF", "HEAD")
+
+
+def source(name: str, variant: str) -> str:
+    """A header of csrc/gemm: from the working tree, or for the ``ref`` variant from git
+    revision ``DDLB_LAB_REF`` (default HEAD), so an edited kernel is timed against the committed
+    one in the same process."""
+    if variant != "ref":
+        return open(os.path.join(CSRC, name)).read()
+    return subprocess.run(["git", "-C", ROOT, "show", f"{REF_REV}:csrc/gemm/{name}"],
+                          capture_output=True, text=True, check=True).stdout
+
+
+DIFFS = {  # variants kept as a diff against the product header (research/lab/<file>)
+    "behind": "pt4_store_behind.diff",
+}
+
+
+def _apply_diff(text: str, diff_name: str) -> str:
+    import tempfile
+
+    with tempfile.TemporaryDirectory() as td:
+        os.makedirs(os.path.join(td, "csrc", "gemm"))
+        with open(os.path.join(td, "csrc", "gemm", "gemm_kernels.h"), "w") as f:
+            f.write(text)
+        r = subprocess.run(["patch", "-p1", "-s", "-i", os.path.join(HERE, diff_name)],
+                           cwd=td, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"{diff_name} does not apply: {r.stdout}{r.stderr}")
+        return open(os.path.join(td, "csrc", "gemm", "gemm_kernels.h")).read()
+
+
 def patched_header(variant: str) -> str:
     """The product header with the variant's substitutions applied inside the pt4 kernel's
     source (from its signature to the next kernel's); each pattern must occur exactly once."""
-    src = open(os.path.join(CSRC, "gemm_kernels.h")).read()
+    src = source("gemm_kernels.h", variant)
+    if variant in DIFFS:
+        return _apply_diff(src, DIFFS[variant])
     i = src.index("void gemm_tn_pt4_kernel(")
     j = src.index("void gemm_tn_pt8_kernel(", i)
     body = src[i:j]
@@ -118,7 +163,8 @@ def build(variant: str, verbose: bool = False) -> str:
     os.makedirs(d, exist_ok=True)
     os.makedirs(BIN, exist_ok=True)
     for h in ("gemm.h", "tile_map.h"):
-        shutil.copy(os.path.join(CSRC, h), os.path.join(d, h))
+        with open(os.path.join(d, h), "w") as f:
+            f.write(source(h, variant))
     text = patched_header(variant)
     with open(os.path.join(d, "gemm_kernels.h"), "w") as f:
         f.write(text)
@@ -192,15 +238,22 @@ def main() -> int:
         fns = {v: launcher(v) for v in names}
         if a.vendor and not mx:
             fns["F.linear"] = lambda: torch.nn.functional.linear(A, W)
-        if "base" in fns:
-            out.fill_(float("nan"))
-            fns["base"]()
-            torch.cuda.synchronize()
+        exact = [v for v in fns if v in ("base", "ref", "stamps", "behind") or
+                 v.startswith("aux")]
+        if exact:
             ref = A.float() @ W.float().t()
-            err = float(torch.nan_to_num((out.float() - ref).abs(), nan=float("inf")).max())
             bound = 2.0 ** -7 * float(ref.abs().max()) + K * 2.0 ** -12
-            print(f"{shp} base check: max|err| {err:.4g} (bound {bound:.4g}) "
-                  f"{'ok' if err <= bound else 'FAIL'}", flush=True)
+            for v in exact:
+                for rep in range(3):  # NaN-filled output, three launches: a race shows as NaN
+                    out.fill_(float("nan"))
+                    fns[v]()
+                    torch.cuda.synchronize()
+                    err = float(torch.nan_to_num((out.float() - ref).abs(),
+                                                 nan=float("inf")).max())
+                    if err > bound:
+                        break
+                print(f"{shp} {v} check: max|err| {err:.4g} (bound {bound:.4g}) "
+                      f"{'ok' if err <= bound else 'FAIL'}", flush=True)
             del ref
         for _ in range(200):  # clock ramp
             fns[names[0]]()

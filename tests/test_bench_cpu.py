@@ -306,6 +306,14 @@ def test_bench_world2_cpu_preflight_fields():
     assert d["preflight"]["ipc"] == "failed: scripted"
     assert d["timing"].startswith("cpu_clock window")
     assert d["harness_mean_ms"] > 0 and d["max_err"] <= d["err_bound"]
+    # first-contact diagnostics at world > 1: every part reported -- here
+    # with the native layer absent, as its own error -- inside the budget
+    diag = d["diag"]
+    assert set(diag) >= {"xgmi", "rccl", "trace", "budget_s", "wall_s", "job_s"}
+    assert set(diag["xgmi"]) == {"0", "1"}  # every rank's probe
+    for part in ("rccl", "trace"):
+        assert "error" in diag[part] or "skipped" in diag[part], diag[part]
+    assert diag["wall_s"] <= diag["budget_s"] + 5 and diag["job_s"] <= diag["budget_s"] + 45
 
 
 def test_autotune_drops_candidates_of_failed_primitive_phases():
@@ -401,3 +409,40 @@ def test_pool_fits_tuning_budget():
         skipped = [k for k, v in tune.items() if isinstance(v, str) and "deadline" in v]
         assert not skipped, (prim, dt, len(pool), spent, skipped)
         assert spent <= 300.0 + 45.0, (prim, dt, spent)
+
+
+def test_diagnose_parts_budget_and_errors():
+    """ddlb_amd.parallel.diagnose.run: parts in order, a raising part reported with its error
+    (the others still run), parts past the budget skipped, wall times recorded."""
+    from ddlb_amd.parallel import diagnose
+
+    t = [0.0]
+
+    def clock():
+        return t[0]
+
+    def slow():
+        t[0] += 20.0
+        return {"ok": 1}
+
+    def bad():
+        raise RuntimeError("no native layer\nsecond line")
+
+    res = diagnose.run({"xgmi": slow, "rccl": bad, "trace": slow, "late": slow}, 30.0,
+                       clock=clock)
+    assert res["xgmi"] == {"ok": 1, "wall_s": 20.0}
+    assert res["rccl"]["error"] == "RuntimeError: no native layer"
+    assert res["trace"]["wall_s"] == 20.0
+    assert res["late"]["skipped"].startswith("budget")
+    assert res["wall_s"] == 40.0
+
+
+def test_diagnose_message_sizes():
+    from ddlb_amd.parallel import diagnose
+
+    sz = diagnose.message_sizes("tp_columnwise", 65536, 1024, 1024, 8, 2)
+    assert sz == {"ag_shard": 16 << 20, "ag_stage_s4": 4 << 20, "ag_stage_s8": 2 << 20}
+    sz = diagnose.message_sizes("tp_rowwise", 16384, 8192, 8192, 8, 2)
+    assert sz["rs_block"] == 2048 * 8192 * 2
+    per = diagnose.merge_ranks([{"rccl": {"x": 1}, "xgmi": {"a": 1}}, {"xgmi": {"a": 2}}])
+    assert per["rccl"] == {"x": 1} and per["xgmi"] == {"0": {"a": 1}, "1": {"a": 2}}

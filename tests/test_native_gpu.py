@@ -1095,7 +1095,6 @@ def test_pt4_multi_tile(comm, M, N, K, dt, odt, mode):
     gemm(a, w, again, tile="pt4", mode=mode, ksplit=1)
     torch.cuda.synchronize()
     assert torch.equal(again, out)
-    assert res["cases"] == 5 and res["worst"] <= 1.0, res
 
 
 def test_cu_holder_occupies_whole_cus(comm):
@@ -1141,3 +1140,23 @@ def test_rccl_cap_phase_world1(comm):
 
     status = pf._rccl_cap_check(comm)
     assert status.startswith("cap 32: all-gather finished"), status
+
+
+def test_diagnose_world1(comm):
+    """bench.py's first-contact diagnostics on the device at world 1: no peers to probe, RCCL
+    bus bandwidth on the default and the 32-CTA communicator, and the per-op timeline of a
+    coll_pipeline plan (GEMM spans present, the span covers them), inside the budget."""
+    from ddlb_amd.parallel import diagnose
+    from ddlb_amd.primitives.tp_columnwise.native import NativeTPColumnwise
+
+    def factory():
+        return NativeTPColumnwise(m=8192, n=1024, k=1024, dtype="bfloat16",
+                                  algorithm="coll_pipeline", backend="rccl", s=4, graph=False)
+
+    res = diagnose.diagnose(comm, "tp_columnwise", 8192, 1024, 1024, 2, factory, budget_s=30.0)
+    assert res["xgmi"]["peers"] == 0, res
+    bw = res["rccl"]["busbw_GBps"]
+    assert set(bw) == {"default", "cap32"} and all(v > 0 for v in bw["default"].values()), res
+    tr = res["trace"]
+    assert tr["span_ms"] > 0 and tr["busy_ms_by_kind"].get("gemm", 0) > 0, tr
+    assert res["wall_s"] <= 35, res
