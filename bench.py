@@ -133,8 +133,9 @@ CANDIDATES_EXTRA = [
     ("coll_pipeline/ipc/kernel/s8/graph", "native", _graph(dict(             # 0.330 ms graph
         _COLL_IPC, s=8, multicast_protocol="kernel", copy_blocks=128, tile="128x128"))),
     ("coll_pipeline/ipc/push/s4", "native", dict(_COLL_IPC, direction="push")),  # host 411 us
-    # batch_memcpy: hipMemcpyBatchAsync is absent from torch's HIP 7.0 runtime, so every "batch"
-    # is per-segment copies (the ipc_batch preflight phase fails there and drops it anyway)
+    # batch_memcpy: without hipMemcpyBatchAsync (torch's HIP 7.0 runtime) an eager batch runs as
+    # one launch of a graph of memcpy nodes (the ipc_batch phase passes with it); kept out of the
+    # default pool for its cost: the s8 graph form's budget is dominated by the RCCL / agk forms
     ("coll_pipeline/ipc/batch/s8/graph", "native", _graph(dict(
         _COLL_IPC, s=8, multicast_protocol="batch_memcpy"))),
     ("coll_pipeline/ipc/memcpy/s8/graph", "native", _graph(dict(_COLL_IPC, s=8))),  # 0.779 ms

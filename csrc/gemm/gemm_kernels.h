@@ -1271,6 +1271,11 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   // per row each (lab: a 128 MB write-through stream 23.1-24.5 us vs 25.1-25.8 us in half lines,
   // nt only 20.8-22.0 vs 38.1-40.1 us, profiles/r05/r5_21_store_pattern.txt).
   constexpr bool PAIRST = DEFER && OUT != DT_F32;
+  // Cache policy of those stores: sc1 | nt (write-through, no L2 allocation), except for the
+  // block-scaled MX-fp8 kernel, whose tiles end twice as often (8 K-tiles per 1024-deep tile):
+  // sc0 | sc1 there, 2.3 % and 3.5 % faster on the MX flagship in two sessions (and 5-6 %
+  // slower for bf16, which keeps sc1 | nt; profiles/r06/r6_3_*, r6_4_*; lab variants auxN)
+  constexpr int CPOL = std::is_same<Mma, MmaMX>::value ? 17 : 18;
   const unsigned c_pair =
       (unsigned)(((wr * 128 + (frow & 7)) * p.ldc + wc * 64) * OSZ + ((frow & 8) ? 64 : 0) +
                  fq * 16);
@@ -1291,8 +1296,8 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
         const int64_t prow = cm0 + mq * 64 + f * 16;
         const unsigned so = (unsigned)((prow * p.ldc + cn0) * OSZ) + (KS ? ccs : 0u);
         const unsigned so8 = so + (unsigned)(8 * p.ldc * OSZ);
-        __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, 18);  // sc1 | nt
-        __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, 18);
+        __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, CPOL);
+        __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, CPOL);
         __builtin_amdgcn_sched_barrier(0);
       }
       __builtin_amdgcn_sched_barrier(0);

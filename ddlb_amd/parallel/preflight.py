@@ -374,7 +374,9 @@ def _own_rccl_check(comm, nbytes: int, count: int) -> None:
 
 def fused_rccl_cap(d: int) -> int:
     """The CTA cap the RCCL-fed fused candidates bind their communicator with (the plan's
-    ``rccl_max_ctas``, ``NativeContext.rccl``), from the rccl_fused phase's own plan."""
+    ``rccl_max_ctas``, ``NativeContext.rccl``), from the rccl_fused phase's own plan (built for
+    at least 2 ranks: at world 1 nothing is gated and the plan carries no cap)."""
+    d = max(int(d), 2)
     from ddlb_amd.parallel.algorithms import build_tp_columnwise
     from ddlb_amd.parallel.context import rccl_gate_cap
     from ddlb_amd.parallel.plan import DT_BF16

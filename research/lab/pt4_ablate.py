@@ -17,6 +17,9 @@ Variants (TIMING-ONLY unless marked exact):
             operands and the vmcnt windows that counted them shrink to the DMA alone
   l2store   C stores with the default (write-back) policy into one 128 KB region per XCD group
             (blocks b and b + 8 share it): the same store instructions, no HBM write stream
+  dmam      the B unit's LDS-DMA issued at the head of the MFMA phase instead of in the load
+            phase (exact); dmam1 the same at MFMA priority
+  lgkm_g0   wave group 0 waits for its fragment reads after the barrier, not before (exact)
   auxN      the product kernel with C store cache-policy bits N (exact)
   behind    store-behind (exact; research/lab/pt4_store_behind.diff, round 6, measured slower:
             profiles/r06/README.md): a tile's C packed into held registers and stored over three
@@ -42,8 +45,8 @@ CSRC = os.path.join(ROOT, "csrc", "gemm")
 BIN = os.path.join(HERE, "bin")
 WORK = os.path.join(ROOT, "build", "lab")
 
-_STORE_PAIR = ("""        __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, 18);  // sc1 | nt
-        __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, 18);""")
+_STORE_PAIR = ("""        __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, CPOL);
+        __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, CPOL);""")
 _SO = """        const unsigned so = (unsigned)((prow * p.ldc + cn0) * OSZ) + (KS ? ccs : 0u);"""
 
 _STAMP_DEF = """  const bool g1 = wr == 1;  // wave-uniform (wave came through readfirstlane)
@@ -92,10 +95,67 @@ PATCHES = {
         (_STORE_PAIR, """        __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, 0);  // lab: write-back
         __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, 0);"""),
     ],
-    # C store cache policy (aux bits of buffer_store: 1 sc0, 2 nt, 16 sc1; the product uses 18)
+    # the B unit's LDS-DMA (2 of the 4 ops a wave issues per load phase) moved from the load
+    # phase to the head of the wave's next MFMA phase (g1's waits after its load phases drop by
+    # the 2 ops issued after them; g0's waits after its MFMA phases keep their counts)
+    **{name: [
+        ("""      stage(0, 1, BUF ^ 1, qa);
+      stage(1, 1, BUF ^ 1, qa);
+      T4_LGKM0();
+      if (g1) wait_vm<KIND == 2 ? 8 + 3 * NS : 8>();
+      T4_BAR();
+      __builtin_amdgcn_s_setprio(1);
+      if constexpr (DEF) mm(1, 1, false);""", """      stage(0, 1, BUF ^ 1, qa);
+      T4_LGKM0();
+      if (g1) wait_vm<KIND == 2 ? 6 + 3 * NS : 6>();
+      T4_BAR();
+""" + ("      __builtin_amdgcn_s_setprio(1);\n" if prio else "") + """      stage(1, 1, BUF ^ 1, qa);  // lab
+      __builtin_amdgcn_s_setprio(1);
+      if constexpr (DEF) mm(1, 1, false);"""),
+        ("""      stage(0, 0, BUF, qb);
+      stage(1, 0, BUF, qb);
+      T4_LGKM0();
+      if (g1) wait_vm<KIND == 1 && !PAIRST ? 8 + NS : 8>();
+      T4_BAR();
+      __builtin_amdgcn_s_setprio(1);
+      mm(0, 1, Z);""", """      stage(0, 0, BUF, qb);
+      T4_LGKM0();
+      if (g1) wait_vm<KIND == 1 && !PAIRST ? 6 + NS : 6>();
+      T4_BAR();
+""" + ("      __builtin_amdgcn_s_setprio(1);\n" if prio else "") + """      stage(1, 0, BUF, qb);  // lab
+      __builtin_amdgcn_s_setprio(1);
+      mm(0, 1, Z);"""),
+    ] for name, prio in (("dmam", False), ("dmam1", True))},
+    # wave group 0 retires its fragment reads after the barrier instead of before it (its reads'
+    # WAR partner, g1's DMA into the same unit, comes 3 intervals later; g1's reads keep the
+    # lgkmcnt before the barrier: g0 restages their unit 1 interval later)
+    "lgkm_g0": [
+        ("""      T4_LGKM0();
+      if (g1) wait_vm<KIND == 2 ? 8 + 3 * NS : 8>();
+      T4_BAR();""", """      if (g1) {  // lab
+        T4_LGKM0();
+        wait_vm<KIND == 2 ? 8 + 3 * NS : 8>();
+        T4_BAR();
+      } else {
+        T4_BAR();
+        T4_LGKM0();
+      }"""),
+        ("""      T4_LGKM0();
+      if (g1) wait_vm<KIND == 1 && !PAIRST ? 8 + NS : 8>();
+      T4_BAR();""", """      if (g1) {  // lab
+        T4_LGKM0();
+        wait_vm<KIND == 1 && !PAIRST ? 8 + NS : 8>();
+        T4_BAR();
+      } else {
+        T4_BAR();
+        T4_LGKM0();
+      }"""),
+    ],
+    # C store cache policy (aux bits of buffer_store: 1 sc0, 2 nt, 16 sc1; the product uses 18,
+    # 17 for MX-fp8)
     **{f"aux{a}": [(_STORE_PAIR, f"""        __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, {a});  // lab
         __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, {a});""")]
-       for a in (0, 1, 3, 17)},
+       for a in (0, 1, 3, 17, 19)},
     "stamps": [
         ("char smem[8 * UNIT];", "char smem[8 * UNIT + 8192];"),
         ("  const bool g1 = wr == 1;  // wave-uniform (wave came through readfirstlane)",
@@ -238,8 +298,8 @@ def main() -> int:
         fns = {v: launcher(v) for v in names}
         if a.vendor and not mx:
             fns["F.linear"] = lambda: torch.nn.functional.linear(A, W)
-        exact = [v for v in fns if v in ("base", "ref", "stamps", "behind") or
-                 v.startswith("aux")]
+        exact = [v for v in fns if v in ("base", "ref", "stamps", "behind", "dmam", "dmam1",
+                                         "lgkm_g0") or v.startswith("aux")]
         if exact:
             ref = A.float() @ W.float().t()
             bound = 2.0 ** -7 * float(ref.abs().max()) + K * 2.0 ** -12

@@ -8,9 +8,9 @@ O=gpurun_out/r6_3
 mkdir -p $O
 export TMPDIR=/tmp
 L=research/lab/pt4_ablate.py
-timeout -k 10 200 python -u $L --variants base,aux0,aux1,aux3,aux17 --rounds 7 --shapes 65536x1024x1024,65536x1024x4096 > $O/ab_cpol_bf16.txt 2>&1 || { echo "ab bf16 failed"; tail -30 $O/ab_cpol_bf16.txt; exit 1; }
+timeout -k 10 200 python -u $L --variants base,dmam,dmam1,aux0,aux1,aux3,aux17 --rounds 7 --shapes 65536x1024x1024,65536x1024x4096 > $O/ab_cpol_bf16.txt 2>&1 || { echo "ab bf16 failed"; tail -30 $O/ab_cpol_bf16.txt; exit 1; }
 cat $O/ab_cpol_bf16.txt
-timeout -k 10 120 python -u $L --variants base,aux0,aux1,aux3,aux17 --dtype mx --rounds 7 --shapes 65536x1024x1024 > $O/ab_cpol_mx.txt 2>&1 || { echo "ab mx failed"; tail -30 $O/ab_cpol_mx.txt; exit 1; }
+timeout -k 10 120 python -u $L --variants base,dmam,dmam1,aux0,aux17 --dtype mx --rounds 7 --shapes 65536x1024x1024 > $O/ab_cpol_mx.txt 2>&1 || { echo "ab mx failed"; tail -30 $O/ab_cpol_mx.txt; exit 1; }
 cat $O/ab_cpol_mx.txt
 timeout -k 10 400 python -u -m pytest tests/test_native_gpu.py -x -v -m gpu --timeout 120 --timeout-method thread -k "cu_holder or rccl_cap or diagnose or pt4_multi_tile or rccl_data_plane" > $O/n1_tests.txt 2>&1 || { echo "tests failed"; grep -v "^  File\|^    " $O/n1_tests.txt | tail -40; exit 1; }
 grep -c PASSED $O/n1_tests.txt; tail -2 $O/n1_tests.txt
