@@ -24,6 +24,12 @@ Variants (TIMING-ONLY unless marked exact):
   behind    store-behind (exact; research/lab/pt4_store_behind.diff, round 6, measured slower:
             profiles/r06/README.md): a tile's C packed into held registers and stored over three
             intervals of the next tile instead of one
+  ring      A in a 3-deep ring of K-tile slots (exact; research/lab/pt4_a_ring.diff, round 6,
+            160 KB LDS, A staged three K-tiles ahead): within 1 % everywhere, slower on square
+            shapes (profiles/r06/README.md, r6_6)
+  stagG_Dk  workgroup slot (blockIdx / 8) mod G starts slot x D thousand shader cycles late
+            (exact): do desynchronized tile ends (C write bursts of fewer CUs at a time) pay for
+            the delay?
   stamps    the product kernel (exact) with an s_memtime stamp after every workgroup barrier by
             waves 0 and 4, kept in 8 KB of LDS beside the staging buffers (no vmcnt traffic) and
             written to the debug buffer at the end: [block][group][512] u64, entry 0 / 1 =
@@ -85,6 +91,7 @@ PATCHES = {
     "base": [],
     "ref": [],
     "behind": [],
+    "ring": [],
     "nostore": [
         ("constexpr int NS = 4 * Store8<OUT>::kStores;", "constexpr int NS = 0;"),
         (_STORE_PAIR, """        asm volatile("" ::"v"(x), "v"(y), "s"(so), "s"(so8));"""),
@@ -156,6 +163,17 @@ PATCHES = {
     **{f"aux{a}": [(_STORE_PAIR, f"""        __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, {a});  // lab
         __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, {a});""")]
        for a in (0, 1, 3, 17, 19)},
+    # desynchronized tile phases (TIMING-ONLY probe, exact results): workgroup slot g = (bid / 8)
+    # mod G (every XCD holds every slot) starts g * D shader cycles late, so the CUs' C write
+    # bursts stop coinciding; the delay is paid at the end
+    **{f"stag{g}_{d // 1000}k": [
+        ("  if (my_tiles == 0) return;\n", f"""  if (my_tiles == 0) return;
+  {{  // lab: stagger
+    const uint64_t lab_d = (uint64_t)((bid >> 3) % {g}) * {d}u;
+    const uint64_t lab_t = __builtin_amdgcn_s_memtime();
+    while (__builtin_amdgcn_s_memtime() - lab_t < lab_d) __builtin_amdgcn_s_sleep(2);
+  }}
+""")] for g, d in ((2, 3000), (2, 6000), (2, 12000), (4, 3000))},
     "stamps": [
         ("char smem[8 * UNIT];", "char smem[8 * UNIT + 8192];"),
         ("  const bool g1 = wr == 1;  // wave-uniform (wave came through readfirstlane)",
@@ -181,6 +199,7 @@ def source(name: str, variant: str) -> str:
 
 DIFFS = {  # variants kept as a diff against the product header (research/lab/<file>)
     "behind": "pt4_store_behind.diff",
+    "ring": "pt4_a_ring.diff",
 }
 
 
@@ -298,8 +317,8 @@ def main() -> int:
         fns = {v: launcher(v) for v in names}
         if a.vendor and not mx:
             fns["F.linear"] = lambda: torch.nn.functional.linear(A, W)
-        exact = [v for v in fns if v in ("base", "ref", "stamps", "behind", "dmam", "dmam1",
-                                         "lgkm_g0") or v.startswith("aux")]
+        exact = [v for v in fns if v in ("base", "ref", "stamps", "behind", "ring", "dmam", "dmam1",
+                                         "lgkm_g0") or v.startswith(("aux", "stag"))]
         if exact:
             ref = A.float() @ W.float().t()
             bound = 2.0 ** -7 * float(ref.abs().max()) + K * 2.0 ** -12

@@ -1072,12 +1072,18 @@ def test_side_stream_cycle_is_not_captured():
     (32768, 2048, 2048, "float16", "float16", "auto"),         # 4 tiles per workgroup, nk = 32
     (8192, 1024, 1024, "bfloat16", "bfloat16", "auto"),        # fewer tiles than CUs
     (4096, 512, 4096, "float8_e4m3fn", "bfloat16", "auto"),    # non-scaled fp8, long K
+    (65536, 1024, 256, "bfloat16", "bfloat16", "auto"),        # nk = 4: the shortest A ring
+    (65536, 1024, 384, "bfloat16", "bfloat16", "auto"),        # nk = 6
+    (65536, 1024, 128, "bfloat16", "bfloat16", "auto"),        # nk = 2: routed off the ring
+    (65536, 1024, 512, "float8_e4m3fn", "bfloat16", "mx"),     # MX, nk = 4
+    (65536, 1024, 256, "float8_e4m3fn", "bfloat16", "mx"),     # MX, nk = 2
 ])
 def test_pt4_multi_tile(comm, M, N, K, dt, odt, mode):
     """The ungated write-through pt4 across tile boundaries: with more tiles than CUs every
     workgroup runs several tiles back to back (the next tile's staging issued during the last
-    K-tiles of the current one, its C stores in flight across the switch). Against
-    the fp32 product with the tight bound, NaN-filled output, repeat bit-identical."""
+    K-tiles of the current one -- A three K-tiles ahead in its ring --, its C stores in flight
+    across the switch). Against the fp32 product with the tight bound, NaN-filled
+    output, repeat bit-identical."""
     from ddlb_amd.ops.gemm import gemm
 
     tdt, todt = getattr(torch, dt), getattr(torch, odt)
