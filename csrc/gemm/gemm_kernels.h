@@ -1064,7 +1064,8 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   // tile_order 3 (own rows first, never gated) exists only for the RCCL-fed gated GEMM, whose A
   // is a row table (APAN): every other pt4 kernel compiles it out (SGPR pressure)
   constexpr bool OWN = GATED && APAN;
-  __shared__ __attribute__((aligned(1024))) char smem[8 * UNIT];
+  // (DEFER 16-bit C: +32 KB, the parked C pairs, see PARK)
+  __shared__ __attribute__((aligned(1024))) char smem[(DEFER && OUT != DT_F32 ? 10 : 8) * UNIT];
   // CMODE 2: C through one wave-uniform descriptor (launch_pt4 checks the extent fits)
   const __amdgpu_buffer_rsrc_t crc =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.c, 0, 0x7FFFFFF0, 0x00020000);
@@ -1279,8 +1280,31 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   const unsigned c_pair =
       (unsigned)(((wr * 128 + (frow & 7)) * p.ldc + wc * 64) * OSZ + ((frow & 8) ? 64 : 0) +
                  fq * 16);
+  typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
+  // PARK (PAIRST): a tile's last NP of its 4 NS C stores per wave (rows mq = 1, f = 2, 3) go to
+  // LDS beside the staging buffers (4 KB per wave, the wave's own) and leave in the next tile's
+  // first K-tile, 2 after each load phase's DMA. The store path drains only ~12.6 B/clk per CU
+  // whatever the rest of the chip does (32 or 256 CUs storing alike, profiles/r06/r6_8), and the
+  // vmcnt of the next DMA waits count the stores issued before it: the tile-end interval is a
+  // queue of C stores, a quarter of which now leaves beside the next tile's MFMAs.
+  // (A workgroup's last tile drains its parked pairs at the end.)
+  constexpr bool PARK = PAIRST;
+  constexpr int NP = PARK ? 4 : 0;
+  constexpr int PBASE = 8 * UNIT;
+  unsigned pso = 0;  // the parked tile's C offset (its row 0, column 0, K-split partial)
+  auto park_read = [&](int j0, u32x4_t (&v)[2]) __attribute__((always_inline)) {
+    v[0] = *(const u32x4_t*)(smem + PBASE + wave * 4096 + j0 * 1024 + lane * 16);
+    v[1] = *(const u32x4_t*)(smem + PBASE + wave * 4096 + (j0 + 1) * 1024 + lane * 16);
+  };
+  auto park_store = [&](int j0, const u32x4_t (&v)[2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int jx = j0 + jj, f = 2 + (jx >> 1);  // slot: x (even) / y (odd, rows + 8) of f
+      const unsigned so = pso + (unsigned)((64 + f * 16 + ((jx & 1) ? 8 : 0)) * p.ldc * OSZ);
+      __builtin_amdgcn_raw_buffer_store_b128(v[jj], crc, c_pair, so, CPOL);
+    }
+  };
   auto store_pair = [&](int mq) __attribute__((always_inline)) {
-    typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
     if constexpr (PAIRST) {
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1293,11 +1317,17 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
           x[d] = (unsigned)__builtin_amdgcn_update_dpp(t, (int)y[d], 0x128, 0xF, 0xC, false);
           y[d] = (unsigned)__builtin_amdgcn_update_dpp((int)y[d], t, 0x128, 0xF, 0x3, false);
         }
-        const int64_t prow = cm0 + mq * 64 + f * 16;
-        const unsigned so = (unsigned)((prow * p.ldc + cn0) * OSZ) + (KS ? ccs : 0u);
-        const unsigned so8 = so + (unsigned)(8 * p.ldc * OSZ);
-        __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, CPOL);
-        __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, CPOL);
+        if (PARK && mq == 1 && f >= 2) {
+          char* pp = smem + PBASE + wave * 4096 + (f - 2) * 2048 + lane * 16;
+          *(u32x4_t*)pp = x;
+          *(u32x4_t*)(pp + 1024) = y;
+        } else {
+          const int64_t prow = cm0 + mq * 64 + f * 16;
+          const unsigned so = (unsigned)((prow * p.ldc + cn0) * OSZ) + (KS ? ccs : 0u);
+          const unsigned so8 = so + (unsigned)(8 * p.ldc * OSZ);
+          __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, CPOL);
+          __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, CPOL);
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -1357,12 +1387,19 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     constexpr bool Z = KIND == 2 || KIND == 4;
     if constexpr (DEFER) {
       constexpr bool DEF = KIND == 0 || KIND == 1;  // previous K-tile's A1 x B1
+      // PARK waits: the previous tile's 4 NS - NP direct stores, then per load phase 4 DMA + 2
+      // parked stores
+      constexpr int WK2A = PARK ? 8 + 4 * NS - NP + 2 : 8 + 3 * NS;
+      constexpr int WK2B = PARK ? 8 + 4 * NS - NP + 4 : 8;
+      u32x4_t pv[2];
       loadB(bufc, 0);  // phase A: halves 0
       loadA(bufc, 0);
+      if constexpr (PARK && KIND == 2) park_read(0, pv);
       stage(0, 1, BUF ^ 1, qa);
       stage(1, 1, BUF ^ 1, qa);
       T4_LGKM0();
-      if (g1) wait_vm<KIND == 2 ? 8 + 3 * NS : 8>();
+      if constexpr (PARK && KIND == 2) park_store(0, pv);
+      if (g1) wait_vm<KIND == 2 ? WK2A : 8>();
       T4_BAR();
       __builtin_amdgcn_s_setprio(1);
       if constexpr (DEF) mm(1, 1, false);
@@ -1371,14 +1408,16 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
       // (PAIRST: every store after phase B, the first pair needs quadrant (0, 1); the counts of
       // the two waits below then drop the NS stores issued here before)
       if constexpr (KIND == 1 && !PAIRST) store_q(0, 0);
-      if (!g1) wait_vm<KIND == 2 ? 8 + 3 * NS : (KIND == 1 && !PAIRST ? 8 + NS : 8)>();
+      if (!g1) wait_vm<KIND == 2 ? WK2A : (KIND == 1 && !PAIRST ? 8 + NS : 8)>();
       T4_BAR();
       loadB(bufc, 1);  // phase B: halves 1
       loadA(bufc, 1);
+      if constexpr (PARK && KIND == 2) park_read(2, pv);
       stage(0, 0, BUF, qb);
       stage(1, 0, BUF, qb);
       T4_LGKM0();
-      if (g1) wait_vm<KIND == 1 && !PAIRST ? 8 + NS : 8>();
+      if constexpr (PARK && KIND == 2) park_store(2, pv);
+      if (g1) wait_vm<KIND == 2 ? WK2B : (KIND == 1 && !PAIRST ? 8 + NS : 8)>();
       T4_BAR();
       __builtin_amdgcn_s_setprio(1);
       mm(0, 1, Z);
@@ -1389,7 +1428,8 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
       if constexpr (KIND == 1) mm(1, 1, false);
       __builtin_amdgcn_s_setprio(0);
       if constexpr (KIND == 1 && PAIRST) {
-        store_pair(1);  // 4 NS stores in all, as the quadrant form's
+        if constexpr (PARK) pso = (unsigned)((cm0 * p.ldc + cn0) * OSZ) + (KS ? ccs : 0u);
+        store_pair(1);  // 4 NS stores in all (NP of them parked), as the quadrant form's
       } else if constexpr (KIND == 1) {
         store_q(0, 1);
         store_q(1, 0);
@@ -1402,7 +1442,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
           acc[4 + f][3] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
-      if (!g1) wait_vm<KIND == 1 ? 8 + 4 * NS : 8>();
+      if (!g1) wait_vm<KIND == 1 ? 8 + 4 * NS - NP : (KIND == 2 ? WK2B : 8)>();
       T4_BAR();
     } else {
       if (GATED && qa.kt == 0) {
@@ -1474,6 +1514,13 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   tile_body(std::integral_constant<int, DEFER ? 4 : 0>{}, K1{});
   for (ti = 1; ti < my_tiles; ++ti) tile_body(std::integral_constant<int, 2>{}, K1{});
   if (!g1) T4_BAR();
+  if constexpr (PARK) {  // the last tile's parked pairs
+    u32x4_t pv[2];
+    park_read(0, pv);
+    park_store(0, pv);
+    park_read(2, pv);
+    park_store(2, pv);
+  }
 #undef T4_BAR
 #undef T4_LGKM0
   wait_vm<0>();  // never leave an LDS-DMA in flight past the end of the workgroup

@@ -27,10 +27,12 @@ Variants (TIMING-ONLY unless marked exact):
   ring      A in a 3-deep ring of K-tile slots (exact; research/lab/pt4_a_ring.diff, round 6,
             160 KB LDS, A staged three K-tiles ahead): within 1 % everywhere, slower on square
             shapes (profiles/r06/README.md, r6_6)
+  relax     the first K-tile after a tile's C stores waits for them only as far as the DMA it
+            needs requires (exact)
   stagG_Dk  workgroup slot (blockIdx / 8) mod G starts slot x D thousand shader cycles late
             (exact): do desynchronized tile ends (C write bursts of fewer CUs at a time) pay for
             the delay?
-  stamps    the product kernel (exact) with an s_memtime stamp after every workgroup barrier by
+  stamps    the product kernel without the C park (exact) with an s_memtime stamp after every workgroup barrier by
             waves 0 and 4, kept in 8 KB of LDS beside the staging buffers (no vmcnt traffic) and
             written to the debug buffer at the end: [block][group][512] u64, entry 0 / 1 =
             s_memrealtime at start / end, 2 = stamp count, 3.. = stamps
@@ -163,6 +165,19 @@ PATCHES = {
     **{f"aux{a}": [(_STORE_PAIR, f"""        __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, {a});  // lab
         __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, {a});""")]
        for a in (0, 1, 3, 17, 19)},
+    # the first K-tile of a tile (KIND 2) keeps the previous tile's C stores in flight up to the
+    # exact counts (PAIRST: 8 + 4 NS at all four waits) instead of 8 + 3 NS / 8
+    "relax": [
+        ("if (g1) wait_vm<KIND == 2 ? 8 + 3 * NS : 8>();",
+         "if (g1) wait_vm<KIND == 2 ? (PAIRST ? 8 + 4 * NS : 8 + 3 * NS) : 8>();  // lab"),
+        ("if (!g1) wait_vm<KIND == 2 ? 8 + 3 * NS : (KIND == 1 && !PAIRST ? 8 + NS : 8)>();",
+         "if (!g1) wait_vm<KIND == 2 ? (PAIRST ? 8 + 4 * NS : 8 + 3 * NS) : "
+         "(KIND == 1 && !PAIRST ? 8 + NS : 8)>();  // lab"),
+        ("if (g1) wait_vm<KIND == 1 && !PAIRST ? 8 + NS : 8>();",
+         "if (g1) wait_vm<KIND == 2 && PAIRST ? 8 + 4 * NS : (KIND == 1 && !PAIRST ? 8 + NS : 8)>();"),
+        ("if (!g1) wait_vm<KIND == 1 ? 8 + 4 * NS : 8>();",
+         "if (!g1) wait_vm<KIND == 1 || (KIND == 2 && PAIRST) ? 8 + 4 * NS : 8>();  // lab"),
+    ],
     # desynchronized tile phases (TIMING-ONLY probe, exact results): workgroup slot g = (bid / 8)
     # mod G (every XCD holds every slot) starts g * D shader cycles late, so the CUs' C write
     # bursts stop coinciding; the delay is paid at the end
@@ -174,8 +189,9 @@ PATCHES = {
     while (__builtin_amdgcn_s_memtime() - lab_t < lab_d) __builtin_amdgcn_s_sleep(2);
   }}
 """)] for g, d in ((2, 3000), (2, 6000), (2, 12000), (4, 3000))},
-    "stamps": [
-        ("char smem[8 * UNIT];", "char smem[8 * UNIT + 8192];"),
+    "stamps": [  # (the C-park area gives way to the stamps: LDS is full with it)
+        ("char smem[(DEFER && OUT != DT_F32 ? 10 : 8) * UNIT];", "char smem[8 * UNIT + 8192];"),
+        ("  constexpr bool PARK = PAIRST;", "  constexpr bool PARK = false;  // lab: stamps"),
         ("  const bool g1 = wr == 1;  // wave-uniform (wave came through readfirstlane)",
          _STAMP_DEF),
         ("  wait_vm<0>();  // never leave an LDS-DMA in flight past the end of the workgroup",
@@ -318,7 +334,7 @@ def main() -> int:
         if a.vendor and not mx:
             fns["F.linear"] = lambda: torch.nn.functional.linear(A, W)
         exact = [v for v in fns if v in ("base", "ref", "stamps", "behind", "ring", "dmam", "dmam1",
-                                         "lgkm_g0") or v.startswith(("aux", "stag"))]
+                                         "lgkm_g0", "relax", "park") or v.startswith(("aux", "stag"))]
         if exact:
             ref = A.float() @ W.float().t()
             bound = 2.0 ** -7 * float(ref.abs().max()) + K * 2.0 ** -12
