@@ -27,6 +27,9 @@ Variants (TIMING-ONLY unless marked exact):
   ring      A in a 3-deep ring of K-tile slots (exact; research/lab/pt4_a_ring.diff, round 6,
             160 KB LDS, A staged three K-tiles ahead): within 1 % everywhere, slower on square
             shapes (profiles/r06/README.md, r6_6)
+  hold      8 of 16 C stores per wave beside the next tile's MFMAs: 4 held in registers (K-tile
+            0), 4 parked (K-tile 1, under a run-time flag) (exact; research/lab/pt4_hold.diff,
+            round 6: slower, r6_11)
   relax     the first K-tile after a tile's C stores waits for them only as far as the DMA it
             needs requires (exact)
   stagG_Dk  workgroup slot (blockIdx / 8) mod G starts slot x D thousand shader cycles late
@@ -94,6 +97,7 @@ PATCHES = {
     "ref": [],
     "behind": [],
     "ring": [],
+    "hold": [],
     "nostore": [
         ("constexpr int NS = 4 * Store8<OUT>::kStores;", "constexpr int NS = 0;"),
         (_STORE_PAIR, """        asm volatile("" ::"v"(x), "v"(y), "s"(so), "s"(so8));"""),
@@ -216,6 +220,7 @@ def source(name: str, variant: str) -> str:
 DIFFS = {  # variants kept as a diff against the product header (research/lab/<file>)
     "behind": "pt4_store_behind.diff",
     "ring": "pt4_a_ring.diff",
+    "hold": "pt4_hold.diff",
 }
 
 
@@ -334,7 +339,7 @@ def main() -> int:
         if a.vendor and not mx:
             fns["F.linear"] = lambda: torch.nn.functional.linear(A, W)
         exact = [v for v in fns if v in ("base", "ref", "stamps", "behind", "ring", "dmam", "dmam1",
-                                         "lgkm_g0", "relax", "park") or v.startswith(("aux", "stag"))]
+                                         "lgkm_g0", "relax", "hold") or v.startswith(("aux", "stag"))]
         if exact:
             ref = A.float() @ W.float().t()
             bound = 2.0 ** -7 * float(ref.abs().max()) + K * 2.0 ** -12
