@@ -17,6 +17,7 @@ Variants (TIMING-ONLY unless marked exact):
             operands and the vmcnt windows that counted them shrink to the DMA alone
   l2store   C stores with the default (write-back) policy into one 128 KB region per XCD group
             (blocks b and b + 8 share it): the same store instructions, no HBM write stream
+            (the parked quarter still goes to C as in the product)
   dmam      the B unit's LDS-DMA issued at the head of the MFMA phase instead of in the load
             phase (exact); dmam1 the same at MFMA priority
   lgkm_g0   wave group 0 waits for its fragment reads after the barrier, not before (exact)
@@ -30,6 +31,8 @@ Variants (TIMING-ONLY unless marked exact):
   hold      8 of 16 C stores per wave beside the next tile's MFMAs: 4 held in registers (K-tile
             0), 4 parked (K-tile 1, under a run-time flag) (exact; research/lab/pt4_hold.diff,
             round 6: slower, r6_11)
+  nodma / noread / nomfma  the iterations without their operand DMA / fragment reads / MFMAs
+            (TIMING-ONLY): what each costs the steady K-tile
   relax     the first K-tile after a tile's C stores waits for them only as far as the DMA it
             needs requires (exact)
   stagG_Dk  workgroup slot (blockIdx / 8) mod G starts slot x D thousand shader cycles late
@@ -56,9 +59,9 @@ CSRC = os.path.join(ROOT, "csrc", "gemm")
 BIN = os.path.join(HERE, "bin")
 WORK = os.path.join(ROOT, "build", "lab")
 
-_STORE_PAIR = ("""        __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, CPOL);
-        __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, CPOL);""")
-_SO = """        const unsigned so = (unsigned)((prow * p.ldc + cn0) * OSZ) + (KS ? ccs : 0u);"""
+_STORE_PAIR = ("""          __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, CPOL);
+          __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, CPOL);""")
+_SO = """          const unsigned so = (unsigned)((prow * p.ldc + cn0) * OSZ) + (KS ? ccs : 0u);"""
 
 _STAMP_DEF = """  const bool g1 = wr == 1;  // wave-uniform (wave came through readfirstlane)
   // lab: stamps after every barrier, waves 0 and 4, in LDS past the staging buffers
@@ -100,13 +103,16 @@ PATCHES = {
     "hold": [],
     "nostore": [
         ("constexpr int NS = 4 * Store8<OUT>::kStores;", "constexpr int NS = 0;"),
-        (_STORE_PAIR, """        asm volatile("" ::"v"(x), "v"(y), "s"(so), "s"(so8));"""),
+        ("  constexpr int NP = PARK ? 4 : 0;", "  constexpr int NP = 0;  // lab"),
+        (_STORE_PAIR, """          asm volatile("" ::"v"(x), "v"(y), "s"(so), "s"(so8));"""),
+        ("      __builtin_amdgcn_raw_buffer_store_b128(v[jj], crc, c_pair, so, CPOL);",
+         '      asm volatile("" ::"v"(v[jj]), "s"(so));  // lab'),
     ],
     "l2store": [
-        (_SO, """        const unsigned so = (unsigned)((((int64_t)(blockIdx.x % 8) * 256 + mq * 64 + f * 16) *
-                                         p.ldc) * OSZ);  // lab: one region per XCD group"""),
-        (_STORE_PAIR, """        __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, 0);  // lab: write-back
-        __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, 0);"""),
+        (_SO, """          const unsigned so = (unsigned)((((int64_t)(blockIdx.x % 8) * 256 + mq * 64 + f * 16) *
+                                           p.ldc) * OSZ);  // lab: one region per XCD group"""),
+        (_STORE_PAIR, """          __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, 0);  // lab: write-back
+          __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, 0);"""),
     ],
     # the B unit's LDS-DMA (2 of the 4 ops a wave issues per load phase) moved from the load
     # phase to the head of the wave's next MFMA phase (g1's waits after its load phases drop by
@@ -166,9 +172,31 @@ PATCHES = {
     ],
     # C store cache policy (aux bits of buffer_store: 1 sc0, 2 nt, 16 sc1; the product uses 18,
     # 17 for MX-fp8)
-    **{f"aux{a}": [(_STORE_PAIR, f"""        __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, {a});  // lab
-        __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, {a});""")]
+    **{f"aux{a}": [(_STORE_PAIR, f"""          __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, {a});  // lab
+          __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, {a});""")]
        for a in (0, 1, 3, 17, 19)},
+    # where the steady K-tile's time goes (TIMING-ONLY, wrong results): no operand DMA in the
+    # iterations (the prologue's stays), no fragment reads, no MFMAs (operands kept alive)
+    "nodma": [
+        ("      stage(0, 1, BUF ^ 1, qa);\n      stage(1, 1, BUF ^ 1, qa);\n      T4_LGKM0();\n"
+         "      if constexpr (PARK", "      T4_LGKM0();\n      if constexpr (PARK"),
+        ("      stage(0, 0, BUF, qb);\n      stage(1, 0, BUF, qb);\n      T4_LGKM0();\n"
+         "      if constexpr (PARK", "      T4_LGKM0();\n      if constexpr (PARK"),
+    ],
+    "noread": [
+        ("      loadB(bufc, 0);  // phase A: halves 0\n      loadA(bufc, 0);\n      if constexpr (PARK",
+         "      if constexpr (PARK"),
+        ("      loadB(bufc, 1);  // phase B: halves 1\n      loadA(bufc, 1);\n      if constexpr (PARK",
+         "      if constexpr (PARK"),
+    ],
+    "nomfma": [
+        ("          Mma::step8(acc[mq * 4 + f][nq * 2 + g], bP[nq][g], aP[h][f]);",
+         '          asm volatile("" ::"v"(bP[nq][g]), "v"(aP[h][f]));  // lab'),
+        ("            Mma::step(acc[mq * 4 + f][nq * 2 + g], bR[nq][g][kk], aR[h][f][kk]);",
+         '            asm volatile("" ::"v"(bR[nq][g][kk]), "v"(aR[h][f][kk]));  // lab'),
+    ],
+    # MFMAs and barriers only
+    "mfmaonly": "nodma+noread",
     # the first K-tile of a tile (KIND 2) keeps the previous tile's C stores in flight up to the
     # exact counts (PAIRST: 8 + 4 NS at all four waits) instead of 8 + 3 NS / 8
     "relax": [
@@ -247,7 +275,10 @@ def patched_header(variant: str) -> str:
     i = src.index("void gemm_tn_pt4_kernel(")
     j = src.index("void gemm_tn_pt8_kernel(", i)
     body = src[i:j]
-    for old, new in PATCHES[variant]:
+    pats = PATCHES[variant]
+    if isinstance(pats, str):  # a combination of other variants' patches
+        pats = [pt for v in pats.split("+") for pt in PATCHES[v]]
+    for old, new in pats:
         n = body.count(old)
         if n != 1:
             raise RuntimeError(f"variant {variant}: pattern found {n} times: {old[:60]!r}")
