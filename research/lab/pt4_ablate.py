@@ -174,7 +174,7 @@ PATCHES = {
     # 17 for MX-fp8)
     **{f"aux{a}": [(_STORE_PAIR, f"""          __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, {a});  // lab
           __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, {a});""")]
-       for a in (0, 1, 3, 17, 19)},
+       for a in (0, 1, 3, 17, 18, 19)},
     # where the steady K-tile's time goes (TIMING-ONLY, wrong results): no operand DMA in the
     # iterations (the prologue's stays), no fragment reads, no MFMAs (operands kept alive)
     "nodma": [
