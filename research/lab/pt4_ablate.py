@@ -33,6 +33,8 @@ Variants (TIMING-ONLY unless marked exact):
             round 6: slower, r6_11)
   nodma / noread / nomfma  the iterations without their operand DMA / fragment reads / MFMAs
             (TIMING-ONLY): what each costs the steady K-tile
+  hold0     the 4 held pairs and the 4 parked ones all stored in the next tile's K-tile 0 (exact;
+            research/lab/pt4_hold0.diff, round 6: 1.3-1.4 % slower, r6_16)
   relax     the first K-tile after a tile's C stores waits for them only as far as the DMA it
             needs requires (exact)
   stagG_Dk  workgroup slot (blockIdx / 8) mod G starts slot x D thousand shader cycles late
@@ -101,6 +103,7 @@ PATCHES = {
     "behind": [],
     "ring": [],
     "hold": [],
+    "hold0": [],
     "nostore": [
         ("constexpr int NS = 4 * Store8<OUT>::kStores;", "constexpr int NS = 0;"),
         ("  constexpr int NP = PARK ? 4 : 0;", "  constexpr int NP = 0;  // lab"),
@@ -249,6 +252,7 @@ DIFFS = {  # variants kept as a diff against the product header (research/lab/<f
     "behind": "pt4_store_behind.diff",
     "ring": "pt4_a_ring.diff",
     "hold": "pt4_hold.diff",
+    "hold0": "pt4_hold0.diff",
 }
 
 
@@ -370,7 +374,7 @@ def main() -> int:
         if a.vendor and not mx:
             fns["F.linear"] = lambda: torch.nn.functional.linear(A, W)
         exact = [v for v in fns if v in ("base", "ref", "stamps", "behind", "ring", "dmam", "dmam1",
-                                         "lgkm_g0", "relax", "hold") or v.startswith(("aux", "stag"))]
+                                         "lgkm_g0", "relax", "hold", "hold0") or v.startswith(("aux", "stag"))]
         if exact:
             ref = A.float() @ W.float().t()
             bound = 2.0 ** -7 * float(ref.abs().max()) + K * 2.0 ** -12
