@@ -237,14 +237,27 @@ PATCHES = {
 
 REF_REV = os.environ.get("DDLB_LAB_REF", "HEAD")
 
+# Variants measured and dropped against an earlier product kernel apply to the headers of that
+# revision (the product moved on: the C park changed the code they patch); they rebuild exactly
+# what was measured.
+PINNED = {
+    "behind": "2c4e4ca",   # r6_2
+    "dmam": "38ab6ea",     # r6_3
+    "dmam1": "38ab6ea",
+    "lgkm_g0": "38ab6ea",  # r6_4
+    "relax": "38ab6ea",    # r6_9
+    "ring": "38ab6ea",     # r6_6
+}
+
 
 def source(name: str, variant: str) -> str:
-    """A header of csrc/gemm: from the working tree, or for the ``ref`` variant from git
-    revision ``DDLB_LAB_REF`` (default HEAD), so an edited kernel is timed against the committed
-    one in the same process."""
-    if variant != "ref":
+    """A header of csrc/gemm: from the working tree; for the ``ref`` variant from git revision
+    ``DDLB_LAB_REF`` (default HEAD), so an edited kernel is timed against the committed one in
+    the same process; for a PINNED variant from its revision."""
+    rev = REF_REV if variant == "ref" else PINNED.get(variant)
+    if rev is None:
         return open(os.path.join(CSRC, name)).read()
-    return subprocess.run(["git", "-C", ROOT, "show", f"{REF_REV}:csrc/gemm/{name}"],
+    return subprocess.run(["git", "-C", ROOT, "show", f"{rev}:csrc/gemm/{name}"],
                           capture_output=True, text=True, check=True).stdout
 
 
