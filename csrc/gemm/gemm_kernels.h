@@ -1387,6 +1387,10 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     constexpr bool Z = KIND == 2 || KIND == 4;
     if constexpr (DEFER) {
       constexpr bool DEF = KIND == 0 || KIND == 1;  // previous K-tile's A1 x B1
+      // MFMA phases at raised wave priority for the MX kernel only: without it the 16-bit
+      // kernels ran 0.2-1.1 % faster on all 8 shapes of two sessions (flagship, K = 4096 / 8192,
+      // 8192^3, 16384x8192x8192), MX-fp8 flat to 0.9 % slower (profiles/r06/r6_18, r6_19)
+      constexpr bool PRIO = std::is_same<Mma, MmaMX>::value;
       // PARK waits: the previous tile's 4 NS - NP direct stores, then per load phase 4 DMA + 2
       // parked stores
       constexpr int WK2A = PARK ? 8 + 4 * NS - NP + 2 : 8 + 3 * NS;
@@ -1401,10 +1405,10 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
       if constexpr (PARK && KIND == 2) park_store(0, pv);
       if (g1) wait_vm<KIND == 2 ? WK2A : 8>();
       T4_BAR();
-      __builtin_amdgcn_s_setprio(1);
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
       if constexpr (DEF) mm(1, 1, false);
       mm(0, 0, Z);
-      __builtin_amdgcn_s_setprio(0);
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
       // (PAIRST: every store after phase B, the first pair needs quadrant (0, 1); the counts of
       // the two waits below then drop the NS stores issued here before)
       if constexpr (KIND == 1 && !PAIRST) store_q(0, 0);
@@ -1419,14 +1423,14 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
       if constexpr (PARK && KIND == 2) park_store(2, pv);
       if (g1) wait_vm<KIND == 2 ? WK2B : (KIND == 1 && !PAIRST ? 8 + NS : 8)>();
       T4_BAR();
-      __builtin_amdgcn_s_setprio(1);
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
       mm(0, 1, Z);
       // PAIRST: rows mq = 0 are final here; storing them now frees their accumulators before
       // the rest of the phase (held to the end of the phase they spilled 52 bytes)
       if constexpr (KIND == 1 && PAIRST) store_pair(0);
       mm(1, 0, Z);
       if constexpr (KIND == 1) mm(1, 1, false);
-      __builtin_amdgcn_s_setprio(0);
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
       if constexpr (KIND == 1 && PAIRST) {
         if constexpr (PARK) pso = (unsigned)((cm0 * p.ldc + cn0) * OSZ) + (KS ? ccs : 0u);
         store_pair(1);  // 4 NS stores in all (NP of them parked), as the quadrant form's

@@ -40,6 +40,9 @@ Variants (TIMING-ONLY unless marked exact):
   stagG_Dk  workgroup slot (blockIdx / 8) mod G starts slot x D thousand shader cycles late
             (exact): do desynchronized tile ends (C write bursts of fewer CUs at a time) pay for
             the delay?
+  dmafirst  each load phase issues its 4 LDS-DMA pieces before its 12 fragment reads (exact);
+            dmamid between the B and the A reads
+  noprio    the MFMA phases without s_setprio 1 (exact)
   stamps    the product kernel without the C park (exact) with an s_memtime stamp after every workgroup barrier by
             waves 0 and 4, kept in 8 KB of LDS beside the staging buffers (no vmcnt traffic) and
             written to the debug buffer at the end: [block][group][512] u64, entry 0 / 1 =
@@ -224,6 +227,37 @@ PATCHES = {
     while (__builtin_amdgcn_s_memtime() - lab_t < lab_d) __builtin_amdgcn_s_sleep(2);
   }}
 """)] for g, d in ((2, 3000), (2, 6000), (2, 12000), (4, 3000))},
+    # load-phase order (exact): the 4 LDS-DMA pieces issued before the 12 fragment reads
+    # (dmafirst) or between the B and the A reads (dmamid). The DMA writes units no read of the
+    # phase touches, and the vmcnt counts stay (the DMA still precedes the parked stores)
+    **{name: [
+        ("""      loadB(bufc, 0);  // phase A: halves 0
+      loadA(bufc, 0);
+      if constexpr (PARK && KIND == 2) park_read(0, pv);
+      stage(0, 1, BUF ^ 1, qa);
+      stage(1, 1, BUF ^ 1, qa);
+""", pre + """      stage(0, 1, BUF ^ 1, qa);  // lab
+      stage(1, 1, BUF ^ 1, qa);
+""" + post.replace("@", "0") + """      if constexpr (PARK && KIND == 2) park_read(0, pv);
+"""),
+        ("""      loadB(bufc, 1);  // phase B: halves 1
+      loadA(bufc, 1);
+      if constexpr (PARK && KIND == 2) park_read(2, pv);
+      stage(0, 0, BUF, qb);
+      stage(1, 0, BUF, qb);
+""", pre.replace("0);", "1);") + """      stage(0, 0, BUF, qb);  // lab
+      stage(1, 0, BUF, qb);
+""" + post.replace("@", "1") + """      if constexpr (PARK && KIND == 2) park_read(2, pv);
+"""),
+    ] for name, pre, post in (
+        ("dmafirst", "", "      loadB(bufc, @);\n      loadA(bufc, @);\n"),
+        ("dmamid", "      loadB(bufc, 0);\n", "      loadA(bufc, @);\n"))},
+    # no wave priority: the MFMA phases without s_setprio 1 (exact)
+    "noprio": [
+        ("      __builtin_amdgcn_s_setprio(1);\n      if constexpr (DEF) mm(1, 1, false);",
+         "      if constexpr (DEF) mm(1, 1, false);  // lab"),
+        ("      __builtin_amdgcn_s_setprio(1);\n      mm(0, 1, Z);", "      mm(0, 1, Z);  // lab"),
+    ],
     "stamps": [  # (the C-park area gives way to the stamps: LDS is full with it)
         ("char smem[(DEFER && OUT != DT_F32 ? 10 : 8) * UNIT];", "char smem[8 * UNIT + 8192];"),
         ("  constexpr bool PARK = PAIRST;", "  constexpr bool PARK = false;  // lab: stamps"),
@@ -247,6 +281,11 @@ PINNED = {
     "lgkm_g0": "38ab6ea",  # r6_4
     "relax": "38ab6ea",    # r6_9
     "ring": "38ab6ea",     # r6_6
+    "hold": "34f0106",     # r6_11
+    "hold0": "b8b30bb",    # r6_16
+    "dmafirst": "8c58daa",  # r6_18
+    "dmamid": "8c58daa",
+    "noprio": "8c58daa",    # r6_18, r6_19 (adopted for the 16-bit kernels)
 }
 
 
@@ -387,7 +426,7 @@ def main() -> int:
         if a.vendor and not mx:
             fns["F.linear"] = lambda: torch.nn.functional.linear(A, W)
         exact = [v for v in fns if v in ("base", "ref", "stamps", "behind", "ring", "dmam", "dmam1",
-                                         "lgkm_g0", "relax", "hold", "hold0") or v.startswith(("aux", "stag"))]
+                                         "lgkm_g0", "relax", "hold", "hold0", "dmafirst", "dmamid", "noprio") or v.startswith(("aux", "stag"))]
         if exact:
             ref = A.float() @ W.float().t()
             bound = 2.0 ** -7 * float(ref.abs().max()) + K * 2.0 ** -12
