@@ -43,6 +43,9 @@ Variants (TIMING-ONLY unless marked exact):
   dmafirst  each load phase issues its 4 LDS-DMA pieces before its 12 fragment reads (exact);
             dmamid between the B and the A reads
   noprio    the MFMA phases without s_setprio 1 (exact)
+  lgkm0     lgkm_g0 on the park kernel: wave group 0's fragment-read wait left to the compiler's
+            waits at the consuming MFMAs, after the barrier (exact)
+  prioload  the load phases at wave priority 2 (exact)
   stamps    the product kernel without the C park (exact) with an s_memtime stamp after every workgroup barrier by
             waves 0 and 4, kept in 8 KB of LDS beside the staging buffers (no vmcnt traffic) and
             written to the debug buffer at the end: [block][group][512] u64, entry 0 / 1 =
@@ -258,6 +261,32 @@ PATCHES = {
          "      if constexpr (DEF) mm(1, 1, false);  // lab"),
         ("      __builtin_amdgcn_s_setprio(1);\n      mm(0, 1, Z);", "      mm(0, 1, Z);  // lab"),
     ],
+    # lgkm_g0 on the park kernel (exact): wave group 0 leaves its fragment-read wait to the
+    # compiler's waits at the MFMAs that consume them, after the barrier
+    "lgkm0": [
+        ("""      T4_LGKM0();
+      if constexpr (PARK && KIND == 2) park_store(0, pv);""",
+         """      if (g1) T4_LGKM0();  // lab
+      if constexpr (PARK && KIND == 2) park_store(0, pv);"""),
+        ("""      T4_LGKM0();
+      if constexpr (PARK && KIND == 2) park_store(2, pv);""",
+         """      if (g1) T4_LGKM0();  // lab
+      if constexpr (PARK && KIND == 2) park_store(2, pv);"""),
+    ],
+    # load phases at wave priority 2, above either MFMA phase (exact)
+    "prioload": [
+        ("      loadB(bufc, 0);  // phase A: halves 0\n",
+         "      __builtin_amdgcn_s_setprio(2);  // lab\n      loadB(bufc, 0);\n"),
+        ("      if (g1) wait_vm<KIND == 2 ? WK2A : 8>();\n      T4_BAR();\n",
+         "      if (g1) wait_vm<KIND == 2 ? WK2A : 8>();\n"
+         "      __builtin_amdgcn_s_setprio(0);  // lab\n      T4_BAR();\n"),
+        ("      loadB(bufc, 1);  // phase B: halves 1\n",
+         "      __builtin_amdgcn_s_setprio(2);  // lab\n      loadB(bufc, 1);\n"),
+        ("      if (g1) wait_vm<KIND == 2 ? WK2B : (KIND == 1 && !PAIRST ? 8 + NS : 8)>();\n"
+         "      T4_BAR();\n",
+         "      if (g1) wait_vm<KIND == 2 ? WK2B : (KIND == 1 && !PAIRST ? 8 + NS : 8)>();\n"
+         "      __builtin_amdgcn_s_setprio(0);  // lab\n      T4_BAR();\n"),
+    ],
     "stamps": [  # (the C-park area gives way to the stamps: LDS is full with it)
         ("char smem[(DEFER && OUT != DT_F32 ? 10 : 8) * UNIT];", "char smem[8 * UNIT + 8192];"),
         ("  constexpr bool PARK = PAIRST;", "  constexpr bool PARK = false;  // lab: stamps"),
@@ -286,6 +315,8 @@ PINNED = {
     "dmafirst": "8c58daa",  # r6_18
     "dmamid": "8c58daa",
     "noprio": "8c58daa",    # r6_18, r6_19 (adopted for the 16-bit kernels)
+    "lgkm0": "e2c6c5f",     # r6_21
+    "prioload": "e2c6c5f",
 }
 
 
@@ -426,7 +457,7 @@ def main() -> int:
         if a.vendor and not mx:
             fns["F.linear"] = lambda: torch.nn.functional.linear(A, W)
         exact = [v for v in fns if v in ("base", "ref", "stamps", "behind", "ring", "dmam", "dmam1",
-                                         "lgkm_g0", "relax", "hold", "hold0", "dmafirst", "dmamid", "noprio") or v.startswith(("aux", "stag"))]
+                                         "lgkm_g0", "relax", "hold", "hold0", "dmafirst", "dmamid", "noprio", "lgkm0", "prioload") or v.startswith(("aux", "stag"))]
         if exact:
             ref = A.float() @ W.float().t()
             bound = 2.0 ** -7 * float(ref.abs().max()) + K * 2.0 ** -12
