@@ -46,6 +46,10 @@ Variants (TIMING-ONLY unless marked exact):
   lgkm0     lgkm_g0 on the park kernel: wave group 0's fragment-read wait left to the compiler's
             waits at the consuming MFMAs, after the barrier (exact)
   prioload  the load phases at wave priority 2 (exact)
+  pstamps   the product kernel without the C park (exact), tagged s_memtime stamps by waves 0
+            and 4 after each barrier (0), after a load phase's DMA issue (1), after an MFMA
+            phase's last MFMA issue (2) and before each barrier (3): which side of a barrier waits
+            (--stamp-report prints the per-phase breakdown)
   stamps    the product kernel without the C park (exact) with an s_memtime stamp after every workgroup barrier by
             waves 0 and 4, kept in 8 KB of LDS beside the staging buffers (no vmcnt traffic) and
             written to the debug buffer at the end: [block][group][512] u64, entry 0 / 1 =
@@ -102,6 +106,32 @@ _STAMP_END = """  wait_vm<0>();  // never leave an LDS-DMA in flight past the en
       d[2] = (uint64_t)lab_i;
     }
   }"""
+
+_PSTAMP_DEF = """  const bool g1 = wr == 1;  // wave-uniform (wave came through readfirstlane)
+  // lab: tagged stamps (t << 4 | tag) by waves 0 and 4 in LDS past the staging buffers:
+  // 0 after a barrier, 1 after a load phase's DMA issue, 2 after an MFMA phase's last MFMA
+  // issue, 3 before a barrier (the phase's waits done)
+  int lab_i = 3;
+  const uint64_t lab_t0 = __builtin_amdgcn_s_memrealtime();
+  auto lab_stamp = [&](int tag) __attribute__((always_inline)) {
+    if ((wave & 3) == 0 && lab_i < 512) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      *(uint64_t*)(smem + 8 * UNIT + (wave >> 2) * 4096 + lab_i * 8) = (t << 4) | (uint64_t)tag;
+    }
+    ++lab_i;
+  };
+#undef T4_BAR
+#define T4_BAR()                         \\
+  do {                                   \\
+    __builtin_amdgcn_sched_barrier(0);   \\
+    lab_stamp(3);                        \\
+    __builtin_amdgcn_sched_barrier(0);   \\
+    __builtin_amdgcn_s_barrier();        \\
+    __builtin_amdgcn_sched_barrier(0);   \\
+    lab_stamp(0);                        \\
+    __builtin_amdgcn_sched_barrier(0);   \\
+  } while (0)"""
+_SB = "__builtin_amdgcn_sched_barrier(0);"
 
 PATCHES = {
     "base": [],
@@ -287,6 +317,27 @@ PATCHES = {
          "      if (g1) wait_vm<KIND == 2 ? WK2B : (KIND == 1 && !PAIRST ? 8 + NS : 8)>();\n"
          "      __builtin_amdgcn_s_setprio(0);  // lab\n      T4_BAR();\n"),
     ],
+    "pstamps": [  # stamps inside the phases (the C park gives way: LDS is full with it)
+        ("char smem[(DEFER && OUT != DT_F32 ? 10 : 8) * UNIT];", "char smem[8 * UNIT + 8192];"),
+        ("  constexpr bool PARK = PAIRST;", "  constexpr bool PARK = false;  // lab: stamps"),
+        ("  const bool g1 = wr == 1;  // wave-uniform (wave came through readfirstlane)",
+         _PSTAMP_DEF),
+        ("  wait_vm<0>();  // never leave an LDS-DMA in flight past the end of the workgroup",
+         _STAMP_END),
+        ("      stage(1, 1, BUF ^ 1, qa);\n      T4_LGKM0();\n",
+         f"      stage(1, 1, BUF ^ 1, qa);\n      {_SB}\n      lab_stamp(1);\n      {_SB}\n"
+         "      T4_LGKM0();\n"),
+        ("      stage(1, 0, BUF, qb);\n      T4_LGKM0();\n",
+         f"      stage(1, 0, BUF, qb);\n      {_SB}\n      lab_stamp(1);\n      {_SB}\n"
+         "      T4_LGKM0();\n"),
+        ("      mm(0, 0, Z);\n      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);\n",
+         f"      mm(0, 0, Z);\n      {_SB}\n      lab_stamp(2);\n      {_SB}\n"
+         "      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);\n"),
+        ("      if constexpr (KIND == 1) mm(1, 1, false);\n"
+         "      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);\n",
+         f"      if constexpr (KIND == 1) mm(1, 1, false);\n      {_SB}\n      lab_stamp(2);\n"
+         f"      {_SB}\n      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);\n"),
+    ],
     "stamps": [  # (the C-park area gives way to the stamps: LDS is full with it)
         ("char smem[(DEFER && OUT != DT_F32 ? 10 : 8) * UNIT];", "char smem[8 * UNIT + 8192];"),
         ("  constexpr bool PARK = PAIRST;", "  constexpr bool PARK = false;  // lab: stamps"),
@@ -457,7 +508,7 @@ def main() -> int:
         if a.vendor and not mx:
             fns["F.linear"] = lambda: torch.nn.functional.linear(A, W)
         exact = [v for v in fns if v in ("base", "ref", "stamps", "behind", "ring", "dmam", "dmam1",
-                                         "lgkm_g0", "relax", "hold", "hold0", "dmafirst", "dmamid", "noprio", "lgkm0", "prioload") or v.startswith(("aux", "stag"))]
+                                         "lgkm_g0", "relax", "hold", "hold0", "dmafirst", "dmamid", "noprio", "lgkm0", "prioload", "pstamps") or v.startswith(("aux", "stag"))]
         if exact:
             ref = A.float() @ W.float().t()
             bound = 2.0 ** -7 * float(ref.abs().max()) + K * 2.0 ** -12
@@ -493,6 +544,12 @@ def main() -> int:
         for k, ts in times.items():
             med = statistics.median(ts)
             print(f"  {k:10s} {med:.4f} / {min(ts):.4f}  ({flop / med / 1e9:.0f} TF)", flush=True)
+        if a.stamp_report and "pstamps" in fns:
+            dbg.zero_()
+            for _ in range(20):
+                fns["pstamps"]()
+            torch.cuda.synchronize()
+            pstamp_report(dbg.cpu())
         if a.stamp_report and "stamps" in fns:
             dbg.zero_()
             for _ in range(20):
@@ -502,6 +559,44 @@ def main() -> int:
         del A, W, out
         torch.cuda.empty_cache()
     return 0
+
+
+def pstamp_report(dbg, skip: int = 24) -> None:
+    """Phase breakdown of one pstamps launch: per wave group, the median over workgroups and
+    phases (stamps ``skip`` onwards: past the prologue) of each segment, in shader cycles. Load
+    phase: 0 -> 1 reads + DMA issued, 1 -> 3 its waits (lgkmcnt, vmcnt), 3 -> 0 barrier; MFMA
+    phase: 0 -> 2 MFMA issue, 2 -> 3 its waits, 3 -> 0 barrier."""
+    import statistics
+
+    import torch
+
+    d = dbg.view(torch.int64).view(-1, 2, 512)
+    nblk = int((d[:, 0, 2] > 0).sum())
+    names = {(0, 1): "load: issue", (1, 3): "load: waits", (0, 2): "mfma: issue",
+             (2, 3): "mfma: waits"}
+    for g in range(2):
+        seg = {}
+        for b in range(nblk):
+            n = min(int(d[b, g, 2]), 512)
+            raw = [int(x) for x in d[b, g, 3:n]]
+            st = [(x >> 4, x & 15) for x in raw]
+            kind = None
+            for i in range(max(skip, 1), len(st)):
+                (t0, a), (t1, c) = st[i - 1], st[i]
+                if a == 0 and c in (1, 2):
+                    kind = "load" if c == 1 else "mfma"
+                key = names.get((a, c))
+                if key is None and (a, c) == (3, 0) and kind:
+                    key = f"{kind}: barrier"
+                if key:
+                    seg.setdefault(key, []).append(t1 - t0)
+        print(f"group {g}: median cycles per segment over {nblk} workgroups", flush=True)
+        for key in ("load: issue", "load: waits", "load: barrier", "mfma: issue", "mfma: waits",
+                    "mfma: barrier"):
+            v = seg.get(key, [])
+            if v:
+                print(f"  {key:14s} {statistics.median(v):7.0f}  (p90 "
+                      f"{sorted(v)[int(0.9 * (len(v) - 1))]:.0f}, n {len(v)})", flush=True)
 
 
 def stamp_report(dbg, M: int, N: int, K: int, mx: bool) -> None:
