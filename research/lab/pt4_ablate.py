@@ -46,6 +46,12 @@ Variants (TIMING-ONLY unless marked exact):
   lgkm0     lgkm_g0 on the park kernel: wave group 0's fragment-read wait left to the compiler's
             waits at the consuming MFMAs, after the barrier (exact)
   prioload  the load phases at wave priority 2 (exact)
+  al2       TIMING-ONLY: every tile reads its A from one of two 256-row panels (L2-resident at
+            K = 1024), C unchanged; al2ns the same without C stores
+  krot      workgroup slot (blockIdx / 8) mod 4 starts each tile's K loop a quarter further in
+            (exact up to summation order): the CUs sharing an A panel stop fetching it in lockstep
+  mrot      tile (tm, tn) starts its K loop at K-tile tm mod nk (exact up to summation order):
+            the A-panel sharers stay in lockstep, concurrent M-blocks fetch different K offsets
   pstamps   the product kernel without the C park (exact), tagged s_memtime stamps by waves 0
             and 4 after each barrier (0), after a load phase's DMA issue (1), after an MFMA
             phase's last MFMA issue (2) and before each barrier (3): which side of a barrier waits
@@ -317,6 +323,36 @@ PATCHES = {
          "      if (g1) wait_vm<KIND == 2 ? WK2B : (KIND == 1 && !PAIRST ? 8 + NS : 8)>();\n"
          "      __builtin_amdgcn_s_setprio(0);  // lab\n      T4_BAR();\n"),
     ],
+    # TIMING-ONLY: every tile's A operand read from one of two 256-row panels (L2-resident at
+    # K = 1024 beside the 2 MB B), the C stores unchanged: what the A stream from HBM costs
+    "al2": [
+        ("rsA = __builtin_amdgcn_make_buffer_rsrc((void*)((APAN ? na : a_panel(nm0)) + (KS ? nko : 0)),",
+         "rsA = __builtin_amdgcn_make_buffer_rsrc((void*)((APAN ? na : a_panel(((nm0 >> 8) & 1) * 256)) + (KS ? nko : 0)),  // lab"),
+    ],
+    "al2ns": "al2+nostore",
+    # K-rotation (exact up to f32 summation order): workgroup slot (blockIdx / 8) mod 4 -- the
+    # four CUs that share an A panel on the flagship -- starts every tile's K loop a quarter of
+    # the way in, so one of them fetches each A K-tile from HBM and the others find it in L2
+    "krot": [
+        ("    const unsigned soff = (unsigned)(c.kt * ROWB);",
+         """    int lab_k = c.kt + (((int)blockIdx.x >> 3) & 3) * (nk >> 2);  // lab
+    if (lab_k >= nk) lab_k -= nk;
+    const unsigned soff = (unsigned)(lab_k * ROWB);"""),
+    ],
+    # K-rotation by M-block (exact up to summation order): tile (tm, tn) starts its K loop at
+    # K-tile tm mod nk, so the four CUs sharing an A panel stay in lockstep while concurrent
+    # M-blocks fetch different K offsets (rows lda apart: a power-of-two stride puts every
+    # concurrent A line of the chip at the same low address bits)
+    "mrot": [
+        ("  int src_tile = -1;\n", "  int src_tile = -1;\n  int lab_nrot = 0, lab_srot = 0;  // lab\n"),
+        ("    if constexpr (APAN) na = a_panel(m0);\n",
+         "    if constexpr (APAN) na = a_panel(m0);\n    lab_nrot = (int)((m0 >> 8) % nk);  // lab\n"),
+        ("      src_tile = c.ti;\n", "      src_tile = c.ti;\n      lab_srot = lab_nrot;  // lab\n"),
+        ("    const unsigned soff = (unsigned)(c.kt * ROWB);",
+         """    int lab_k = c.kt + lab_srot;  // lab
+    if (lab_k >= nk) lab_k -= nk;
+    const unsigned soff = (unsigned)(lab_k * ROWB);"""),
+    ],
     "pstamps": [  # stamps inside the phases (the C park gives way: LDS is full with it)
         ("char smem[(DEFER && OUT != DT_F32 ? 10 : 8) * UNIT];", "char smem[8 * UNIT + 8192];"),
         ("  constexpr bool PARK = PAIRST;", "  constexpr bool PARK = false;  // lab: stamps"),
@@ -368,6 +404,8 @@ PINNED = {
     "noprio": "8c58daa",    # r6_18, r6_19 (adopted for the 16-bit kernels)
     "lgkm0": "e2c6c5f",     # r6_21
     "prioload": "e2c6c5f",
+    "krot": "e2c6c5f",      # r6_24
+    "mrot": "e2c6c5f",      # r6_25
 }
 
 
@@ -508,7 +546,7 @@ def main() -> int:
         if a.vendor and not mx:
             fns["F.linear"] = lambda: torch.nn.functional.linear(A, W)
         exact = [v for v in fns if v in ("base", "ref", "stamps", "behind", "ring", "dmam", "dmam1",
-                                         "lgkm_g0", "relax", "hold", "hold0", "dmafirst", "dmamid", "noprio", "lgkm0", "prioload", "pstamps") or v.startswith(("aux", "stag"))]
+                                         "lgkm_g0", "relax", "hold", "hold0", "dmafirst", "dmamid", "noprio", "lgkm0", "prioload", "pstamps", "krot", "mrot") or v.startswith(("aux", "stag"))]
         if exact:
             ref = A.float() @ W.float().t()
             bound = 2.0 ** -7 * float(ref.abs().max()) + K * 2.0 ** -12
