@@ -52,6 +52,8 @@ Variants (TIMING-ONLY unless marked exact):
             (exact up to summation order): the CUs sharing an A panel stop fetching it in lockstep
   mrot      tile (tm, tn) starts its K loop at K-tile tm mod nk (exact up to summation order):
             the A-panel sharers stay in lockstep, concurrent M-blocks fetch different K offsets
+  nocross   the steady K-loop without the tile-crossing test in stage() (exact): all of a tile's
+            loop iterations but the last stage K-tiles of that tile
   pstamps   the product kernel without the C park (exact), tagged s_memtime stamps by waves 0
             and 4 after each barrier (0), after a load phase's DMA issue (1), after an MFMA
             phase's last MFMA issue (2) and before each barrier (3): which side of a barrier waits
@@ -223,9 +225,9 @@ PATCHES = {
     # where the steady K-tile's time goes (TIMING-ONLY, wrong results): no operand DMA in the
     # iterations (the prologue's stays), no fragment reads, no MFMAs (operands kept alive)
     "nodma": [
-        ("      stage(0, 1, BUF ^ 1, qa);\n      stage(1, 1, BUF ^ 1, qa);\n      T4_LGKM0();\n"
+        ("      stage_ab(same_tag, 1, BUF ^ 1, qa);\n      T4_LGKM0();\n"
          "      if constexpr (PARK", "      T4_LGKM0();\n      if constexpr (PARK"),
-        ("      stage(0, 0, BUF, qb);\n      stage(1, 0, BUF, qb);\n      T4_LGKM0();\n"
+        ("      stage_ab(same_tag, 0, BUF, qb);\n      T4_LGKM0();\n"
          "      if constexpr (PARK", "      T4_LGKM0();\n      if constexpr (PARK"),
     ],
     "noread": [
@@ -353,6 +355,70 @@ PATCHES = {
     if (lab_k >= nk) lab_k -= nk;
     const unsigned soff = (unsigned)(lab_k * ROWB);"""),
     ],
+    # the steady K-loop without the tile-crossing check (exact): every iteration but the last of
+    # a tile's loop stages K-tiles of the same tile, so its stage() skips the descriptor rebuild
+    # test (8 s_cselect per load phase) and its cursor advance is ++kt
+    "nocross": [
+        ("  };\n  const int frow = lane & 15, fq = lane >> 4, sw = (frow >> 1) & 7;\n",
+         """  };
+  auto stage_nc = [&](int X, int q, int buf, Cur c) __attribute__((always_inline)) {  // lab
+    const unsigned* off = X == 0 ? offA[q] : offB[q];
+    char* dst = smem + uoff(X, buf, q) + wave * 16 * ROWB;
+    const unsigned soff = (unsigned)(c.kt * ROWB);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(X == 0 ? rsA : rsB, (LDS_AS void*)dst, 16, off[0],
+                                             soff, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(X == 0 ? rsA : rsB, (LDS_AS void*)(dst + 8 * ROWB),
+                                             16, off[1], soff, 0, 0);
+  };
+  const int frow = lane & 15, fq = lane >> 4, sw = (frow >> 1) & 7;
+"""),
+        ("  auto iter = [&](auto bufc, auto kind_tag) __attribute__((always_inline)) {\n",
+         "  auto iter = [&](auto bufc, auto kind_tag, auto nc_tag) __attribute__((always_inline)) {\n"
+         "    constexpr bool NC = decltype(nc_tag)::value;  // lab\n"),
+        ("      stage(0, 1, BUF ^ 1, qa);\n      stage(1, 1, BUF ^ 1, qa);\n      T4_LGKM0();\n"
+         "      if constexpr (PARK && KIND == 2) park_store(0, pv);",
+         """      if constexpr (NC) {  // lab
+        stage_nc(0, 1, BUF ^ 1, qa);
+        stage_nc(1, 1, BUF ^ 1, qa);
+      } else {
+        stage(0, 1, BUF ^ 1, qa);
+        stage(1, 1, BUF ^ 1, qa);
+      }
+      T4_LGKM0();
+      if constexpr (PARK && KIND == 2) park_store(0, pv);"""),
+        ("      stage(0, 0, BUF, qb);\n      stage(1, 0, BUF, qb);\n      T4_LGKM0();\n"
+         "      if constexpr (PARK && KIND == 2) park_store(2, pv);",
+         """      if constexpr (NC) {  // lab
+        stage_nc(0, 0, BUF, qb);
+        stage_nc(1, 0, BUF, qb);
+      } else {
+        stage(0, 0, BUF, qb);
+        stage(1, 0, BUF, qb);
+      }
+      T4_LGKM0();
+      if constexpr (PARK && KIND == 2) park_store(2, pv);"""),
+        ("    qa = qb;\n    adv(qb);\n  };\n",
+         "    qa = qb;\n    if constexpr (NC) ++qb.kt; else adv(qb);  // lab\n  };\n"),
+        ("""    iter(B0{}, first_kind);  // K-tile 0
+    for (int t = 1; t + 2 < nk; t += 2) {
+      iter(B1{}, K0{});
+      iter(B0{}, K0{});
+    }
+    iter(B1{}, last_kind);  // K-tile nk - 1 (nk even)""",
+         """    using NCT = std::true_type;  // lab
+    using NCF = std::false_type;
+    iter(B0{}, first_kind, NCF{});  // K-tile 0
+    int t = 1;
+    for (; t + 4 < nk; t += 2) {  // qb <= K-tile t + 3 <= nk - 2: the same tile
+      iter(B1{}, K0{}, NCT{});
+      iter(B0{}, K0{}, NCT{});
+    }
+    if (t + 2 < nk) {
+      iter(B1{}, K0{}, NCF{});
+      iter(B0{}, K0{}, NCF{});
+    }
+    iter(B1{}, last_kind, NCF{});  // K-tile nk - 1 (nk even)"""),
+    ],
     "pstamps": [  # stamps inside the phases (the C park gives way: LDS is full with it)
         ("char smem[(DEFER && OUT != DT_F32 ? 10 : 8) * UNIT];", "char smem[8 * UNIT + 8192];"),
         ("  constexpr bool PARK = PAIRST;", "  constexpr bool PARK = false;  // lab: stamps"),
@@ -360,11 +426,11 @@ PATCHES = {
          _PSTAMP_DEF),
         ("  wait_vm<0>();  // never leave an LDS-DMA in flight past the end of the workgroup",
          _STAMP_END),
-        ("      stage(1, 1, BUF ^ 1, qa);\n      T4_LGKM0();\n",
-         f"      stage(1, 1, BUF ^ 1, qa);\n      {_SB}\n      lab_stamp(1);\n      {_SB}\n"
+        ("      stage_ab(same_tag, 1, BUF ^ 1, qa);\n      T4_LGKM0();\n",
+         f"      stage_ab(same_tag, 1, BUF ^ 1, qa);\n      {_SB}\n      lab_stamp(1);\n      {_SB}\n"
          "      T4_LGKM0();\n"),
-        ("      stage(1, 0, BUF, qb);\n      T4_LGKM0();\n",
-         f"      stage(1, 0, BUF, qb);\n      {_SB}\n      lab_stamp(1);\n      {_SB}\n"
+        ("      stage_ab(same_tag, 0, BUF, qb);\n      T4_LGKM0();\n",
+         f"      stage_ab(same_tag, 0, BUF, qb);\n      {_SB}\n      lab_stamp(1);\n      {_SB}\n"
          "      T4_LGKM0();\n"),
         ("      mm(0, 0, Z);\n      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);\n",
          f"      mm(0, 0, Z);\n      {_SB}\n      lab_stamp(2);\n      {_SB}\n"
@@ -406,6 +472,7 @@ PINNED = {
     "prioload": "e2c6c5f",
     "krot": "e2c6c5f",      # r6_24
     "mrot": "e2c6c5f",      # r6_25
+    "nocross": "e2c6c5f",   # r6_28 (adopted: stage_ab)
 }
 
 
@@ -546,7 +613,7 @@ def main() -> int:
         if a.vendor and not mx:
             fns["F.linear"] = lambda: torch.nn.functional.linear(A, W)
         exact = [v for v in fns if v in ("base", "ref", "stamps", "behind", "ring", "dmam", "dmam1",
-                                         "lgkm_g0", "relax", "hold", "hold0", "dmafirst", "dmamid", "noprio", "lgkm0", "prioload", "pstamps", "krot", "mrot") or v.startswith(("aux", "stag"))]
+                                         "lgkm_g0", "relax", "hold", "hold0", "dmafirst", "dmamid", "noprio", "lgkm0", "prioload", "pstamps", "krot", "mrot", "nocross") or v.startswith(("aux", "stag"))]
         if exact:
             ref = A.float() @ W.float().t()
             bound = 2.0 ** -7 * float(ref.abs().max()) + K * 2.0 ** -12
