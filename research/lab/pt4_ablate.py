@@ -54,6 +54,8 @@ Variants (TIMING-ONLY unless marked exact):
             the A-panel sharers stay in lockstep, concurrent M-blocks fetch different K offsets
   nocross   the steady K-loop without the tile-crossing test in stage() (exact): all of a tile's
             loop iterations but the last stage K-tiles of that tile
+  g1split   the body instantiated once per wave group (exact): the per-phase `if (g1)` branches
+            around the vmcnt waits fold away
   pstamps   the product kernel without the C park (exact), tagged s_memtime stamps by waves 0
             and 4 after each barrier (0), after a load phase's DMA issue (1), after an MFMA
             phase's last MFMA issue (2) and before each barrier (3): which side of a barrier waits
@@ -419,6 +421,17 @@ PATCHES = {
     }
     iter(B1{}, last_kind, NCF{});  // K-tile nk - 1 (nk even)"""),
     ],
+    # the wave groups' code split at compile time (exact): the body after the prologue's
+    # setup is instantiated once per wave group, so `if (g1)` around the vmcnt waits folds away
+    # (no branch per phase)
+    "g1split": [
+        ("  const bool g1 = wr == 1;  // wave-uniform (wave came through readfirstlane)\n",
+         "  auto lab_body = [&](auto g1_tag) __attribute__((always_inline)) {  // lab\n"
+         "  constexpr bool g1 = decltype(g1_tag)::value;\n"),
+        ("#undef T4_BAR\n#undef T4_LGKM0\n  wait_vm<0>();",
+         "  };  // lab\n  if (wr == 1)\n    lab_body(std::true_type{});\n  else\n"
+         "    lab_body(std::false_type{});\n#undef T4_BAR\n#undef T4_LGKM0\n  wait_vm<0>();"),
+    ],
     "pstamps": [  # stamps inside the phases (the C park gives way: LDS is full with it)
         ("char smem[(DEFER && OUT != DT_F32 ? 10 : 8) * UNIT];", "char smem[8 * UNIT + 8192];"),
         ("  constexpr bool PARK = PAIRST;", "  constexpr bool PARK = false;  // lab: stamps"),
@@ -613,7 +626,7 @@ def main() -> int:
         if a.vendor and not mx:
             fns["F.linear"] = lambda: torch.nn.functional.linear(A, W)
         exact = [v for v in fns if v in ("base", "ref", "stamps", "behind", "ring", "dmam", "dmam1",
-                                         "lgkm_g0", "relax", "hold", "hold0", "dmafirst", "dmamid", "noprio", "lgkm0", "prioload", "pstamps", "krot", "mrot", "nocross") or v.startswith(("aux", "stag"))]
+                                         "lgkm_g0", "relax", "hold", "hold0", "dmafirst", "dmamid", "noprio", "lgkm0", "prioload", "pstamps", "krot", "mrot", "nocross", "g1split") or v.startswith(("aux", "stag"))]
         if exact:
             ref = A.float() @ W.float().t()
             bound = 2.0 ** -7 * float(ref.abs().max()) + K * 2.0 ** -12
