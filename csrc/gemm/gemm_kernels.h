@@ -1397,10 +1397,12 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   // first K-tile (DEFER: no deferred product, no stores counted); BUF: the buffer this K-tile
   // reads. vmcnt counts keep exactly the DMA (and C stores) issued after the units the next phase
   // reads in flight; stores count in issue order with the DMA.
-  // SAME (same_tag): qa and qb stay inside the current tile (stage_ab, cursor advance)
-  auto iter = [&](auto bufc, auto kind_tag, auto same_tag) __attribute__((always_inline)) {
+  // SAME (same_tag): qa and qb stay inside the current tile (stage_ab, cursor advance); G1: this
+  // wave's group, a compile-time tag where the tile loop is split per group (SPLIT, below)
+  auto iter = [&](auto bufc, auto kind_tag, auto same_tag, auto g1v) __attribute__((always_inline)) {
     constexpr int KIND = decltype(kind_tag)::value;
     constexpr bool SAME = decltype(same_tag)::value;
+    const bool g1 = g1v;
     constexpr int BUF = decltype(bufc)::value;
     constexpr bool Z = KIND == 2 || KIND == 4;
     if constexpr (DEFER) {
@@ -1520,7 +1522,7 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
   using B1 = std::integral_constant<int, 1>;
   using K0 = std::integral_constant<int, 0>;
   using K1 = std::integral_constant<int, 1>;
-  auto tile_body = [&](auto first_kind, auto last_kind) __attribute__((always_inline)) {
+  auto tile_body = [&](auto first_kind, auto last_kind, auto g1v) __attribute__((always_inline)) {
     cm0 = nm0;  // this tile (C rows: physical, grouped C rows keep a tile contiguous)
     cn0 = nn0;
     if constexpr (KS) ccs = ncs;
@@ -1528,21 +1530,36 @@ __global__ __launch_bounds__(512) void gemm_tn_pt4_kernel(const GemmArgs p) {
     if (ti + 1 < my_tiles) origin(ti + 1, nm0, nn0);
     using InTile = std::true_type;
     using Crosses = std::false_type;
-    iter(B0{}, first_kind, Crosses{});  // K-tile 0
+    iter(B0{}, first_kind, Crosses{}, g1v);  // K-tile 0
     int t = 1;
     for (; t + 4 < nk; t += 2) {  // qb <= K-tile t + 3 <= nk - 2: this tile
-      iter(B1{}, K0{}, InTile{});
-      iter(B0{}, K0{}, InTile{});
+      iter(B1{}, K0{}, InTile{}, g1v);
+      iter(B0{}, K0{}, InTile{}, g1v);
     }
     if (t + 2 < nk) {  // the last pair stages the next tile's first K-tile
-      iter(B1{}, K0{}, Crosses{});
-      iter(B0{}, K0{}, Crosses{});
+      iter(B1{}, K0{}, Crosses{}, g1v);
+      iter(B0{}, K0{}, Crosses{}, g1v);
     }
-    iter(B1{}, last_kind, Crosses{});  // K-tile nk - 1 (nk even)
+    iter(B1{}, last_kind, Crosses{}, g1v);  // K-tile nk - 1 (nk even)
   };
-  ti = 0;
-  tile_body(std::integral_constant<int, DEFER ? 4 : 0>{}, K1{});
-  for (ti = 1; ti < my_tiles; ++ti) tile_body(std::integral_constant<int, 2>{}, K1{});
+  auto tiles = [&](auto g1v) __attribute__((always_inline)) {
+    ti = 0;
+    tile_body(std::integral_constant<int, DEFER ? 4 : 0>{}, K1{}, g1v);
+    for (ti = 1; ti < my_tiles; ++ti) tile_body(std::integral_constant<int, 2>{}, K1{}, g1v);
+  };
+  // SPLIT: the tile loop instantiated once per wave group, so every `if (g1)` around a vmcnt
+  // wait folds away (no branch per phase): bf16 flagship -1.9 %, 8192^3 -1.7 %, K = 512 -4.1 %
+  // (profiles/r06/r6_30, r6_31). The MX, row-table (APAN), f32-output and gated forms spill
+  // with two copies of the loop (MX 72-76 bytes and 37-67 % slower, f32 C 8 bytes) and keep one
+  constexpr bool SPLIT = DEFER && !APAN && OUT != DT_F32 && !std::is_same<Mma, MmaMX>::value;
+  if constexpr (SPLIT) {
+    if (g1)
+      tiles(std::true_type{});
+    else
+      tiles(std::false_type{});
+  } else {
+    tiles(g1);
+  }
   if (!g1) T4_BAR();
   if constexpr (PARK) {  // the last tile's parked pairs
     u32x4_t pv[2];

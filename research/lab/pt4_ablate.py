@@ -486,6 +486,7 @@ PINNED = {
     "krot": "e2c6c5f",      # r6_24
     "mrot": "e2c6c5f",      # r6_25
     "nocross": "e2c6c5f",   # r6_28 (adopted: stage_ab)
+    "g1split": "cb084d4",   # r6_30 (adopted for the 16-bit flagship forms: SPLIT)
 }
 
 
