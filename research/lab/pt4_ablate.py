@@ -56,6 +56,8 @@ Variants (TIMING-ONLY unless marked exact):
             loop iterations but the last stage K-tiles of that tile
   g1split   the body instantiated once per wave group (exact): the per-phase `if (g1)` branches
             around the vmcnt waits fold away
+  m0share   the second 1 KB piece of each unit slice addressed through the DMA's instruction
+            offset (exact iff that offset also applies to the LDS address): half the M0 writes
   pstamps   the product kernel without the C park (exact), tagged s_memtime stamps by waves 0
             and 4 after each barrier (0), after a load phase's DMA issue (1), after an MFMA
             phase's last MFMA issue (2) and before each barrier (3): which side of a barrier waits
@@ -432,6 +434,19 @@ PATCHES = {
          "  };  // lab\n  if (wr == 1)\n    lab_body(std::true_type{});\n  else\n"
          "    lab_body(std::false_type{});\n#undef T4_BAR\n#undef T4_LGKM0\n  wait_vm<0>();"),
     ],
+    # one M0 per unit (exact if the DMA's instruction offset also offsets its LDS address): the
+    # second 1 KB piece of a wave's unit slice takes the first's LDS base with offset:1024 and a
+    # voffset 1024 lower, so the compiler needs 2 M0 writes (and s_nops) per load phase, not 4
+    "m0share": [
+        ("      offB[q][i] = (unsigned)(lc * p.ldb * esz + ch);\n",
+         "      offB[q][i] = (unsigned)(lc * p.ldb * esz + ch);\n"
+         "      if (i == 1) {  // lab: rows 8.. of the slice are >= 8 rows in, so >= 1024 bytes\n"
+         "        offA[q][i] -= 1024u;\n        offB[q][i] -= 1024u;\n      }\n"),
+        ("""    __builtin_amdgcn_raw_ptr_buffer_load_lds(X == 0 ? rsA : rsB, (LDS_AS void*)(dst + 8 * ROWB),
+                                             16, off[1], soff, 0, 0);""",
+         """    __builtin_amdgcn_raw_ptr_buffer_load_lds(X == 0 ? rsA : rsB, (LDS_AS void*)dst,  // lab
+                                             16, off[1], soff, 8 * ROWB, 0);"""),
+    ],
     "pstamps": [  # stamps inside the phases (the C park gives way: LDS is full with it)
         ("char smem[(DEFER && OUT != DT_F32 ? 10 : 8) * UNIT];", "char smem[8 * UNIT + 8192];"),
         ("  constexpr bool PARK = PAIRST;", "  constexpr bool PARK = false;  // lab: stamps"),
@@ -627,7 +642,7 @@ def main() -> int:
         if a.vendor and not mx:
             fns["F.linear"] = lambda: torch.nn.functional.linear(A, W)
         exact = [v for v in fns if v in ("base", "ref", "stamps", "behind", "ring", "dmam", "dmam1",
-                                         "lgkm_g0", "relax", "hold", "hold0", "dmafirst", "dmamid", "noprio", "lgkm0", "prioload", "pstamps", "krot", "mrot", "nocross", "g1split") or v.startswith(("aux", "stag"))]
+                                         "lgkm_g0", "relax", "hold", "hold0", "dmafirst", "dmamid", "noprio", "lgkm0", "prioload", "pstamps", "krot", "mrot", "nocross", "g1split", "m0share") or v.startswith(("aux", "stag"))]
         if exact:
             ref = A.float() @ W.float().t()
             bound = 2.0 ** -7 * float(ref.abs().max()) + K * 2.0 ** -12
