@@ -58,6 +58,8 @@ Variants (TIMING-ONLY unless marked exact):
             around the vmcnt waits fold away
   m0share   the second 1 KB piece of each unit slice addressed through the DMA's instruction
             offset (exact iff that offset also applies to the LDS address): half the M0 writes
+  waitall   steady K-tiles wait on vmcnt in both wave groups at all four sites (exact): no
+            per-phase branch, no second copy of the loop
   pstamps   the product kernel without the C park (exact), tagged s_memtime stamps by waves 0
             and 4 after each barrier (0), after a load phase's DMA issue (1), after an MFMA
             phase's last MFMA issue (2) and before each barrier (3): which side of a barrier waits
@@ -447,6 +449,19 @@ PATCHES = {
          """    __builtin_amdgcn_raw_ptr_buffer_load_lds(X == 0 ? rsA : rsB, (LDS_AS void*)dst,  // lab
                                              16, off[1], soff, 8 * ROWB, 0);"""),
     ],
+    # branch-free steady K-tiles (exact): in KIND 0 iterations both wave groups wait at all four
+    # vmcnt sites (same count 8: group 1 gains no-op waits, group 0 waits for its DMA one interval
+    # earlier), so the per-phase `if (g1)` branch disappears without a second copy of the loop
+    "waitall": [
+        ("      if (g1) wait_vm<KIND == 2 ? WK2A : 8>();",
+         "      if (KIND == 0 || g1) wait_vm<KIND == 2 ? WK2A : 8>();  // lab"),
+        ("      if (!g1) wait_vm<KIND == 2 ? WK2A : (KIND == 1 && !PAIRST ? 8 + NS : 8)>();",
+         "      if (KIND == 0 || !g1) wait_vm<KIND == 2 ? WK2A : (KIND == 1 && !PAIRST ? 8 + NS : 8)>();  // lab"),
+        ("      if (g1) wait_vm<KIND == 2 ? WK2B : (KIND == 1 && !PAIRST ? 8 + NS : 8)>();",
+         "      if (KIND == 0 || g1) wait_vm<KIND == 2 ? WK2B : (KIND == 1 && !PAIRST ? 8 + NS : 8)>();  // lab"),
+        ("      if (!g1) wait_vm<KIND == 1 ? 8 + 4 * NS - NP : (KIND == 2 ? WK2B : 8)>();",
+         "      if (KIND == 0 || !g1) wait_vm<KIND == 1 ? 8 + 4 * NS - NP : (KIND == 2 ? WK2B : 8)>();  // lab"),
+    ],
     "pstamps": [  # stamps inside the phases (the C park gives way: LDS is full with it)
         ("char smem[(DEFER && OUT != DT_F32 ? 10 : 8) * UNIT];", "char smem[8 * UNIT + 8192];"),
         ("  constexpr bool PARK = PAIRST;", "  constexpr bool PARK = false;  // lab: stamps"),
@@ -502,6 +517,8 @@ PINNED = {
     "mrot": "e2c6c5f",      # r6_25
     "nocross": "e2c6c5f",   # r6_28 (adopted: stage_ab)
     "g1split": "cb084d4",   # r6_30 (adopted for the 16-bit flagship forms: SPLIT)
+    "m0share": "fc1ce0f",   # r6_32 (exact, flat)
+    "waitall": "fc1ce0f",   # r6_33 (MX spills)
 }
 
 
@@ -642,7 +659,7 @@ def main() -> int:
         if a.vendor and not mx:
             fns["F.linear"] = lambda: torch.nn.functional.linear(A, W)
         exact = [v for v in fns if v in ("base", "ref", "stamps", "behind", "ring", "dmam", "dmam1",
-                                         "lgkm_g0", "relax", "hold", "hold0", "dmafirst", "dmamid", "noprio", "lgkm0", "prioload", "pstamps", "krot", "mrot", "nocross", "g1split", "m0share") or v.startswith(("aux", "stag"))]
+                                         "lgkm_g0", "relax", "hold", "hold0", "dmafirst", "dmamid", "noprio", "lgkm0", "prioload", "pstamps", "krot", "mrot", "nocross", "g1split", "m0share", "waitall") or v.startswith(("aux", "stag"))]
         if exact:
             ref = A.float() @ W.float().t()
             bound = 2.0 ** -7 * float(ref.abs().max()) + K * 2.0 ** -12
