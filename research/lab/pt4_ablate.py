@@ -60,8 +60,6 @@ Variants (TIMING-ONLY unless marked exact):
             offset (exact iff that offset also applies to the LDS address): half the M0 writes
   waitall   steady K-tiles wait on vmcnt in both wave groups at all four sites (exact): no
             per-phase branch, no second copy of the loop
-  ilv       the tile end's packing and stores of C rows mq = 0 interleaved with the last
-            K-tile's remaining MFMAs (2 VALU per MFMA, a store every 4) (exact)
   pstamps   the product kernel without the C park (exact), tagged s_memtime stamps by waves 0
             and 4 after each barrier (0), after a load phase's DMA issue (1), after an MFMA
             phase's last MFMA issue (2) and before each barrier (3): which side of a barrier waits
@@ -464,54 +462,6 @@ PATCHES = {
         ("      if (!g1) wait_vm<KIND == 1 ? 8 + 4 * NS - NP : (KIND == 2 ? WK2B : 8)>();",
          "      if (KIND == 0 || !g1) wait_vm<KIND == 1 ? 8 + 4 * NS - NP : (KIND == 2 ? WK2B : 8)>();  // lab"),
     ],
-    # tile end: the packing (cvt + DPP) and stores of C rows mq = 0 interleaved with the last
-    # K-tile's mm(1, 0) / mm(1, 1) MFMAs (2 VALU per MFMA, a store every 4) instead of issued as a
-    # burst between them (exact)
-    "ilv": [
-        ("  auto store_pair = [&](int mq) __attribute__((always_inline)) {",
-         """  auto store_pair0_nb = [&]() __attribute__((always_inline)) {  // lab: no barriers
-#pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      u32x4_t x = pack8<OUT>(acc[f][0], acc[f][1]), y = pack8<OUT>(acc[f][2], acc[f][3]);
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        const int t = (int)x[d];
-        x[d] = (unsigned)__builtin_amdgcn_update_dpp(t, (int)y[d], 0x128, 0xF, 0xC, false);
-        y[d] = (unsigned)__builtin_amdgcn_update_dpp((int)y[d], t, 0x128, 0xF, 0x3, false);
-      }
-      const int64_t prow = cm0 + f * 16;
-      const unsigned so = (unsigned)((prow * p.ldc + cn0) * OSZ) + (KS ? ccs : 0u);
-      const unsigned so8 = so + (unsigned)(8 * p.ldc * OSZ);
-      __builtin_amdgcn_raw_buffer_store_b128(x, crc, c_pair, so, CPOL);
-      __builtin_amdgcn_raw_buffer_store_b128(y, crc, c_pair, so8, CPOL);
-    }
-  };
-  auto store_pair = [&](int mq) __attribute__((always_inline)) {"""),
-        ("""      if constexpr (KIND == 1 && PAIRST) store_pair(0);
-      mm(1, 0, Z);
-      if constexpr (KIND == 1) mm(1, 1, false);
-""",
-         """      if constexpr (KIND == 1 && PAIRST) {  // lab
-        __builtin_amdgcn_sched_barrier(0);
-        store_pair0_nb();
-        mm(1, 0, Z);
-        mm(1, 1, false);
-#pragma unroll
-        for (int g = 0; g < 8; ++g) {
-#pragma unroll
-          for (int m = 0; m < 4; ++m) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-          }
-          __builtin_amdgcn_sched_group_barrier(0x040, 1, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      } else {
-        mm(1, 0, Z);
-        if constexpr (KIND == 1) mm(1, 1, false);
-      }
-"""),
-    ],
     "pstamps": [  # stamps inside the phases (the C park gives way: LDS is full with it)
         ("char smem[(DEFER && OUT != DT_F32 ? 10 : 8) * UNIT];", "char smem[8 * UNIT + 8192];"),
         ("  constexpr bool PARK = PAIRST;", "  constexpr bool PARK = false;  // lab: stamps"),
@@ -709,7 +659,7 @@ def main() -> int:
         if a.vendor and not mx:
             fns["F.linear"] = lambda: torch.nn.functional.linear(A, W)
         exact = [v for v in fns if v in ("base", "ref", "stamps", "behind", "ring", "dmam", "dmam1",
-                                         "lgkm_g0", "relax", "hold", "hold0", "dmafirst", "dmamid", "noprio", "lgkm0", "prioload", "pstamps", "krot", "mrot", "nocross", "g1split", "m0share", "waitall", "ilv") or v.startswith(("aux", "stag"))]
+                                         "lgkm_g0", "relax", "hold", "hold0", "dmafirst", "dmamid", "noprio", "lgkm0", "prioload", "pstamps", "krot", "mrot", "nocross", "g1split", "m0share", "waitall") or v.startswith(("aux", "stag"))]
         if exact:
             ref = A.float() @ W.float().t()
             bound = 2.0 ** -7 * float(ref.abs().max()) + K * 2.0 ** -12
