@@ -60,6 +60,7 @@ Variants (TIMING-ONLY unless marked exact):
             offset (exact iff that offset also applies to the LDS address): half the M0 writes
   waitall   steady K-tiles wait on vmcnt in both wave groups at all four sites (exact): no
             per-phase branch, no second copy of the loop
+  unroll2   the steady loop unrolled by two (exact)
   pstamps   the product kernel without the C park (exact), tagged s_memtime stamps by waves 0
             and 4 after each barrier (0), after a load phase's DMA issue (1), after an MFMA
             phase's last MFMA issue (2) and before each barrier (3): which side of a barrier waits
@@ -462,6 +463,12 @@ PATCHES = {
         ("      if (!g1) wait_vm<KIND == 1 ? 8 + 4 * NS - NP : (KIND == 2 ? WK2B : 8)>();",
          "      if (KIND == 0 || !g1) wait_vm<KIND == 1 ? 8 + 4 * NS - NP : (KIND == 2 ? WK2B : 8)>();  // lab"),
     ],
+    # the steady loop unrolled by two (4 K-tiles per trip: half the loop-control instructions
+    # and back branches) (exact)
+    "unroll2": [
+        ("    for (; t + 4 < nk; t += 2) {  // qb <= K-tile t + 3 <= nk - 2: this tile\n",
+         "#pragma unroll 2\n    for (; t + 4 < nk; t += 2) {  // lab\n"),
+    ],
     "pstamps": [  # stamps inside the phases (the C park gives way: LDS is full with it)
         ("char smem[(DEFER && OUT != DT_F32 ? 10 : 8) * UNIT];", "char smem[8 * UNIT + 8192];"),
         ("  constexpr bool PARK = PAIRST;", "  constexpr bool PARK = false;  // lab: stamps"),
@@ -659,7 +666,7 @@ def main() -> int:
         if a.vendor and not mx:
             fns["F.linear"] = lambda: torch.nn.functional.linear(A, W)
         exact = [v for v in fns if v in ("base", "ref", "stamps", "behind", "ring", "dmam", "dmam1",
-                                         "lgkm_g0", "relax", "hold", "hold0", "dmafirst", "dmamid", "noprio", "lgkm0", "prioload", "pstamps", "krot", "mrot", "nocross", "g1split", "m0share", "waitall") or v.startswith(("aux", "stag"))]
+                                         "lgkm_g0", "relax", "hold", "hold0", "dmafirst", "dmamid", "noprio", "lgkm0", "prioload", "pstamps", "krot", "mrot", "nocross", "g1split", "m0share", "waitall", "unroll2") or v.startswith(("aux", "stag"))]
         if exact:
             ref = A.float() @ W.float().t()
             bound = 2.0 ** -7 * float(ref.abs().max()) + K * 2.0 ** -12
