@@ -526,6 +526,7 @@ PINNED = {
     "g1split": "cb084d4",   # r6_30 (adopted for the 16-bit flagship forms: SPLIT)
     "m0share": "fc1ce0f",   # r6_32 (exact, flat)
     "waitall": "fc1ce0f",   # r6_33 (MX spills)
+    "unroll2": "d2e1ff0",   # r6_38 (flat)
 }
 
 
